@@ -1,0 +1,269 @@
+"""TEST INFRASTRUCTURE — ctypes wrapper over oracle/build/liboracle.so, the CPU
+restatement of the reference algorithms (see poa_oracle.cpp / aligner_oracle.cpp
+headers).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+may import this module; the product path never does.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+MAX_EDGES = 50
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _declare(_lib)
+    return _lib
+
+
+def _p(arr):
+    return arr.ctypes.data_as(C.c_void_p) if arr is not None else None
+
+
+def _declare(L):
+    vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
+    L.oracle_poa_window.restype = C.c_int
+    L.oracle_poa_window.argtypes = [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
+                                    vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.oracle_poa_batch.restype = C.c_int
+    L.oracle_poa_batch.argtypes = [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
+                                   vp, vp, vp, vp, vp]
+    L.oracle_topsort.restype = None
+    L.oracle_topsort.argtypes = [i32, vp, vp, vp, vp]
+    L.oracle_nw.restype = C.c_int
+    L.oracle_nw.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]
+    L.oracle_add_alignment.restype = C.c_int
+    L.oracle_add_alignment.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp]
+    L.oracle_consensus_raw.restype = C.c_int
+    L.oracle_consensus_raw.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp]
+    if hasattr(L, "oracle_align"):
+        L.oracle_align.restype = C.c_int
+        L.oracle_align.argtypes = [C.c_char_p, i32, C.c_char_p, i32, i32, vp]
+    del i64
+
+
+class WindowResult:
+    def __init__(self, status, consensus, coverage, msa, cells, band_cells, final_nodes, graph):
+        self.status = status
+        self.consensus = consensus
+        self.coverage = coverage
+        self.msa = msa
+        self.cells = cells
+        self.band_cells = band_cells
+        self.final_nodes = final_nodes
+        self.graph = graph
+
+
+def poa_window(reads, weights=None, gap=-8, mismatch=-6, match=8, banded=False, band_width=256,
+               score_bits=16, msa=False, max_nodes=None, max_consensus=None, max_seqs=None,
+               want_graph=False):
+    """Run one window through the restatement; reads are bytes/str."""
+    reads = [r.encode() if isinstance(r, str) else bytes(r) for r in reads]
+    max_len = max([len(r) for r in reads] + [1])
+    if max_nodes is None:
+        max_nodes = ((3 * max_len + 3) // 4) * 4 if not banded else ((4 * max_len + 3) // 4) * 4
+    if max_consensus is None:
+        max_consensus = 2 * max_len
+    if max_seqs is None:
+        max_seqs = len(reads)
+    seqs = np.frombuffer(b"".join(reads) + b"\0" * 16, dtype=np.uint8).copy()
+    lens = np.array([len(r) for r in reads], dtype=np.int32)
+    if weights is None:
+        wts = np.ones(max(len(seqs), 1), dtype=np.int8)
+    else:
+        wts = np.concatenate([np.asarray(w, dtype=np.int8) for w in weights] + [np.zeros(16, np.int8)])
+    cons = np.zeros(max_consensus + 1, dtype=np.uint8)
+    cov = np.zeros(max_consensus + 1, dtype=np.uint16)
+    clen = np.zeros(1, dtype=np.int32)
+    msa_buf = np.zeros(max(len(reads), 1) * max_consensus, dtype=np.uint8) if msa else None
+    cells = np.zeros(2, dtype=np.int64)
+    fnodes = np.zeros(1, dtype=np.int32)
+    gb = gc = ge = gw = None
+    if want_graph:
+        gb = np.zeros(max_nodes, dtype=np.uint8)
+        gc = np.zeros(max_nodes, dtype=np.int32)
+        ge = np.zeros(max_nodes * MAX_EDGES, dtype=np.int32)
+        gw = np.zeros(max_nodes * MAX_EDGES, dtype=np.int32)
+    st = lib().oracle_poa_window(_p(seqs), _p(lens), _p(wts), len(reads), gap, mismatch, match, int(banded),
+                                 band_width, score_bits, int(msa), max_nodes, max_consensus, max_seqs,
+                                 _p(cons), _p(cov), _p(clen), _p(msa_buf), _p(cells), _p(fnodes),
+                                 _p(gb), _p(gc), _p(ge), _p(gw))
+    n = int(clen[0])
+    consensus = bytes(cons[:n]).decode() if st == 0 and not msa else ""
+    coverage = cov[:n].tolist() if st == 0 and not msa else []
+    rows = None
+    if msa and st == 0:
+        rows = []
+        for s in range(len(reads)):
+            row = bytes(msa_buf[s * max_consensus:(s + 1) * max_consensus])
+            rows.append(row.split(b"\0", 1)[0].decode())
+    graph = None
+    if want_graph:
+        nn = int(fnodes[0])
+        graph = {"bases": bytes(gb[:nn]).decode(errors="replace"),
+                 "in": [[(int(ge[v * MAX_EDGES + e]), int(gw[v * MAX_EDGES + e])) for e in range(int(gc[v]))]
+                        for v in range(nn)]}
+    return WindowResult(st, consensus, coverage, rows, int(cells[0]), int(cells[1]), int(fnodes[0]), graph)
+
+
+def poa_batch(windows, nthreads=0, gap=-8, mismatch=-6, match=8, banded=False, band_width=256, score_bits=16,
+              max_nodes=None, max_consensus=None, max_seqs=None):
+    """Run many windows (list of lists of bytes) on all host cores (OpenMP).
+    Returns (consensus list, status array, cells array, threads used)."""
+    flat = []
+    lens = []
+    first = []
+    nseq = []
+    for w in windows:
+        first.append(len(lens))
+        nseq.append(len(w))
+        for r in w:
+            r = r.encode() if isinstance(r, str) else bytes(r)
+            flat.append(r)
+            lens.append(len(r))
+    max_len = max(lens + [1])
+    if max_nodes is None:
+        max_nodes = ((3 * max_len + 3) // 4) * 4
+    if max_consensus is None:
+        max_consensus = 2 * max_len
+    if max_seqs is None:
+        max_seqs = max(nseq + [1])
+    seqs = np.frombuffer(b"".join(flat) + b"\0" * 16, dtype=np.uint8).copy()
+    lens_a = np.array(lens, dtype=np.int32)
+    offs = np.zeros(len(lens), dtype=np.int64)
+    if len(lens) > 1:
+        offs[1:] = np.cumsum(lens_a[:-1])
+    first_a = np.array(first, dtype=np.int32)
+    nseq_a = np.array(nseq, dtype=np.int32)
+    nw = len(windows)
+    cons = np.zeros(nw * max_consensus, dtype=np.uint8)
+    cov = np.zeros(nw * max_consensus, dtype=np.uint16)
+    clen = np.zeros(nw, dtype=np.int32)
+    status = np.zeros(nw, dtype=np.uint8)
+    cells = np.zeros(nw, dtype=np.int64)
+    used = lib().oracle_poa_batch(_p(seqs), _p(offs), _p(lens_a), _p(first_a), _p(nseq_a), nw, gap, mismatch,
+                                  match, int(banded), band_width, score_bits, max_nodes, max_consensus, max_seqs,
+                                  nthreads, _p(cons), _p(cov), _p(clen), _p(status), _p(cells))
+    out = [bytes(cons[i * max_consensus:i * max_consensus + clen[i]]).decode() for i in range(nw)]
+    return out, status, cells, used
+
+
+# ---- single-kernel known-answer hooks ------------------------------------------
+
+def topsort(outgoing):
+    n = len(outgoing)
+    in_cnt = np.zeros(n, np.uint16)
+    out_cnt = np.zeros(n, np.uint16)
+    out_e = np.zeros(n * MAX_EDGES, np.int32)
+    for i, outs in enumerate(outgoing):
+        out_cnt[i] = len(outs)
+        for j, o in enumerate(outs):
+            in_cnt[o] += 1
+            out_e[i * MAX_EDGES + j] = o
+    res = np.zeros(n, np.int32)
+    lib().oracle_topsort(n, _p(in_cnt), _p(out_e), _p(out_cnt), _p(res))
+    return res.tolist()
+
+
+def edges_from_lists(outgoing, n):
+    """BasicGraph::get_edges (reference cudapoa/tests/basic_graph.hpp:70-85)."""
+    in_cnt = np.zeros(n, np.uint16)
+    out_cnt = np.zeros(n, np.uint16)
+    in_e = np.zeros(n * MAX_EDGES, np.int32)
+    out_e = np.zeros(n * MAX_EDGES, np.int32)
+    for i, outs in enumerate(outgoing):
+        out_cnt[i] = len(outs)
+        for j, o in enumerate(outs):
+            in_e[o * MAX_EDGES + in_cnt[o]] = i
+            in_cnt[o] += 1
+            out_e[i * MAX_EDGES + j] = o
+    return in_cnt, in_e, out_cnt, out_e
+
+
+def nw(nodes, sorted_graph, outgoing, read, gap=-8, mismatch=-6, match=8):
+    n = len(nodes)
+    in_cnt, in_e, out_cnt, _ = edges_from_lists(outgoing, n)
+    bases = np.frombuffer(nodes.encode(), np.uint8).copy()
+    srt = np.array(sorted_graph, np.int32)
+    pos = np.zeros(n, np.int32)
+    for p, v in enumerate(sorted_graph):
+        pos[v] = p
+    rd = np.frombuffer(read.encode() + b"\0" * 8, np.uint8).copy()
+    ag = np.zeros(n + len(read) + 4, np.int32)
+    ar = np.zeros(n + len(read) + 4, np.int32)
+    k = lib().oracle_nw(n, _p(bases), _p(srt), _p(pos), _p(in_cnt), _p(in_e), _p(out_cnt), _p(rd), len(read),
+                        gap, mismatch, match, _p(ag), _p(ar))
+    return ag[:k].tolist(), ar[:k].tolist()
+
+
+def add_alignment(nodes, edges, aligned, coverage, read, graph, readpos, max_nodes=3072, weights=None):
+    n = len(nodes)
+    in_cnt, in_e, out_cnt, out_e = (np.zeros(max_nodes, np.uint16), np.zeros(max_nodes * MAX_EDGES, np.int32),
+                                    np.zeros(max_nodes, np.uint16), np.zeros(max_nodes * MAX_EDGES, np.int32))
+    a, b, c, d = edges_from_lists(edges, n)
+    in_cnt[:n], in_e[:n * MAX_EDGES], out_cnt[:n], out_e[:n * MAX_EDGES] = a, b, c, d
+    bases = np.zeros(max_nodes, np.uint8)
+    bases[:n] = np.frombuffer(nodes.encode(), np.uint8)
+    in_w = np.zeros(max_nodes * MAX_EDGES, np.uint16)
+    aln_cnt = np.zeros(max_nodes, np.uint16)
+    aln = np.zeros(max_nodes * MAX_EDGES, np.int32)
+    for i, al in enumerate(aligned):
+        for j, x in enumerate(al):
+            aln[i * MAX_EDGES + j] = x
+            aln_cnt[i] += 1
+    cov = np.zeros(max_nodes, np.uint16)
+    cov[:len(coverage)] = coverage
+    ncount = np.array([n], np.int32)
+    ag = np.array(graph, np.int32)
+    ar = np.array(readpos, np.int32)
+    rd = np.frombuffer(read.encode() + b"\0" * 8, np.uint8).copy()
+    w = np.zeros(len(read) + 8, np.int8) if weights is None else np.asarray(weights + [0] * 8, np.int8)
+    st = lib().oracle_add_alignment(max_nodes, _p(ncount), _p(bases), _p(in_cnt), _p(in_e), _p(in_w), _p(out_cnt),
+                                    _p(out_e), _p(aln_cnt), _p(aln), _p(cov), _p(ag), _p(ar), len(graph), _p(rd),
+                                    _p(w))
+    nn = int(ncount[0])
+    outs = [[int(out_e[v * MAX_EDGES + e]) for e in range(int(out_cnt[v]))] for v in range(nn)]
+    return st, outs
+
+
+def consensus_raw(nodes, sorted_graph, aligned, outgoing, coverage, weights, max_cons=2048):
+    """generateConsensusTestKernel input construction as in the reference test
+    (Test_CudapoaGenerateConsensus.cu:30-75, 160-240): the incoming weight of
+    edge i->o is written at slot index i of node o (the test's own indexing)."""
+    n = len(nodes)
+    in_cnt, in_e, out_cnt, out_e = edges_from_lists(outgoing, n)
+    in_w = np.zeros(n * MAX_EDGES, np.uint16)
+    for i, outs in enumerate(outgoing):
+        for j, o in enumerate(outs):
+            in_w[o * MAX_EDGES + i] = weights[i][j]
+    bases = np.frombuffer(nodes.encode(), np.uint8).copy()
+    srt = np.array(sorted_graph, np.int32)
+    pos = np.zeros(n, np.int32)
+    for p, v in enumerate(sorted_graph):
+        pos[v] = p
+    aln_cnt = np.zeros(n, np.uint16)
+    aln = np.zeros(n * MAX_EDGES, np.int32)
+    for i, al in enumerate(aligned):
+        for j, x in enumerate(al):
+            aln[i * MAX_EDGES + j] = x
+            aln_cnt[i] += 1
+    cov = np.array(coverage, np.uint16)
+    cons = np.zeros(max_cons + 1, np.uint8)
+    ccov = np.zeros(max_cons + 1, np.uint16)
+    st = lib().oracle_consensus_raw(n, _p(bases), _p(srt), _p(pos), _p(in_cnt), _p(in_e), _p(in_w), _p(out_cnt),
+                                    _p(out_e), _p(aln_cnt), _p(aln), _p(cov), max_cons, _p(cons), _p(ccov))
+    return st, bytes(cons).split(b"\0", 1)[0].decode()
