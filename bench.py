@@ -1,0 +1,229 @@
+"""Benchmark: POA consensus windows/s on MI355X (BASELINE.json configs[1], "B").
+
+Workload: 1024 windows per GPU; window w uses
+std::minstd_rand(seed w) -> 1000-base backbone + 31 mutated copies
+(generate_random_sequences(bb, 32, rng, 50, 50, 50)), BatchSize(1100, 32),
+full alignment, scores -8/-6/8, int16 scores.  A step is one pass of the POA
+kernel over the whole resident batch (graph build + NW + add + topsort +
+consensus for every window).  Inputs are uploaded before timing.
+
+N GPUs: one process per GPU (torch.distributed, RCCL), each rank runs its own
+1024 windows (weak scaling); the consensus strings are gathered to rank 0 over
+RCCL once after the timed region.
+
+Prints one JSON line (rank 0) with roofline and cpu_baseline objects.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (import before libgwamd so both share one HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    # name: (backbone, reads, mut, ins, del, max_seq, banded, band_width, windows per GPU)
+    "B": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=False, bw=256, windows=1024),
+    "B_banded": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=True, bw=256, windows=1024),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--config", default="B", choices=sorted(CONFIGS))
+    p.add_argument("--windows", type=int, default=None, help="override windows per GPU")
+    p.add_argument("--cpu-sample", type=int, default=None, help="windows in the CPU baseline sample")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_poa_B.json"))
+    return p.parse_args()
+
+
+def cpu_threads():
+    v = os.environ.get("OMP_NUM_THREADS")
+    if v and v.isdigit() and int(v) > 0:
+        return int(v)
+    return os.cpu_count() or 1
+
+
+def main():
+    args = parse()
+    cfg = dict(CONFIGS[args.config])
+    if args.windows:
+        cfg["windows"] = args.windows
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    torch.cuda.set_device(local_rank)
+    dev = local_rank
+
+    from claragenomicsanalysis_amd import synth
+    from claragenomicsanalysis_amd.cudapoa import CudaPoaBatch
+
+    nwin = cfg["windows"]
+    first_seed = 1 + rank * nwin
+    t0 = time.time()
+    bases, lens = synth.poa_windows_packed(first_seed, nwin, cfg["backbone"], cfg["reads"], cfg["err"], cfg["err"],
+                                           cfg["err"])
+    raw = bases.tobytes()
+    gen_s = time.time() - t0
+
+    stream = torch.cuda.Stream(device=dev)
+    max_mem = int(nwin * 12.5e6) + (2 << 30)
+    batch = CudaPoaBatch(cfg["reads"], cfg["max_seq"], max_mem, device_id=dev, stream=stream,
+                         cuda_banded_alignment=cfg["banded"], alignment_band_width=cfg["bw"])
+    off = 0
+    windows = []
+    for w in range(nwin):
+        win = []
+        for r in range(cfg["reads"]):
+            k = int(lens[w, r])
+            win.append(raw[off:off + k])
+            off += k
+        windows.append(win)
+        st, _ = batch.add_poa_group(win)
+        if st != 0:
+            raise RuntimeError("add_poa_group failed for window %d: %d" % (w, st))
+    batch.upload()
+    batch.synchronize()
+    score_bits, size_bits = batch.get_types()
+
+    for _ in range(args.warmup):
+        batch.launch()
+    batch.synchronize()
+
+    # timed region: barrier + sync on both sides, HIP events on the batch stream
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t_start = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        batch.launch()
+    ev1.record(stream)
+    batch.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t_start
+    kernel_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
+
+    t_max = torch.tensor([wall], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    wall_max = float(t_max.item())
+
+    # outputs + work counters (outside the timed region)
+    cons, cov, status = batch.get_consensus()
+    cells, final_nodes = batch.get_stats()
+    n_ok = int(sum(1 for s in status if s == 0))
+    sb = score_bits // 8
+    cells_total = int(cells.sum())
+    alg_bytes = cells_total * sb * 2 + 2 * int(lens.sum()) + 3 * int(sum(len(c) for c in cons))
+
+    # final consensus gather to rank 0 over RCCL
+    gather_ms = None
+    if world > 1:
+        cmax = 2 * cfg["max_seq"]
+        buf = np.zeros((nwin, cmax + 4), np.uint8)
+        for i, c in enumerate(cons):
+            b = c.encode()
+            buf[i, :4] = np.frombuffer(np.int32(len(b)).tobytes(), np.uint8)
+            buf[i, 4:4 + len(b)] = np.frombuffer(b, np.uint8)
+        t = torch.from_numpy(buf).cuda()
+        parts = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        dist.gather(t, parts, dst=0)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) * 1e3
+
+    # parity spot-check and CPU baseline (rank 0, test infrastructure)
+    parity = None
+    cpu = None
+    if rank == 0:
+        from oracle import oracle
+        mn = ((4 if cfg["banded"] else 3) * cfg["max_seq"] + 3) // 4 * 4
+        k = min(4, nwin)
+        ok = True
+        for i in range(k):
+            r = oracle.poa_window(windows[i], banded=cfg["banded"], band_width=cfg["bw"], score_bits=score_bits,
+                                  max_nodes=mn, max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"])
+            ok = ok and (r.status == status[i] and r.consensus == cons[i] and r.coverage == cov[i])
+        parity = {"windows_checked": k, "bit_exact_vs_oracle": bool(ok)}
+        if not args.no_cpu and world == 1:
+            th = cpu_threads()
+            ns = args.cpu_sample or min(nwin, max(th * 4, 16))
+            tc = time.perf_counter()
+            ccons, cst, _, used = oracle.poa_batch(windows[:ns], nthreads=th, banded=cfg["banded"],
+                                                   band_width=cfg["bw"], score_bits=score_bits, max_nodes=mn,
+                                                   max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"])
+            cpu_s = time.perf_counter() - tc
+            cpu = {"value": round(ns / cpu_s, 3), "unit": "windows/s", "cores": int(used), "kind": "port",
+                   "sample": "first %d windows of the same workload, oracle/poa_oracle.cpp (reference-algorithm "
+                             "C++ restatement, not SPOA), OpenMP one window per thread, %.1f s wall" % (ns, cpu_s),
+                   "matches_gpu": bool(all(ccons[i] == cons[i] for i in range(ns)))}
+
+    if rank == 0:
+        kernel_s = kernel_ms / 1e3
+        achieved = alg_bytes / kernel_s / 1e9
+        traffic = None
+        if os.path.exists(args.traffic_file):
+            try:
+                tf = json.load(open(args.traffic_file))
+                if tf.get("config") == args.config and tf.get("windows") == nwin:
+                    traffic = tf.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        total_windows = nwin * world
+        out = {
+            "metric": "POA windows/sec (consensus)",
+            "value": round(total_windows * args.steps / wall_max, 3),
+            "unit": "windows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int16" if score_bits == 16 else "int32",
+            "data": "synthetic (reference genomeutils generators, seeds 1..N)",
+            "config": {"workload": "cudapoa consensus, %d windows/GPU x %d reads x ~%d bp synthetic ONT, %s"
+                                   % (nwin, cfg["reads"], cfg["backbone"],
+                                      "banded bw=%d" % cfg["bw"] if cfg["banded"] else "full alignment"),
+                       "config_key": args.config, "windows_per_gpu": nwin, "batch_size": [cfg["max_seq"],
+                                                                                        cfg["reads"]],
+                       "scores": [-8, -6, 8], "parallelism": "dp%d (windows sharded, RCCL gather)" % world,
+                       "score_bits": score_bits, "size_bits": size_bits,
+                       "windows_ok": n_ok, "dp_cells_per_step": cells_total,
+                       "gcups": round(cells_total / kernel_s / 1e9, 3),
+                       "mean_final_nodes": round(float(np.mean(final_nodes)), 1),
+                       "gather_ms": gather_ms, "input_gen_s": round(gen_s, 2)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "poa_window_kernel", "kernel_ms": round(kernel_ms, 3),
+                         "algorithmic_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,978 @@
+// Host side of the MI355X POA path: the reference's cudapoa::Batch API
+// (cudapoa/include/.../batch.hpp:133-228) implemented over HIP, plus the plain
+// C ABI declared in include/gwamd_cudapoa.h.
+//
+// Host semantics follow the reference's CudapoaBatch (cudapoa_batch.cuh:56-632)
+// and BatchBlock (allocate_block.hpp:47-460): the same score/size type choice,
+// the same window capacity (max_poas) and score-buffer budget accounting, the
+// same per-entry status codes, and the same error behaviour (throws where the
+// reference throws).  Device memory is laid out for the HIP kernels
+// (poa_kernels.hip), not the reference's slab.
+#include <claraparabricks/genomeworks/cudapoa/batch.hpp>
+
+#include "gwamd_cudapoa.h"
+#include "poa_common.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <iomanip>
+#include <sstream>
+#include <string>
+
+extern "C" hipError_t gwamd_internal_poa_launch(const gwamd::poa::Buffers* b, const gwamd::poa::Dims* d,
+                                       const gwamd::poa::Scores* sc, int score_bits, int size_bits, int banded,
+                                       int msa, hipStream_t stream);
+
+namespace claraparabricks
+{
+namespace genomeworks
+{
+namespace cudapoa
+{
+
+namespace
+{
+
+#define GWAMD_HIP_CHECK(expr)                                                                                  \
+    do                                                                                                         \
+    {                                                                                                          \
+        hipError_t e__ = (expr);                                                                               \
+        if (e__ != hipSuccess)                                                                                 \
+            throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e__) + " at " #expr);       \
+    } while (0)
+
+struct ScopedDevice
+{
+    int prev = -1;
+    explicit ScopedDevice(int dev)
+    {
+        GWAMD_HIP_CHECK(hipGetDevice(&prev));
+        if (prev != dev)
+            GWAMD_HIP_CHECK(hipSetDevice(dev));
+    }
+    ~ScopedDevice()
+    {
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0)
+            (void)hipSetDevice(prev);
+    }
+};
+
+// use32bitScore / use32bitSize (cudapoa_limits.hpp:28-53)
+bool use32bit_score(const BatchSize& bs, int16_t gap, int16_t mismatch, int16_t match)
+{
+    int32_t upper = bs.max_sequence_size * match;
+    int32_t lower = bs.max_sequence_size * std::max(gap, mismatch) +
+                    (bs.max_matrix_graph_dimension - bs.max_sequence_size) * gap;
+    return upper > INT16_MAX || (-lower) > (INT16_MAX + 1);
+}
+
+bool use32bit_size(const BatchSize& bs, bool banded)
+{
+    int32_t m = bs.max_consensus_size;
+    m         = std::max(m, banded ? bs.max_matrix_graph_dimension_banded : bs.max_matrix_graph_dimension);
+    m         = std::max(m, bs.max_matrix_sequence_dimension);
+    return m > INT16_MAX;
+}
+
+inline int64_t align8(int64_t v) { return (v + 7) & ~int64_t(7); }
+
+// Device bytes per window as accounted by the reference
+// (allocate_block.hpp:292-338); sizes of SizeT/ScoreT are the chosen types.
+int64_t reference_device_bytes_per_poa(const BatchSize& bs, bool banded, bool msa, int size_bytes)
+{
+    const int64_t gdim  = banded ? bs.max_matrix_graph_dimension_banded : bs.max_matrix_graph_dimension;
+    const int64_t nodes = banded ? bs.max_nodes_per_window_banded : bs.max_nodes_per_window;
+    const int64_t E = gwamd::poa::kMaxEdges, A = gwamd::poa::kMaxAlignments, S = bs.max_sequences_per_poa;
+    int64_t b = 0;
+    b += bs.max_consensus_size;                                   // consensus
+    b += !msa ? bs.max_consensus_size * 2 : 0;                    // coverage
+    b += msa ? bs.max_consensus_size * S : 0;                     // msa
+    b += S * bs.max_sequence_size * 2;                            // sequences + weights
+    b += S * size_bytes;                                          // sequence lengths
+    b += 32;                                                      // WindowDetails
+    b += msa ? S * size_bytes : 0;                                // sequence_begin_nodes_ids
+    b += nodes;                                                   // nodes
+    b += nodes * A * size_bytes + nodes * 2;                      // node_alignments (+count)
+    b += nodes * E * size_bytes + nodes * 2;                      // incoming edges (+count)
+    b += nodes * E * size_bytes + nodes * 2;                      // outgoing edges (+count)
+    b += nodes * E * 2 * 2;                                       // in/out edge weights
+    b += nodes * size_bytes * 2 + nodes * 2;                      // sorted, node map, local count
+    b += !msa ? nodes * 4 + nodes * size_bytes : 0;               // consensus scores / predecessors
+    b += nodes + nodes + nodes * size_bytes;                      // marks, check, nodes_to_visit
+    b += nodes * 2;                                               // node coverage
+    b += msa ? nodes * E * S * 2 + nodes * E * 2 + nodes * size_bytes : 0; // edge coverage, msa pos
+    b += gdim * size_bytes * 2;                                   // alignment graph/read
+    return b;
+}
+
+struct DevBuf
+{
+    void* p = nullptr;
+    size_t n = 0;
+};
+
+class PinnedBuf
+{
+public:
+    ~PinnedBuf() { release(); }
+    void reserve(size_t bytes, hipStream_t stream)
+    {
+        if (bytes <= cap_)
+            return;
+        size_t ncap = std::max(bytes, cap_ * 2);
+        void* np    = nullptr;
+        GWAMD_HIP_CHECK(hipHostMalloc(&np, ncap, hipHostMallocDefault));
+        if (p_)
+        {
+            // an async H2D copy may still read the old buffer
+            GWAMD_HIP_CHECK(hipStreamSynchronize(stream));
+            std::memcpy(np, p_, used_);
+            (void)hipHostFree(p_);
+        }
+        p_   = np;
+        cap_ = ncap;
+    }
+    template <typename T>
+    T* as() const { return static_cast<T*>(p_); }
+    size_t used_ = 0;
+
+private:
+    void release()
+    {
+        if (p_)
+            (void)hipHostFree(p_);
+        p_ = nullptr;
+    }
+    void* p_    = nullptr;
+    size_t cap_ = 0;
+};
+
+} // namespace
+
+class PoaBatch : public Batch
+{
+public:
+    PoaBatch(int32_t device_id, hipStream_t stream, size_t max_mem, int8_t output_mask, const BatchSize& bs,
+             int16_t gap, int16_t mismatch, int16_t match, bool banded)
+        : device_id_(detail::check_non_negative(device_id, "Device ID has to be non-negative"))
+        , stream_(stream)
+        , output_mask_(output_mask)
+        , bs_(bs)
+        , gap_(gap)
+        , mismatch_(mismatch)
+        , match_(match)
+        , banded_(banded)
+    {
+        detail::check_non_negative(bs.max_sequences_per_poa, "Maximum sequences per POA has to be non-negative");
+        ScopedDevice dev(device_id_);
+        score_bits_ = use32bit_score(bs_, gap_, mismatch_, match_) ? 32 : 16;
+        size_bits_  = (score_bits_ == 32 && use32bit_size(bs_, banded_)) ? 32 : 16;
+        // batch.cu:45-73: 16-bit score implies 16-bit size
+        const int sz      = size_bits_ / 8;
+        const int sbytes  = score_bits_ / 8;
+        const bool msa    = (output_mask_ & OutputType::msa) != 0;
+        const int64_t gdim = banded_ ? bs_.max_matrix_graph_dimension_banded : bs_.max_matrix_graph_dimension;
+        const int64_t ref_seq_dim = banded_ ? bs_.alignment_band_width + gwamd::poa::kBandPad : bs_.max_matrix_sequence_dimension;
+
+        // BatchBlock ctor (allocate_block.hpp:51-91)
+        const int64_t per_poa = reference_device_bytes_per_poa(bs_, banded_, msa, sz);
+        if (int64_t(max_mem) < per_poa)
+        {
+            throw std::runtime_error(std::string("Require at least ") + std::to_string(per_poa) +
+                                     " bytes of device memory per CUDAPOA batch to process correctly.");
+        }
+        const int64_t ref_score_matrix = ref_seq_dim * gdim * sbytes;
+        int64_t max_poas               = int64_t(max_mem) / (per_poa + ref_score_matrix);
+
+        // this build's own per-window footprint
+        dims_.max_nodes     = banded_ ? bs_.max_nodes_per_window_banded : bs_.max_nodes_per_window;
+        dims_.max_seqs      = bs_.max_sequences_per_poa;
+        dims_.max_seq_len   = bs_.max_sequence_size;
+        dims_.max_consensus = bs_.max_consensus_size;
+        dims_.band_width    = bs_.alignment_band_width;
+        dims_.score_stride  = banded_ ? bs_.alignment_band_width + gwamd::poa::kBandPad
+                                      : int32_t(align8(int64_t(bs_.max_sequence_size) + 16));
+        dims_.score_rows    = dims_.max_nodes + 2;
+        dims_.aln_cap       = dims_.max_nodes + bs_.max_sequence_size + 4;
+        dims_.want_consensus = (output_mask_ & OutputType::consensus) ? 1 : 0;
+        const int64_t own = own_bytes_per_window(sz, sbytes, msa);
+        if (own > 0)
+            max_poas = std::min<int64_t>(max_poas, int64_t(max_mem) / own);
+        if (max_poas < 1)
+            throw std::runtime_error("Require more device memory per CUDAPOA batch to process correctly.");
+        max_poas_ = int32_t(std::min<int64_t>(max_poas, INT32_MAX));
+
+        // score budget (allocate_block.hpp:196-201): what the reference's slab
+        // leaves for the variable-width score matrices
+        scorebuf_alloc_ = int64_t(max_mem) - reference_fixed_slab(sz, msa);
+        if (scorebuf_alloc_ < 0)
+            scorebuf_alloc_ = 0;
+
+        allocate(sz, sbytes, msa);
+        bid_ = batches_++;
+        reset();
+    }
+
+    ~PoaBatch() override
+    {
+        (void)hipSetDevice(device_id_);
+        for (auto* b : {&d_seqs_, &d_wts_, &d_len_, &d_off_, &d_win_, &d_slab_})
+            if (b->p)
+                (void)hipFree(b->p);
+    }
+
+    StatusType add_poa_group(std::vector<StatusType>& per_seq_status, const Group& poa_group) override
+    {
+        int32_t max_len = 0;
+        for (const auto& e : poa_group)
+            max_len = std::max(max_len, e.length);
+        if (!reserve_buf(max_len))
+            return StatusType::exceeded_maximum_poas;
+        per_seq_status.clear();
+        StatusType st = add_poa();
+        if (st != StatusType::success)
+            return st;
+        for (const auto& e : poa_group)
+            per_seq_status.push_back(add_seq_to_poa(e.seq, e.weights, e.length));
+        return StatusType::success;
+    }
+
+    int32_t get_total_poas() const override { return poa_count_; }
+
+    void generate_poa() override
+    {
+        if (poa_count_ == 0)
+            return;
+        upload();
+        launch();
+    }
+
+    void upload()
+    {
+        ScopedDevice dev(device_id_);
+        const size_t nb = num_bases_;
+        GWAMD_HIP_CHECK(hipMemcpyAsync(d_seqs_.p, h_seqs_.as<uint8_t>(), nb + 16, hipMemcpyHostToDevice, stream_));
+        GWAMD_HIP_CHECK(hipMemcpyAsync(d_wts_.p, h_wts_.as<int8_t>(), nb + 16, hipMemcpyHostToDevice, stream_));
+        GWAMD_HIP_CHECK(hipMemcpyAsync(d_len_.p, h_len_.as<int32_t>(), size_t(num_seqs_) * 4, hipMemcpyHostToDevice,
+                                       stream_));
+        GWAMD_HIP_CHECK(hipMemcpyAsync(d_off_.p, h_off_.as<int64_t>(), size_t(num_seqs_) * 8, hipMemcpyHostToDevice,
+                                       stream_));
+        GWAMD_HIP_CHECK(hipMemcpyAsync(d_win_.p, h_win_.as<gwamd::poa::WindowDesc>(),
+                                       size_t(poa_count_) * sizeof(gwamd::poa::WindowDesc), hipMemcpyHostToDevice,
+                                       stream_));
+    }
+
+    void launch()
+    {
+        if (poa_count_ == 0)
+            return;
+        ScopedDevice dev(device_id_);
+        gwamd::poa::Buffers b = bufs_;
+        b.num_windows         = poa_count_;
+        gwamd::poa::Scores sc{gap_, mismatch_, match_};
+        const bool msa = (output_mask_ & OutputType::msa) != 0;
+        GWAMD_HIP_CHECK(gwamd_internal_poa_launch(&b, &dims_, &sc, score_bits_, size_bits_, banded_ ? 1 : 0, msa ? 1 : 0,
+                                         stream_));
+        generated_ = true;
+    }
+
+    void synchronize()
+    {
+        ScopedDevice dev(device_id_);
+        GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+
+    // Copies per-window outputs of the last launch to host staging.
+    void fetch(bool consensus, bool msa)
+    {
+        ScopedDevice dev(device_id_);
+        const size_t n = size_t(poa_count_);
+        h_status_.resize(n);
+        h_msa_status_.resize(n);
+        h_len_out_.resize(n);
+        h_msa_len_.resize(n);
+        if (consensus)
+        {
+            h_cons_.resize(n * dims_.max_consensus);
+            h_cov_.resize(n * dims_.max_consensus);
+            GWAMD_HIP_CHECK(hipMemcpyAsync(h_cons_.data(), bufs_.cons, n * dims_.max_consensus, hipMemcpyDeviceToHost,
+                                           stream_));
+            GWAMD_HIP_CHECK(hipMemcpyAsync(h_cov_.data(), bufs_.cov, n * dims_.max_consensus * 2,
+                                           hipMemcpyDeviceToHost, stream_));
+            GWAMD_HIP_CHECK(hipMemcpyAsync(h_len_out_.data(), bufs_.cons_len, n * 4, hipMemcpyDeviceToHost, stream_));
+            GWAMD_HIP_CHECK(hipMemcpyAsync(h_status_.data(), bufs_.status, n, hipMemcpyDeviceToHost, stream_));
+        }
+        if (msa)
+        {
+            h_msa_.resize(n * size_t(dims_.max_seqs) * dims_.max_consensus);
+            GWAMD_HIP_CHECK(hipMemcpyAsync(h_msa_.data(), bufs_.msa, h_msa_.size(), hipMemcpyDeviceToHost, stream_));
+            GWAMD_HIP_CHECK(hipMemcpyAsync(h_msa_len_.data(), bufs_.msa_len, n * 4, hipMemcpyDeviceToHost, stream_));
+            GWAMD_HIP_CHECK(hipMemcpyAsync(h_msa_status_.data(), bufs_.msa_status, n, hipMemcpyDeviceToHost, stream_));
+        }
+        GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+
+    StatusType get_consensus(std::vector<std::string>& consensus, std::vector<std::vector<uint16_t>>& coverage,
+                             std::vector<StatusType>& output_status) override
+    {
+        if (!(output_mask_ & OutputType::consensus))
+            return StatusType::output_type_unavailable;
+        fetch(true, false);
+        for (int32_t w = 0; w < poa_count_; w++)
+        {
+            const StatusType st = StatusType(h_status_[w]);
+            if (!generated_ || st != StatusType::success)
+            {
+                output_status.push_back(generated_ ? st : StatusType::generic_error);
+                consensus.emplace_back();
+                coverage.emplace_back();
+                continue;
+            }
+            output_status.push_back(StatusType::success);
+            const char* c = reinterpret_cast<const char*>(&h_cons_[size_t(w) * dims_.max_consensus]);
+            consensus.emplace_back(c, size_t(h_len_out_[w]));
+            const uint16_t* v = &h_cov_[size_t(w) * dims_.max_consensus];
+            coverage.emplace_back(v, v + h_len_out_[w]);
+        }
+        return StatusType::success;
+    }
+
+    StatusType get_msa(std::vector<std::vector<std::string>>& msa, std::vector<StatusType>& output_status) override
+    {
+        if (!(output_mask_ & OutputType::msa))
+            return StatusType::output_type_unavailable;
+        fetch(false, true);
+        for (int32_t w = 0; w < poa_count_; w++)
+        {
+            msa.emplace_back();
+            const StatusType st = StatusType(h_msa_status_[w]);
+            if (!generated_ || st != StatusType::success)
+            {
+                output_status.push_back(generated_ ? st : StatusType::generic_error);
+                continue;
+            }
+            output_status.push_back(StatusType::success);
+            const int nseq = h_win_.as<gwamd::poa::WindowDesc>()[w].num_seqs;
+            for (int s = 0; s < nseq; s++)
+            {
+                const char* row = reinterpret_cast<const char*>(
+                    &h_msa_[(size_t(w) * dims_.max_seqs + s) * dims_.max_consensus]);
+                msa[w].emplace_back(row, size_t(h_msa_len_[w]));
+            }
+        }
+        return StatusType::success;
+    }
+
+    void fetch_graphs()
+    {
+        ScopedDevice dev(device_id_);
+        const size_t n  = size_t(poa_count_);
+        const size_t mn = size_t(dims_.max_nodes);
+        h_g_bases_.resize(n * mn);
+        h_g_in_cnt_.resize(n * mn);
+        h_g_in_w_.resize(n * mn * gwamd::poa::kMaxEdges);
+        h_g_in_e_raw_.resize(n * mn * gwamd::poa::kMaxEdges * (size_bits_ / 8));
+        h_final_nodes_.resize(n);
+        h_status_.resize(n);
+        h_msa_status_.resize(n);
+        GWAMD_HIP_CHECK(hipMemcpyAsync(h_g_bases_.data(), bufs_.base, n * mn, hipMemcpyDeviceToHost, stream_));
+        GWAMD_HIP_CHECK(hipMemcpyAsync(h_g_in_cnt_.data(), bufs_.in_cnt, n * mn * 2, hipMemcpyDeviceToHost, stream_));
+        GWAMD_HIP_CHECK(hipMemcpyAsync(h_g_in_w_.data(), bufs_.in_w, h_g_in_w_.size() * 2, hipMemcpyDeviceToHost,
+                                       stream_));
+        GWAMD_HIP_CHECK(hipMemcpyAsync(h_g_in_e_raw_.data(), bufs_.in_e, h_g_in_e_raw_.size(), hipMemcpyDeviceToHost,
+                                       stream_));
+        GWAMD_HIP_CHECK(hipMemcpyAsync(h_final_nodes_.data(), bufs_.final_nodes, n * 4, hipMemcpyDeviceToHost, stream_));
+        GWAMD_HIP_CHECK(hipMemcpyAsync(h_status_.data(), bufs_.status, n, hipMemcpyDeviceToHost, stream_));
+        GWAMD_HIP_CHECK(hipMemcpyAsync(h_msa_status_.data(), bufs_.msa_status, n, hipMemcpyDeviceToHost, stream_));
+        GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
+        h_g_in_e_.resize(h_g_in_w_.size());
+        if (size_bits_ == 16)
+        {
+            const int16_t* s = reinterpret_cast<const int16_t*>(h_g_in_e_raw_.data());
+            for (size_t i = 0; i < h_g_in_e_.size(); i++)
+                h_g_in_e_[i] = s[i];
+        }
+        else
+            std::memcpy(h_g_in_e_.data(), h_g_in_e_raw_.data(), h_g_in_e_raw_.size());
+    }
+
+    // Graph status: the consensus status when consensus is produced, else MSA's.
+    StatusType graph_status(int32_t w) const
+    {
+        if (!generated_)
+            return StatusType::generic_error;
+        return StatusType((output_mask_ & OutputType::consensus) ? h_status_[w] : h_msa_status_[w]);
+    }
+
+    void get_graphs(std::vector<DirectedGraph>& graphs, std::vector<StatusType>& output_status) override
+    {
+        fetch_graphs();
+        graphs.resize(poa_count_);
+        const size_t mn = size_t(dims_.max_nodes);
+        for (int32_t w = 0; w < poa_count_; w++)
+        {
+            StatusType st = graph_status(w);
+            output_status.push_back(st);
+            if (st != StatusType::success)
+                continue;
+            DirectedGraph& g = graphs[w];
+            for (int32_t v = 0; v < h_final_nodes_[w]; v++)
+            {
+                g.set_node_label(v, std::string(1, char(h_g_bases_[w * mn + v])));
+                const int ne = h_g_in_cnt_[w * mn + v];
+                for (int e = 0; e < ne; e++)
+                {
+                    size_t idx = (w * mn + v) * gwamd::poa::kMaxEdges + e;
+                    g.add_edge(h_g_in_e_[idx], v, h_g_in_w_[idx]);
+                }
+            }
+        }
+    }
+
+    int32_t batch_id() const override { return bid_; }
+
+    void reset() override
+    {
+        poa_count_          = 0;
+        num_bases_          = 0;
+        num_seqs_           = 0;
+        next_scores_offset_ = 0;
+        avail_scorebuf_     = scorebuf_alloc_;
+        generated_          = false;
+    }
+
+    // --- C ABI support ------------------------------------------------------
+    int32_t score_bits() const { return score_bits_; }
+    int32_t size_bits() const { return size_bits_; }
+    const gwamd::poa::Dims& dims() const { return dims_; }
+    const std::vector<uint8_t>& host_cons() const { return h_cons_; }
+    const std::vector<uint16_t>& host_cov() const { return h_cov_; }
+    const std::vector<int32_t>& host_cons_len() const { return h_len_out_; }
+    const std::vector<uint8_t>& host_status() const { return h_status_; }
+    const std::vector<uint8_t>& host_msa() const { return h_msa_; }
+    const std::vector<int32_t>& host_msa_len() const { return h_msa_len_; }
+    const std::vector<uint8_t>& host_msa_status() const { return h_msa_status_; }
+    const std::vector<uint8_t>& host_g_bases() const { return h_g_bases_; }
+    const std::vector<uint16_t>& host_g_in_cnt() const { return h_g_in_cnt_; }
+    const std::vector<int32_t>& host_g_in_e() const { return h_g_in_e_; }
+    const std::vector<uint16_t>& host_g_in_w() const { return h_g_in_w_; }
+    const std::vector<int32_t>& host_final_nodes() const { return h_final_nodes_; }
+    int32_t window_num_seqs(int32_t w) const { return h_win_.as<const gwamd::poa::WindowDesc>()[w].num_seqs; }
+    int8_t output_mask() const { return output_mask_; }
+    int64_t device_bytes() const { return int64_t(d_slab_.n + d_seqs_.n + d_wts_.n + d_len_.n + d_off_.n + d_win_.n); }
+    int32_t max_poas() const { return max_poas_; }
+
+    void get_stats(int64_t* cells, int32_t* final_nodes)
+    {
+        ScopedDevice dev(device_id_);
+        if (poa_count_ == 0)
+            return;
+        GWAMD_HIP_CHECK(hipMemcpyAsync(cells, bufs_.cells, size_t(poa_count_) * 8, hipMemcpyDeviceToHost, stream_));
+        GWAMD_HIP_CHECK(hipMemcpyAsync(final_nodes, bufs_.final_nodes, size_t(poa_count_) * 4, hipMemcpyDeviceToHost,
+                                       stream_));
+        GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+
+private:
+    int64_t own_bytes_per_window(int sz, int sbytes, bool msa) const
+    {
+        const int64_t mn = dims_.max_nodes, E = gwamd::poa::kMaxEdges, S = dims_.max_seqs;
+        int64_t b        = 0;
+        b += align8(mn) + 4 * align8(mn * 2) + align8(mn * E * 2);   // base, counts, coverage, in_w
+        b += 3 * align8(mn * E * sz) + 2 * align8(mn * sz);           // in_e, out_e, aln, sorted, pos
+        b += 2 * align8(int64_t(dims_.aln_cap) * sz);                 // ag, ar
+        b += int64_t(dims_.score_rows) * dims_.score_stride * sbytes; // scores
+        b += align8(mn * 4) + align8(mn * 4 * sz);                    // cscore, cpred
+        b += align8(dims_.max_consensus) + align8(int64_t(dims_.max_consensus) * 2) + 32; // outputs
+        b += int64_t(S) * dims_.max_seq_len * 2 + S * 12;             // inputs
+        if (msa)
+            b += align8(mn * E * S * 2) + align8(mn * E * 2) + align8(S * sz) +
+                 align8(S * int64_t(dims_.max_consensus));
+        return b;
+    }
+
+    // Non-score bytes of the reference slab for max_poas windows
+    // (allocate_block.hpp:121-285, each buffer aligned to 8 B).
+    int64_t reference_fixed_slab(int sz, bool msa) const
+    {
+        const int64_t P = max_poas_, S = bs_.max_sequences_per_poa, E = gwamd::poa::kMaxEdges;
+        const int64_t nodes = banded_ ? bs_.max_nodes_per_window_banded : bs_.max_nodes_per_window;
+        const int64_t gdim  = banded_ ? bs_.max_matrix_graph_dimension_banded : bs_.max_matrix_graph_dimension;
+        const bool cons     = (output_mask_ & OutputType::consensus) != 0;
+        int64_t o           = 0;
+        o += align8(P * bs_.max_consensus_size);
+        o += cons ? align8(P * bs_.max_consensus_size * 2) : 0;
+        o += msa ? align8(P * bs_.max_consensus_size * S) : 0;
+        o += 2 * align8(P * S * bs_.max_sequence_size);
+        o += align8(P * S * sz) + align8(P * 32);
+        o += msa ? align8(P * S * sz) : 0;
+        o += 2 * align8(P * gdim * sz); // alignment graph / read
+        o += align8(P * nodes) + align8(P * nodes * E * sz) + align8(P * nodes * 2);
+        o += align8(P * nodes * E * sz) + align8(P * nodes * 2);
+        o += align8(P * nodes * E * sz) + align8(P * nodes * 2);
+        o += 2 * align8(P * nodes * E * 2);
+        o += 2 * align8(P * nodes * sz) + align8(P * nodes * 2);
+        o += cons ? align8(P * nodes * 4) + align8(P * nodes * sz) : 0;
+        o += 2 * align8(P * nodes) + align8(P * nodes * sz) + align8(P * nodes * 2);
+        o += msa ? align8(P * nodes * E * S * 2) + align8(P * nodes * E * 2) + align8(P * nodes * sz) : 0;
+        return o;
+    }
+
+    void allocate(int sz, int sbytes, bool msa)
+    {
+        const int64_t P = max_poas_, mn = dims_.max_nodes, E = gwamd::poa::kMaxEdges, S = dims_.max_seqs;
+        struct Item
+        {
+            void** dst;
+            int64_t bytes;
+        };
+        void* dummy = nullptr;
+        std::vector<Item> items = {
+            {reinterpret_cast<void**>(&bufs_.base), align8(P * mn)},
+            {reinterpret_cast<void**>(&bufs_.in_cnt), align8(P * mn * 2)},
+            {reinterpret_cast<void**>(&bufs_.out_cnt), align8(P * mn * 2)},
+            {reinterpret_cast<void**>(&bufs_.aln_cnt), align8(P * mn * 2)},
+            {reinterpret_cast<void**>(&bufs_.node_cov), align8(P * mn * 2)},
+            {reinterpret_cast<void**>(&bufs_.in_w), align8(P * mn * E * 2)},
+            {&bufs_.in_e, align8(P * mn * E * sz)},
+            {&bufs_.out_e, align8(P * mn * E * sz)},
+            {&bufs_.aln, align8(P * mn * E * sz)},
+            {&bufs_.sorted, align8(P * mn * sz)},
+            {&bufs_.pos, align8(P * mn * sz)},
+            {&bufs_.ag, align8(P * dims_.aln_cap * sz)},
+            {&bufs_.ar, align8(P * dims_.aln_cap * sz)},
+            {reinterpret_cast<void**>(&bufs_.cscore), align8(P * mn * 4)},
+            {&bufs_.cpred, align8(P * mn * 4 * sz)},
+            {reinterpret_cast<void**>(&bufs_.cons), align8(P * dims_.max_consensus)},
+            {reinterpret_cast<void**>(&bufs_.cov), align8(P * dims_.max_consensus * 2)},
+            {reinterpret_cast<void**>(&bufs_.cons_len), align8(P * 4)},
+            {reinterpret_cast<void**>(&bufs_.status), align8(P)},
+            {reinterpret_cast<void**>(&bufs_.msa_status), align8(P)},
+            {reinterpret_cast<void**>(&bufs_.msa_len), align8(P * 4)},
+            {reinterpret_cast<void**>(&bufs_.final_nodes), align8(P * 4)},
+            {reinterpret_cast<void**>(&bufs_.cells), align8(P * 8)},
+            {msa ? reinterpret_cast<void**>(&bufs_.edge_cov) : &dummy, msa ? align8(P * mn * E * S * 2) : 0},
+            {msa ? reinterpret_cast<void**>(&bufs_.edge_cov_cnt) : &dummy, msa ? align8(P * mn * E * 2) : 0},
+            {msa ? &bufs_.seq_begin : &dummy, msa ? align8(P * S * sz) : 0},
+            {msa ? reinterpret_cast<void**>(&bufs_.msa) : &dummy, msa ? align8(P * S * dims_.max_consensus) : 0},
+        };
+        // the score matrices go last, 256-B aligned
+        int64_t off = 0;
+        for (auto& it : items)
+            off += it.bytes;
+        off                   = (off + 255) & ~int64_t(255);
+        const int64_t sc_off  = off;
+        const int64_t sc_size = P * int64_t(dims_.score_rows) * dims_.score_stride * sbytes;
+        d_slab_.n             = size_t(off + sc_size);
+        GWAMD_HIP_CHECK(hipMalloc(&d_slab_.p, d_slab_.n));
+        uint8_t* base = static_cast<uint8_t*>(d_slab_.p);
+        int64_t cur   = 0;
+        for (auto& it : items)
+        {
+            if (it.bytes > 0)
+                *it.dst = base + cur;
+            cur += it.bytes;
+        }
+        bufs_.scores = base + sc_off;
+        // inputs (allocate_block.hpp:84: max_poas * max_seqs * max_seq bytes)
+        const int64_t in_bytes = P * S * dims_.max_seq_len + 64;
+        d_seqs_.n              = size_t(in_bytes);
+        d_wts_.n               = size_t(in_bytes);
+        d_len_.n               = size_t(P * S * 4 + 8);
+        d_off_.n               = size_t(P * S * 8 + 8);
+        d_win_.n               = size_t(P * sizeof(gwamd::poa::WindowDesc) + 8);
+        for (auto* b : {&d_seqs_, &d_wts_, &d_len_, &d_off_, &d_win_})
+            GWAMD_HIP_CHECK(hipMalloc(&b->p, b->n));
+        bufs_.seqs    = static_cast<const uint8_t*>(d_seqs_.p);
+        bufs_.wts     = static_cast<const int8_t*>(d_wts_.p);
+        bufs_.seq_len = static_cast<const int32_t*>(d_len_.p);
+        bufs_.seq_off = static_cast<const int64_t*>(d_off_.p);
+        bufs_.windows = static_cast<const gwamd::poa::WindowDesc*>(d_win_.p);
+        // status defaults so that reading before generate is defined
+        GWAMD_HIP_CHECK(hipMemsetAsync(bufs_.status, int(StatusType::generic_error), size_t(P), stream_));
+        GWAMD_HIP_CHECK(hipMemsetAsync(bufs_.msa_status, int(StatusType::generic_error), size_t(P), stream_));
+        GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+
+    // cudapoa_batch.cuh:542-564
+    bool reserve_buf(int32_t max_seq_length)
+    {
+        const int64_t gdim  = banded_ ? bs_.max_matrix_graph_dimension_banded : bs_.max_matrix_graph_dimension;
+        const int64_t width = banded_ ? bs_.alignment_band_width + gwamd::poa::kBandPad
+                                      : detail::align_up(max_seq_length + 1 + 4, 4);
+        const int64_t need  = width * gdim * (score_bits_ / 8);
+        if (need > avail_scorebuf_)
+        {
+            if (poa_count_ == 0)
+            {
+                std::cout << "Memory available " << std::fixed << std::setprecision(2)
+                          << double(avail_scorebuf_) / 1024. / 1024. / 1024.;
+                std::cout << "GB, Memory required " << double(need) / 1024. / 1024. / 1024.;
+                std::cout << "GB (sequence length " << max_seq_length << ", graph length " << gdim << ")" << std::endl;
+            }
+            return false;
+        }
+        avail_scorebuf_ -= need;
+        return true;
+    }
+
+    // cudapoa_batch.cuh:471-487
+    StatusType add_poa()
+    {
+        if (poa_count_ == max_poas_)
+            return StatusType::exceeded_maximum_poas;
+        h_win_.reserve(size_t(poa_count_ + 1) * sizeof(gwamd::poa::WindowDesc), stream_);
+        gwamd::poa::WindowDesc& wd = h_win_.as<gwamd::poa::WindowDesc>()[poa_count_];
+        wd.first_seq               = num_seqs_;
+        wd.num_seqs                = 0;
+        h_win_.used_               = size_t(poa_count_ + 1) * sizeof(gwamd::poa::WindowDesc);
+        poa_count_++;
+        generated_ = false;
+        return StatusType::success;
+    }
+
+    // cudapoa_batch.cuh:490-539
+    StatusType add_seq_to_poa(const char* seq, const int8_t* weights, int32_t seq_len)
+    {
+        if (seq_len > bs_.max_sequence_size)
+            return StatusType::exceeded_maximum_sequence_size;
+        gwamd::poa::WindowDesc& wd = h_win_.as<gwamd::poa::WindowDesc>()[poa_count_ - 1];
+        if (wd.num_seqs >= bs_.max_sequences_per_poa)
+            return StatusType::exceeded_maximum_sequences_per_poa;
+        if (weights != nullptr)
+            for (int32_t i = 0; i < seq_len; i++)
+                detail::check_non_negative(weights[i], "Base weights need to be non-negative");
+        wd.num_seqs++;
+        const size_t need = num_bases_ + size_t(seq_len) + 16;
+        h_seqs_.reserve(need, stream_);
+        h_wts_.reserve(need, stream_);
+        if (seq_len > 0)
+            std::memcpy(h_seqs_.as<uint8_t>() + num_bases_, seq, size_t(seq_len));
+        if (weights == nullptr)
+            std::memset(h_wts_.as<int8_t>() + num_bases_, 1, size_t(seq_len));
+        else if (seq_len > 0)
+            std::memcpy(h_wts_.as<int8_t>() + num_bases_, weights, size_t(seq_len));
+        std::memset(h_seqs_.as<uint8_t>() + num_bases_ + seq_len, 0, 16);
+        std::memset(h_wts_.as<int8_t>() + num_bases_ + seq_len, 0, 16);
+        h_len_.reserve(size_t(num_seqs_ + 1) * 4, stream_);
+        h_off_.reserve(size_t(num_seqs_ + 1) * 8, stream_);
+        h_len_.as<int32_t>()[num_seqs_] = seq_len;
+        h_off_.as<int64_t>()[num_seqs_] = int64_t(num_bases_);
+        num_bases_ += size_t(seq_len);
+        h_seqs_.used_ = h_wts_.used_ = num_bases_ + 16;
+        num_seqs_++;
+        h_len_.used_ = size_t(num_seqs_) * 4;
+        h_off_.used_ = size_t(num_seqs_) * 8;
+        return StatusType::success;
+    }
+
+    int32_t device_id_;
+    hipStream_t stream_;
+    int8_t output_mask_;
+    BatchSize bs_;
+    int16_t gap_, mismatch_, match_;
+    bool banded_;
+    int32_t score_bits_ = 16, size_bits_ = 16;
+    int32_t max_poas_   = 0;
+    int64_t scorebuf_alloc_ = 0, avail_scorebuf_ = 0, next_scores_offset_ = 0;
+    int32_t poa_count_  = 0;
+    int32_t num_seqs_   = 0;
+    size_t num_bases_   = 0;
+    bool generated_     = false;
+    int32_t bid_        = 0;
+    gwamd::poa::Dims dims_{};
+    gwamd::poa::Buffers bufs_{};
+    DevBuf d_seqs_, d_wts_, d_len_, d_off_, d_win_, d_slab_;
+    PinnedBuf h_seqs_, h_wts_, h_len_, h_off_, h_win_;
+    std::vector<uint8_t> h_cons_, h_status_, h_msa_, h_msa_status_, h_g_bases_, h_g_in_e_raw_;
+    std::vector<uint16_t> h_cov_, h_g_in_cnt_, h_g_in_w_;
+    std::vector<int32_t> h_len_out_, h_msa_len_, h_g_in_e_, h_final_nodes_;
+    static int32_t batches_; // batch id counter (cudapoa_batch.cuh:631-635)
+};
+
+int32_t PoaBatch::batches_ = 0;
+
+StatusType Init()
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return StatusType::generic_error;
+    return StatusType::success;
+}
+
+std::unique_ptr<Batch> create_batch(int32_t device_id, hipStream_t stream, size_t max_mem, int8_t output_mask,
+                                    const BatchSize& batch_size, int16_t gap_score, int16_t mismatch_score,
+                                    int16_t match_score, bool cuda_banded_alignment)
+{
+    detail::check_non_negative(batch_size.max_sequences_per_poa, "Maximum sequences per POA has to be non-negative");
+    return std::unique_ptr<Batch>(new PoaBatch(device_id, stream, max_mem, output_mask, batch_size, gap_score,
+                                               mismatch_score, match_score, cuda_banded_alignment));
+}
+
+} // namespace cudapoa
+} // namespace genomeworks
+} // namespace claraparabricks
+
+// ===========================================================================
+// C ABI (include/gwamd_cudapoa.h)
+// ===========================================================================
+namespace cp = claraparabricks::genomeworks::cudapoa;
+
+namespace
+{
+thread_local std::string g_last_error;
+
+template <typename F>
+int32_t guarded(F&& f)
+{
+    try
+    {
+        g_last_error.clear();
+        return f();
+    }
+    catch (const std::invalid_argument& e)
+    {
+        g_last_error = e.what();
+        return GWAMD_E_INVALID_ARGUMENT;
+    }
+    catch (const std::runtime_error& e)
+    {
+        g_last_error = e.what();
+        return std::string(e.what()).rfind("HIP error", 0) == 0 ? GWAMD_E_HIP : GWAMD_E_RUNTIME;
+    }
+    catch (const std::exception& e)
+    {
+        g_last_error = e.what();
+        return GWAMD_E_RUNTIME;
+    }
+}
+
+void to_c(const cp::BatchSize& b, gwamd_poa_batch_size* o)
+{
+    o->max_sequence_size                 = b.max_sequence_size;
+    o->max_consensus_size                = b.max_consensus_size;
+    o->max_nodes_per_window              = b.max_nodes_per_window;
+    o->max_nodes_per_window_banded       = b.max_nodes_per_window_banded;
+    o->max_matrix_graph_dimension        = b.max_matrix_graph_dimension;
+    o->max_matrix_graph_dimension_banded = b.max_matrix_graph_dimension_banded;
+    o->max_matrix_sequence_dimension     = b.max_matrix_sequence_dimension;
+    o->alignment_band_width              = b.alignment_band_width;
+    o->max_sequences_per_poa             = b.max_sequences_per_poa;
+}
+
+cp::BatchSize from_c(const gwamd_poa_batch_size* i)
+{
+    cp::BatchSize b;
+    b.max_sequence_size                 = i->max_sequence_size;
+    b.max_consensus_size                = i->max_consensus_size;
+    b.max_nodes_per_window              = i->max_nodes_per_window;
+    b.max_nodes_per_window_banded       = i->max_nodes_per_window_banded;
+    b.max_matrix_graph_dimension        = i->max_matrix_graph_dimension;
+    b.max_matrix_graph_dimension_banded = i->max_matrix_graph_dimension_banded;
+    b.max_matrix_sequence_dimension     = i->max_matrix_sequence_dimension;
+    b.alignment_band_width              = i->alignment_band_width;
+    b.max_sequences_per_poa             = i->max_sequences_per_poa;
+    return b;
+}
+} // namespace
+
+struct gwamd_poa_batch
+{
+    std::unique_ptr<cp::PoaBatch> impl;
+};
+
+extern "C" {
+
+const char* gwamd_last_error(void) { return g_last_error.c_str(); }
+
+int32_t gwamd_poa_batch_size_init(gwamd_poa_batch_size* out, int32_t max_seq_sz, int32_t max_seq_per_poa,
+                                  int32_t band_width)
+{
+    return guarded([&] {
+        to_c(cp::BatchSize(max_seq_sz, max_seq_per_poa, band_width), out);
+        return 0;
+    });
+}
+
+int32_t gwamd_poa_batch_size_init_full(gwamd_poa_batch_size* out, int32_t max_seq_sz, int32_t max_consensus_sz,
+                                       int32_t max_nodes_per_w, int32_t max_nodes_per_w_banded, int32_t band_width,
+                                       int32_t max_seq_per_poa)
+{
+    return guarded([&] {
+        to_c(cp::BatchSize(max_seq_sz, max_consensus_sz, max_nodes_per_w, max_nodes_per_w_banded, band_width,
+                           max_seq_per_poa),
+             out);
+        return 0;
+    });
+}
+
+int32_t gwamd_poa_create_batch(gwamd_poa_batch** out, int32_t device_id, void* stream, size_t max_mem,
+                               int8_t output_mask, const gwamd_poa_batch_size* batch_size, int16_t gap_score,
+                               int16_t mismatch_score, int16_t match_score, int32_t cuda_banded_alignment)
+{
+    *out = nullptr;
+    return guarded([&] {
+        auto* h = new gwamd_poa_batch;
+        try
+        {
+            h->impl.reset(new cp::PoaBatch(device_id, static_cast<hipStream_t>(stream), max_mem, output_mask,
+                                           from_c(batch_size), gap_score, mismatch_score, match_score,
+                                           cuda_banded_alignment != 0));
+        }
+        catch (...)
+        {
+            delete h;
+            throw;
+        }
+        *out = h;
+        return 0;
+    });
+}
+
+void gwamd_poa_destroy_batch(gwamd_poa_batch* batch) { delete batch; }
+
+int32_t gwamd_poa_add_poa_group(gwamd_poa_batch* batch, const char* const* seqs, const int8_t* const* weights,
+                                const int32_t* lengths, int32_t n, int32_t* per_seq_status)
+{
+    return guarded([&] {
+        cp::Group group;
+        for (int32_t i = 0; i < n; i++)
+            group.push_back(cp::Entry{seqs[i], weights ? weights[i] : nullptr, lengths[i]});
+        std::vector<cp::StatusType> st;
+        cp::StatusType rc = batch->impl->add_poa_group(st, group);
+        for (size_t i = 0; i < st.size(); i++)
+            per_seq_status[i] = int32_t(st[i]);
+        for (size_t i = st.size(); i < size_t(n); i++)
+            per_seq_status[i] = int32_t(rc);
+        return int32_t(rc);
+    });
+}
+
+int32_t gwamd_poa_get_total_poas(const gwamd_poa_batch* batch) { return batch->impl->get_total_poas(); }
+
+int32_t gwamd_poa_generate_poa(gwamd_poa_batch* batch)
+{
+    return guarded([&] {
+        batch->impl->generate_poa();
+        return 0;
+    });
+}
+
+int32_t gwamd_poa_upload(gwamd_poa_batch* batch)
+{
+    return guarded([&] {
+        batch->impl->upload();
+        return 0;
+    });
+}
+
+int32_t gwamd_poa_launch(gwamd_poa_batch* batch)
+{
+    return guarded([&] {
+        batch->impl->launch();
+        return 0;
+    });
+}
+
+int32_t gwamd_poa_synchronize(gwamd_poa_batch* batch)
+{
+    return guarded([&] {
+        batch->impl->synchronize();
+        return 0;
+    });
+}
+
+int32_t gwamd_poa_get_consensus(gwamd_poa_batch* batch, int32_t* status, int32_t* lengths, const char** cons_base,
+                                const uint16_t** cov_base, int32_t* stride)
+{
+    return guarded([&] {
+        std::vector<std::string> cons;
+        std::vector<std::vector<uint16_t>> cov;
+        std::vector<cp::StatusType> st;
+        cp::StatusType rc = batch->impl->get_consensus(cons, cov, st);
+        if (rc != cp::StatusType::success)
+            return int32_t(rc);
+        for (size_t i = 0; i < st.size(); i++)
+        {
+            status[i]  = int32_t(st[i]);
+            lengths[i] = int32_t(cons[i].size());
+        }
+        *cons_base = reinterpret_cast<const char*>(batch->impl->host_cons().data());
+        *cov_base  = batch->impl->host_cov().data();
+        *stride    = batch->impl->dims().max_consensus;
+        return int32_t(rc);
+    });
+}
+
+int32_t gwamd_poa_get_msa(gwamd_poa_batch* batch, int32_t* status, int32_t* num_rows, const char** msa_base,
+                          int32_t* row_stride, int32_t* max_seqs)
+{
+    return guarded([&] {
+        std::vector<std::vector<std::string>> msa;
+        std::vector<cp::StatusType> st;
+        cp::StatusType rc = batch->impl->get_msa(msa, st);
+        if (rc != cp::StatusType::success)
+            return int32_t(rc);
+        for (size_t i = 0; i < st.size(); i++)
+        {
+            status[i]   = int32_t(st[i]);
+            num_rows[i] = int32_t(msa[i].size());
+        }
+        *msa_base   = reinterpret_cast<const char*>(batch->impl->host_msa().data());
+        *row_stride = batch->impl->dims().max_consensus;
+        *max_seqs   = batch->impl->dims().max_seqs;
+        return int32_t(rc);
+    });
+}
+
+int32_t gwamd_poa_get_graphs(gwamd_poa_batch* batch, int32_t* status, int32_t* num_nodes, const uint8_t** bases,
+                             const uint16_t** in_count, const int32_t** in_edges, const uint16_t** in_weights,
+                             int32_t* max_nodes)
+{
+    return guarded([&] {
+        batch->impl->fetch_graphs();
+        const int32_t n = batch->impl->get_total_poas();
+        for (int32_t w = 0; w < n; w++)
+        {
+            status[w]    = int32_t(batch->impl->graph_status(w));
+            num_nodes[w] = batch->impl->host_final_nodes()[w];
+        }
+        *bases      = batch->impl->host_g_bases().data();
+        *in_count   = batch->impl->host_g_in_cnt().data();
+        *in_edges   = batch->impl->host_g_in_e().data();
+        *in_weights = batch->impl->host_g_in_w().data();
+        *max_nodes  = batch->impl->dims().max_nodes;
+        return 0;
+    });
+}
+
+int32_t gwamd_poa_batch_id(const gwamd_poa_batch* batch) { return batch->impl->batch_id(); }
+
+void gwamd_poa_reset(gwamd_poa_batch* batch) { batch->impl->reset(); }
+
+int32_t gwamd_poa_get_stats(gwamd_poa_batch* batch, int64_t* cells, int32_t* final_nodes)
+{
+    return guarded([&] {
+        batch->impl->get_stats(cells, final_nodes);
+        return 0;
+    });
+}
+
+int32_t gwamd_poa_get_types(const gwamd_poa_batch* batch, int32_t* score_bits, int32_t* size_bits)
+{
+    *score_bits = batch->impl->score_bits();
+    *size_bits  = batch->impl->size_bits();
+    return 0;
+}
+
+int32_t gwamd_poa_get_capacity(const gwamd_poa_batch* batch, int64_t* device_bytes, int32_t* max_poas)
+{
+    *device_bytes = batch->impl->device_bytes();
+    *max_poas     = batch->impl->max_poas();
+    return 0;
+}
+
+} // extern "C"

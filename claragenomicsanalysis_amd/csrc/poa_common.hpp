@@ -1,0 +1,112 @@
+// Shared host/device definitions for the MI355X POA path.
+//
+// Layout summary (DESIGN.md "Data layout in HBM"): every per-window buffer is a
+// fixed-capacity slot of one batch-wide allocation, window w at offset
+// w * capacity.  Graph adjacency keeps the reference's fixed 50-slot lists
+// (cudapoa_structs.cuh:17-21) so edge/alignment overflow errors fire at exactly
+// the same point as in the reference.
+#pragma once
+
+#include <cstdint>
+
+namespace gwamd
+{
+namespace poa
+{
+
+constexpr int kMaxEdges      = 50; // CUDAPOA_MAX_NODE_EDGES (cudapoa_structs.cuh:18)
+constexpr int kMaxAlignments = 50; // CUDAPOA_MAX_NODE_ALIGNMENTS (cudapoa_structs.cuh:21)
+constexpr int kBandPad       = 8;  // CUDAPOA_BANDED_MATRIX_RIGHT_PADDING (cudapoa_structs.cuh:27)
+constexpr int kWave          = 64; // CDNA wavefront
+constexpr int kCellsPerLane  = 8;  // full-mode DP: 8 consecutive columns per lane
+constexpr int kChunk         = kWave * kCellsPerLane; // 512 columns per wave pass
+constexpr int kColShift      = 7;  // column j of a full-mode score row lives at index j + 7,
+                                   // so each lane's 8 cells are one 16-B aligned group
+
+// StatusType (cudapoa.hpp:26-38); values are ABI.
+enum Status : uint8_t
+{
+    kSuccess               = 0,
+    kExceededMaxPoas       = 1,
+    kExceededMaxSeqSize    = 2,
+    kExceededMaxSeqsPerPoa = 3,
+    kNodeCountExceeded     = 4,
+    kEdgeCountExceeded     = 5,
+    kSeqLenExceededNodes   = 6,
+    kLoopCountExceeded     = 7,
+    kOutputTypeUnavailable = 8,
+    kGenericError          = 9,
+};
+
+// One window of the packed input batch.
+struct WindowDesc
+{
+    int32_t first_seq; // index of the window's first read in seq_len / seq_off
+    int32_t num_seqs;
+};
+
+// Capacities, identical for every window of a batch.
+struct Dims
+{
+    int32_t max_nodes;     // graph node capacity (BatchSize max_nodes_per_window[_banded])
+    int32_t max_seqs;      // reads per window
+    int32_t max_seq_len;   // BatchSize max_sequence_size
+    int32_t max_consensus; // BatchSize max_consensus_size
+    int32_t score_stride;  // ScoreT elements per score row
+    int32_t score_rows;    // rows per window score matrix (max_nodes + 1)
+    int32_t aln_cap;       // traceback buffer capacity
+    int32_t band_width;    // banded mode only
+    int32_t want_consensus; // MSA kernels also emit the consensus when set
+};
+
+// Device pointers of one batch (all batch-wide; per-window slots are derived
+// in-kernel).  SizeT-typed arrays are passed as void* and cast in the kernel.
+struct Buffers
+{
+    // input
+    const uint8_t* seqs;
+    const int8_t* wts;
+    const int32_t* seq_len;
+    const int64_t* seq_off;
+    const WindowDesc* windows;
+    int32_t num_windows;
+    // graph scratch
+    uint8_t* base;
+    uint16_t* in_cnt;
+    uint16_t* out_cnt;
+    uint16_t* aln_cnt;
+    uint16_t* node_cov;
+    uint16_t* in_w;
+    void* in_e;
+    void* out_e;
+    void* aln;
+    void* sorted;
+    void* pos;
+    void* ag;
+    void* ar;
+    void* scores;
+    // consensus / topsort / msa scratch
+    int32_t* cscore;
+    void* cpred;
+    uint16_t* edge_cov;     // msa: read ids per outgoing edge
+    uint16_t* edge_cov_cnt; // msa
+    void* seq_begin;        // msa
+    // outputs
+    uint8_t* cons;      // max_consensus per window; consensus in host order
+    uint16_t* cov;      // max_consensus per window
+    int32_t* cons_len;  // per window
+    uint8_t* status;    // per window, consensus output
+    uint8_t* msa_status; // per window, MSA output
+    uint8_t* msa;       // max_seqs * max_consensus per window
+    int32_t* msa_len;   // per window
+    int32_t* final_nodes;
+    int64_t* cells;     // per window: sum over reads of (|V|+1)*(|r|+1) (or band cells)
+};
+
+struct Scores
+{
+    int32_t gap, mismatch, match;
+};
+
+} // namespace poa
+} // namespace gwamd

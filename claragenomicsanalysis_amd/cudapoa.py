@@ -1,0 +1,283 @@
+"""Python API for MI355X batched POA; mirrors pygenomeworks'
+``genomeworks.cudapoa.CudaPoaBatch`` (pygenomeworks/genomeworks/cudapoa/cudapoa.pyx:19-320):
+same constructor arguments and defaults, same methods and return shapes.
+Everything runs through the C ABI of libgwamd.so (include/gwamd_cudapoa.h).
+"""
+import ctypes as C
+
+import numpy as np
+
+from ._lib import load_library, last_error
+
+MAX_EDGES = 50
+
+# StatusType (cudapoa.hpp:26-38)
+STATUS_NAMES = ["success", "exceeded_maximum_poas", "exceeded_maximum_sequence_size",
+                "exceeded_maximum_sequences_per_poa", "node_count_exceeded_maximum_graph_size",
+                "edge_count_exceeded_maximum_graph_size", "seq_len_exceeded_maximum_nodes_per_window",
+                "loop_count_exceeded_upper_bound", "output_type_unavailable", "generic_error"]
+SUCCESS = 0
+OUTPUT_TYPE_UNAVAILABLE = 8
+CONSENSUS = 0x1
+MSA = 0x2
+
+
+def status_to_str(status):
+    """cudapoa.pyx:19-40."""
+    if 0 <= int(status) < len(STATUS_NAMES):
+        return STATUS_NAMES[int(status)]
+    raise RuntimeError("Unknown error status : " + str(status))
+
+
+class BatchSize(C.Structure):
+    """cudapoa::BatchSize (batch.hpp:53-129)."""
+    _fields_ = [(n, C.c_int32) for n in (
+        "max_sequence_size", "max_consensus_size", "max_nodes_per_window", "max_nodes_per_window_banded",
+        "max_matrix_graph_dimension", "max_matrix_graph_dimension_banded", "max_matrix_sequence_dimension",
+        "alignment_band_width", "max_sequences_per_poa")]
+
+    @classmethod
+    def make(cls, max_seq_sz=1024, max_seq_per_poa=100, band_width=256):
+        bs = cls()
+        _check(load_library().gwamd_poa_batch_size_init(C.byref(bs), max_seq_sz, max_seq_per_poa, band_width))
+        return bs
+
+    @classmethod
+    def make_full(cls, max_seq_sz, max_consensus_sz, max_nodes_per_w, max_nodes_per_w_banded, band_width,
+                  max_seq_per_poa):
+        bs = cls()
+        _check(load_library().gwamd_poa_batch_size_init_full(C.byref(bs), max_seq_sz, max_consensus_sz,
+                                                             max_nodes_per_w, max_nodes_per_w_banded, band_width,
+                                                             max_seq_per_poa))
+        return bs
+
+
+def _check(rc):
+    if rc == -1:
+        raise ValueError(last_error())
+    if rc < 0:
+        raise RuntimeError(last_error())
+    return rc
+
+
+class DiGraph:
+    """Minimal directed graph returned by get_graphs (the reference returns a
+    networkx.DiGraph, cudapoa.pyx:268-288; networkx is not a dependency here)."""
+
+    def __init__(self):
+        self._succ = {}
+        self._labels = {}
+        self._weights = {}
+
+    def add_edge(self, u, v, weight=0):
+        self._succ.setdefault(u, set())
+        self._succ.setdefault(v, set())
+        if v not in self._succ[u]:
+            self._succ[u].add(v)
+            self._weights[(u, v)] = weight
+
+    def add_node(self, n, label=None):
+        self._succ.setdefault(n, set())
+        if label is not None:
+            self._labels[n] = label
+
+    @property
+    def nodes(self):
+        return sorted(self._succ)
+
+    @property
+    def edges(self):
+        return sorted(self._weights)
+
+    def number_of_nodes(self):
+        return len(self._succ)
+
+    def number_of_edges(self):
+        return len(self._weights)
+
+    def label(self, n):
+        return self._labels.get(n, "")
+
+    def weight(self, u, v):
+        return self._weights[(u, v)]
+
+
+class CudaPoaBatch:
+    """Python API for MI355X partial order alignment (cudapoa.pyx:60-320)."""
+
+    def __init__(self, max_sequences_per_poa, max_sequence_size, max_gpu_mem, output_type="consensus",
+                 device_id=0, stream=None, gap_score=-8, mismatch_score=-6, match_score=8,
+                 cuda_banded_alignment=False, alignment_band_width=256, max_consensus_size=None,
+                 max_nodes_per_window=None, max_nodes_per_window_banded=None, *args, **kwargs):
+        self._lib = load_library()
+        self._handle = C.c_void_p()
+        if stream is None:
+            st = None
+        elif isinstance(stream, int):
+            st = stream
+        elif hasattr(stream, "cuda_stream"):  # torch.cuda.Stream
+            st = stream.cuda_stream
+        elif hasattr(stream, "stream"):
+            st = stream.stream
+        else:
+            raise RuntimeError("Type for stream option must be a HIP stream handle")
+        if output_type == "consensus":
+            output_mask = CONSENSUS
+        elif output_type == "msa":
+            output_mask = MSA
+        elif output_type in ("both", "consensus+msa"):
+            output_mask = CONSENSUS | MSA
+        else:
+            raise RuntimeError("Unknown output_type provided. Must be consensus/msa.")
+        self.output_type = output_type
+        mx_cons = 2 * max_sequence_size if max_consensus_size is None else max_consensus_size
+        mx_nodes = 3 * max_sequence_size if max_nodes_per_window is None else max_nodes_per_window
+        mx_nodes_b = 4 * max_sequence_size if max_nodes_per_window_banded is None else max_nodes_per_window_banded
+        self.batch_size = BatchSize.make_full(max_sequence_size, mx_cons, mx_nodes, mx_nodes_b,
+                                              alignment_band_width, max_sequences_per_poa)
+        _check(self._lib.gwamd_poa_create_batch(C.byref(self._handle), device_id, st, int(max_gpu_mem),
+                                                output_mask, C.byref(self.batch_size), gap_score, mismatch_score,
+                                                match_score, int(bool(cuda_banded_alignment))))
+
+    def __del__(self):
+        h = getattr(self, "_handle", None)
+        if h is not None and h.value:
+            self._lib.gwamd_poa_destroy_batch(h)
+            self._handle = None
+
+    def add_poa_group(self, poa, weights=None):
+        """cudapoa.pyx:147-178; returns (status, per-sequence status list)."""
+        if not isinstance(poa, list):
+            poa = [poa]
+        if len(poa) < 1:
+            raise RuntimeError("At least one sequence must be present in POA group")
+        n = len(poa)
+        data = [s.encode() if isinstance(s, str) else bytes(s) for s in poa]
+        seqs = (C.c_char_p * n)(*data)
+        lens = (C.c_int32 * n)(*[len(d) for d in data])
+        wptrs = None
+        keep = []
+        if weights is not None:
+            wptrs = (C.c_void_p * n)()
+            for i, w in enumerate(weights):
+                if w is None:
+                    wptrs[i] = None
+                else:
+                    a = np.ascontiguousarray(w, dtype=np.int8)
+                    keep.append(a)
+                    wptrs[i] = a.ctypes.data
+        seq_status = (C.c_int32 * n)()
+        rc = _check(self._lib.gwamd_poa_add_poa_group(self._handle, seqs, wptrs, lens, n, seq_status))
+        return rc, list(seq_status)
+
+    @property
+    def total_poas(self):
+        return self._lib.gwamd_poa_get_total_poas(self._handle)
+
+    @property
+    def batch_id(self):
+        return self._lib.gwamd_poa_batch_id(self._handle)
+
+    def generate_poa(self):
+        _check(self._lib.gwamd_poa_generate_poa(self._handle))
+
+    # split form of generate_poa used by bench.py
+    def upload(self):
+        _check(self._lib.gwamd_poa_upload(self._handle))
+
+    def launch(self):
+        _check(self._lib.gwamd_poa_launch(self._handle))
+
+    def synchronize(self):
+        _check(self._lib.gwamd_poa_synchronize(self._handle))
+
+    def get_consensus(self):
+        """cudapoa.pyx:226-245: (consensus list, coverage list, status list)."""
+        n = self.total_poas
+        status = (C.c_int32 * max(n, 1))()
+        lens = (C.c_int32 * max(n, 1))()
+        cbase, vbase, stride = C.c_void_p(), C.c_void_p(), C.c_int32()
+        rc = _check(self._lib.gwamd_poa_get_consensus(self._handle, status, lens, C.byref(cbase), C.byref(vbase),
+                                                      C.byref(stride)))
+        if rc == OUTPUT_TYPE_UNAVAILABLE:
+            raise RuntimeError("Output type not requested during batch initialization")
+        cons, covs = [], []
+        for i in range(n):
+            L = lens[i]
+            if L > 0:
+                cons.append(C.string_at(cbase.value + i * stride.value, L).decode())
+                buf = (C.c_uint16 * L).from_address(vbase.value + 2 * i * stride.value)
+                covs.append(list(buf))
+            else:
+                cons.append("")
+                covs.append([])
+        return cons, covs, [status[i] for i in range(n)]
+
+    def get_msa(self):
+        """cudapoa.pyx:207-224: (list of per-window MSA row lists, status list)."""
+        n = self.total_poas
+        status = (C.c_int32 * max(n, 1))()
+        rows = (C.c_int32 * max(n, 1))()
+        base, rstride, mseq = C.c_void_p(), C.c_int32(), C.c_int32()
+        rc = _check(self._lib.gwamd_poa_get_msa(self._handle, status, rows, C.byref(base), C.byref(rstride),
+                                                C.byref(mseq)))
+        if rc == OUTPUT_TYPE_UNAVAILABLE:
+            raise RuntimeError("Output type not requested during batch initialization")
+        out = []
+        for i in range(n):
+            msa = []
+            for s in range(rows[i]):
+                msa.append(C.string_at(base.value + (i * mseq.value + s) * rstride.value).decode())
+            out.append(msa)
+        return out, [status[i] for i in range(n)]
+
+    def get_graphs(self):
+        """cudapoa.pyx:247-288: (list of DiGraph, status list)."""
+        n = self.total_poas
+        status = (C.c_int32 * max(n, 1))()
+        nodes = (C.c_int32 * max(n, 1))()
+        b, cnt, ie, iw = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+        mn = C.c_int32()
+        _check(self._lib.gwamd_poa_get_graphs(self._handle, status, nodes, C.byref(b), C.byref(cnt), C.byref(ie),
+                                              C.byref(iw), C.byref(mn)))
+        graphs = []
+        M = mn.value
+        for w in range(n):
+            g = DiGraph()
+            if status[w] == SUCCESS:
+                nn = nodes[w]
+                labels = C.string_at(b.value + w * M, nn)
+                counts = np.ctypeslib.as_array((C.c_uint16 * (nn or 1)).from_address(cnt.value + 2 * w * M))
+                edges = np.ctypeslib.as_array((C.c_int32 * (nn * MAX_EDGES or 1)).from_address(
+                    ie.value + 4 * w * M * MAX_EDGES))
+                wts = np.ctypeslib.as_array((C.c_uint16 * (nn * MAX_EDGES or 1)).from_address(
+                    iw.value + 2 * w * M * MAX_EDGES))
+                for v in range(nn):
+                    for e in range(int(counts[v])):
+                        g.add_edge(int(edges[v * MAX_EDGES + e]), v, weight=int(wts[v * MAX_EDGES + e]))
+                for v in g.nodes:
+                    g.add_node(v, chr(labels[v]) if v < nn else "")
+            graphs.append(g)
+        return graphs, [status[i] for i in range(n)]
+
+    def get_stats(self):
+        """Per-window DP cell counts and final node counts of the last run."""
+        n = self.total_poas
+        cells = np.zeros(max(n, 1), np.int64)
+        fn = np.zeros(max(n, 1), np.int32)
+        _check(self._lib.gwamd_poa_get_stats(self._handle, cells.ctypes.data_as(C.POINTER(C.c_int64)),
+                                             fn.ctypes.data_as(C.POINTER(C.c_int32))))
+        return cells[:n], fn[:n]
+
+    def get_types(self):
+        sb, zb = C.c_int32(), C.c_int32()
+        self._lib.gwamd_poa_get_types(self._handle, C.byref(sb), C.byref(zb))
+        return sb.value, zb.value
+
+    def get_capacity(self):
+        nb, mp = C.c_int64(), C.c_int32()
+        self._lib.gwamd_poa_get_capacity(self._handle, C.byref(nb), C.byref(mp))
+        return nb.value, mp.value
+
+    def reset(self):
+        self._lib.gwamd_poa_reset(self._handle)

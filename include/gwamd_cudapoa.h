@@ -1,0 +1,121 @@
+/*
+ * gwamd_cudapoa.h -- C ABI of the MI355X POA path (libgwamd.so).
+ *
+ * Plain C: opaque handles, plain pointers and sizes, no C++ or torch types.
+ * Each entry point replaces one method of the reference's C++ POA API, which
+ * is what the reference's own FFI (pygenomeworks Cython,
+ * pygenomeworks/genomeworks/cudapoa/cudapoa.pxd) binds:
+ *
+ *   gwamd_poa_batch_size_init       BatchSize(max_seq, max_seq_per_poa, band)      batch.hpp:74-95
+ *   gwamd_poa_batch_size_init_full  BatchSize(6 args)                              batch.hpp:97-128
+ *   gwamd_poa_create_batch          create_batch(...)                              batch.hpp:220-228
+ *   gwamd_poa_destroy_batch         ~Batch                                         batch.hpp:137
+ *   gwamd_poa_add_poa_group         Batch::add_poa_group                           batch.hpp:153-154
+ *   gwamd_poa_get_total_poas        Batch::get_total_poas                          batch.hpp:159
+ *   gwamd_poa_generate_poa          Batch::generate_poa                            batch.hpp:162
+ *   gwamd_poa_get_consensus         Batch::get_consensus                           batch.hpp:174-176
+ *   gwamd_poa_get_msa               Batch::get_msa                                 batch.hpp:186-187
+ *   gwamd_poa_get_graphs            Batch::get_graphs                              batch.hpp:195-196
+ *   gwamd_poa_batch_id              Batch::batch_id                                batch.hpp:201
+ *   gwamd_poa_reset                 Batch::reset                                   batch.hpp:204
+ *
+ * Extra entry points (no reference counterpart; used by bench.py): split
+ * generate_poa into its H2D copy and its kernel launch, and read per-window
+ * work counters.
+ *
+ * Error convention: functions returning int32_t return a StatusType value
+ * (cudapoa.hpp:26-38) >= 0, or a negative GWAMD_E_* code when the reference
+ * would have thrown (message in gwamd_last_error()).
+ */
+#ifndef GWAMD_CUDAPOA_H
+#define GWAMD_CUDAPOA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GWAMD_E_INVALID_ARGUMENT (-1) /* reference: std::invalid_argument */
+#define GWAMD_E_RUNTIME (-2)          /* reference: std::runtime_error    */
+#define GWAMD_E_HIP (-3)              /* HIP runtime failure              */
+
+typedef struct gwamd_poa_batch gwamd_poa_batch;
+
+/* Mirror of cudapoa::BatchSize (batch.hpp:53-71), same field order. */
+typedef struct gwamd_poa_batch_size
+{
+    int32_t max_sequence_size;
+    int32_t max_consensus_size;
+    int32_t max_nodes_per_window;
+    int32_t max_nodes_per_window_banded;
+    int32_t max_matrix_graph_dimension;
+    int32_t max_matrix_graph_dimension_banded;
+    int32_t max_matrix_sequence_dimension;
+    int32_t alignment_band_width;
+    int32_t max_sequences_per_poa;
+} gwamd_poa_batch_size;
+
+/* Last error message of the calling thread ("" if none). */
+const char* gwamd_last_error(void);
+
+int32_t gwamd_poa_batch_size_init(gwamd_poa_batch_size* out, int32_t max_seq_sz, int32_t max_seq_per_poa,
+                                  int32_t band_width);
+int32_t gwamd_poa_batch_size_init_full(gwamd_poa_batch_size* out, int32_t max_seq_sz, int32_t max_consensus_sz,
+                                       int32_t max_nodes_per_w, int32_t max_nodes_per_w_banded, int32_t band_width,
+                                       int32_t max_seq_per_poa);
+
+/* stream: a hipStream_t (NULL = default stream). */
+int32_t gwamd_poa_create_batch(gwamd_poa_batch** out, int32_t device_id, void* stream, size_t max_mem,
+                               int8_t output_mask, const gwamd_poa_batch_size* batch_size, int16_t gap_score,
+                               int16_t mismatch_score, int16_t match_score, int32_t cuda_banded_alignment);
+void gwamd_poa_destroy_batch(gwamd_poa_batch* batch);
+
+/* One group = n entries; weights[i] may be NULL (all ones).  per_seq_status
+ * receives n StatusType values.  Returns the group's StatusType. */
+int32_t gwamd_poa_add_poa_group(gwamd_poa_batch* batch, const char* const* seqs, const int8_t* const* weights,
+                                const int32_t* lengths, int32_t n, int32_t* per_seq_status);
+int32_t gwamd_poa_get_total_poas(const gwamd_poa_batch* batch);
+int32_t gwamd_poa_generate_poa(gwamd_poa_batch* batch);
+
+/* Blocks on the stream.  status/lengths receive get_total_poas() entries; the
+ * consensus of window i is cons_base[i*stride .. +lengths[i]) and its coverage
+ * cov_base[i*stride ..].  Buffers stay valid until the next generate/reset. */
+int32_t gwamd_poa_get_consensus(gwamd_poa_batch* batch, int32_t* status, int32_t* lengths, const char** cons_base,
+                                const uint16_t** cov_base, int32_t* stride);
+
+/* Blocks on the stream.  Row s of window i is the NUL-terminated string at
+ * msa_base + (i*max_seqs + s)*row_stride; num_rows[i] = reads in window i. */
+int32_t gwamd_poa_get_msa(gwamd_poa_batch* batch, int32_t* status, int32_t* num_rows, const char** msa_base,
+                          int32_t* row_stride, int32_t* max_seqs);
+
+/* Blocks on the stream.  Window i has num_nodes[i] nodes; node v's label is
+ * bases[i*max_nodes + v]; its incoming edges (src, weight) are
+ * in_edges/in_weights[(i*max_nodes + v)*50 + e] for e < in_count[i*max_nodes+v].
+ * Caller arrays: status, num_nodes sized get_total_poas(); the rest are
+ * returned as pointers to batch-owned host memory. */
+int32_t gwamd_poa_get_graphs(gwamd_poa_batch* batch, int32_t* status, int32_t* num_nodes, const uint8_t** bases,
+                             const uint16_t** in_count, const int32_t** in_edges, const uint16_t** in_weights,
+                             int32_t* max_nodes);
+
+int32_t gwamd_poa_batch_id(const gwamd_poa_batch* batch);
+void gwamd_poa_reset(gwamd_poa_batch* batch);
+
+/* bench.py helpers: generate_poa == upload + launch. */
+int32_t gwamd_poa_upload(gwamd_poa_batch* batch);
+int32_t gwamd_poa_launch(gwamd_poa_batch* batch);
+int32_t gwamd_poa_synchronize(gwamd_poa_batch* batch);
+/* Per-window DP cells (sum over reads of (|V|+1)*(|r|+1), banded: band cells)
+ * and final node counts of the last generate; arrays sized get_total_poas(). */
+int32_t gwamd_poa_get_stats(gwamd_poa_batch* batch, int64_t* cells, int32_t* final_nodes);
+/* Score/size types chosen by create_batch (16 or 32 bits each). */
+int32_t gwamd_poa_get_types(const gwamd_poa_batch* batch, int32_t* score_bits, int32_t* size_bits);
+/* Device bytes allocated by the batch and its window capacity (max_poas). */
+int32_t gwamd_poa_get_capacity(const gwamd_poa_batch* batch, int64_t* device_bytes, int32_t* max_poas);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GWAMD_CUDAPOA_H */

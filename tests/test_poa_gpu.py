@@ -1,0 +1,190 @@
+"""GPU parity tests for the POA path: the HIP kernels (through the C ABI of
+libgwamd.so) against the CPU restatement (oracle/) and the reference KATs.
+Bit-exact: consensus strings, coverage vectors, MSA rows, graphs, statuses."""
+import json
+import os
+
+import pytest
+
+from claragenomicsanalysis_amd import synth
+from claragenomicsanalysis_amd.cudapoa import CudaPoaBatch
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "poa_kat.json")))
+MEM = 8 << 30
+
+
+def _batch(name):
+    return [b for b in GOLD["batch"] if b["name"] == name][0]
+
+
+def run_gpu(windows, max_seq, max_seqs, banded=False, bw=256, output_type="consensus", mem=MEM, **kw):
+    b = CudaPoaBatch(max_seqs, max_seq, mem, output_type=output_type, cuda_banded_alignment=banded,
+                     alignment_band_width=bw, **kw)
+    for w in windows:
+        st, seq_st = b.add_poa_group(list(w))
+        assert st == 0
+    b.generate_poa()
+    return b
+
+
+def run_oracle(w, max_seq, max_seqs, banded=False, bw=256, msa=False, score_bits=16, **kw):
+    mn = kw.get("max_nodes", ((4 if banded else 3) * max_seq + 3) // 4 * 4)
+    return oracle.poa_window(w, banded=banded, band_width=bw, msa=msa, score_bits=score_bits,
+                             max_nodes=mn, max_consensus=kw.get("max_consensus", 2 * max_seq), max_seqs=max_seqs,
+                             want_graph=kw.get("want_graph", False))
+
+
+def test_kat_all_A():
+    case = _batch("all_A_1023x3")
+    b = run_gpu(case["windows"], 1024, 10)
+    cons, cov, st = b.get_consensus()
+    assert st == [0]
+    assert cons == case["consensus"]
+
+
+def test_kat_python_graph():
+    case = _batch("py_graph")
+    b = run_gpu(case["windows"], 1024, 10)
+    graphs, st = b.get_graphs()
+    assert st == [0]
+    assert graphs[0].number_of_nodes() == 10
+    assert graphs[0].number_of_edges() == 11
+
+
+def test_kat_python_seed2():
+    case = _batch("py_complex_seed2")
+    b = run_gpu(case["windows"], 1024, 1000)
+    cons, cov, st = b.get_consensus()
+    assert st == [0]
+    assert cons[0] == case["consensus"][0]
+
+
+def test_kat_python_simple():
+    case = _batch("py_simple")
+    for banded in (False, True):
+        b = run_gpu(case["windows"], 1024, 10, banded=banded)
+        cons, cov, st = b.get_consensus()
+        assert len(cons) == 2 and b.total_poas == 2
+        for w, c, v, s in zip(case["windows"], cons, cov, st):
+            r = run_oracle(w, 1024, 10, banded=banded)
+            assert (s, c, v) == (r.status, r.consensus, r.coverage)
+
+
+@pytest.mark.parametrize("L,nreads,nwin,err", [(60, 6, 32, 5), (300, 12, 24, 20), (1000, 32, 8, 50)])
+def test_full_parity_synthetic(L, nreads, nwin, err):
+    wins = synth.poa_windows(7, nwin, L, nreads, err, err, err)
+    max_seq = L + err + 8
+    b = run_gpu(wins, max_seq, nreads)
+    cons, cov, st = b.get_consensus()
+    cells, _ = b.get_stats()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, max_seq, nreads)
+        assert st[i] == r.status, i
+        assert cons[i] == r.consensus, i
+        assert cov[i] == r.coverage, i
+        assert cells[i] == r.cells, i
+
+
+def test_full_parity_int32_scores():
+    # max_sequence_size large enough that use32bitScore selects int32
+    wins = synth.poa_windows(11, 6, 400, 10, 20, 20, 20)
+    b = run_gpu(wins, 4200, 10)
+    assert b.get_types()[0] == 32
+    cons, cov, st = b.get_consensus()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 4200, 10)
+        assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage)
+
+
+@pytest.mark.parametrize("bw", [128, 256])
+def test_banded_parity_synthetic(bw):
+    wins = synth.poa_windows(21, 12, 600, 10, 30, 30, 30)
+    max_seq = 700
+    b = run_gpu(wins, max_seq, 10, banded=True, bw=bw)
+    sbits = b.get_types()[0]
+    cons, cov, st = b.get_consensus()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, max_seq, 10, banded=True, bw=bw, score_bits=sbits)
+        assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), i
+
+
+def test_msa_parity_synthetic():
+    wins = synth.poa_windows(31, 8, 300, 8, 15, 15, 15)
+    b = run_gpu(wins, 400, 8, output_type="msa")
+    msa, st = b.get_msa()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 400, 8, msa=True)
+        assert st[i] == r.status
+        assert msa[i] == r.msa
+        # de-gapped rows equal the inputs (Test_CudapoaGenerateMSA2.cu:125-140)
+        assert [row.replace("-", "") for row in msa[i]] == [x.decode() for x in w]
+
+
+def test_banded_msa_parity():
+    wins = synth.poa_windows(41, 4, 500, 6, 25, 25, 25)
+    b = run_gpu(wins, 600, 6, banded=True, output_type="msa")
+    sbits = b.get_types()[0]
+    msa, st = b.get_msa()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 600, 6, banded=True, msa=True, score_bits=sbits)
+        assert (st[i], msa[i]) == (r.status, r.msa)
+
+
+def test_graph_parity():
+    wins = synth.poa_windows(51, 4, 200, 6, 10, 10, 10)
+    b = run_gpu(wins, 300, 6)
+    graphs, st = b.get_graphs()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 300, 6, want_graph=True)
+        g = graphs[i]
+        expect = {(src, v): wt for v, ins in enumerate(r.graph["in"]) for (src, wt) in ins}
+        got = {(u, v): g.weight(u, v) for (u, v) in g.edges}
+        assert got == expect
+        assert "".join(g.label(v) for v in range(r.final_nodes)) == r.graph["bases"]
+
+
+def test_single_read_and_status_codes():
+    b = CudaPoaBatch(4, 64, MEM)
+    st, seq_st = b.add_poa_group(["ACGTACGT"])
+    assert (st, seq_st) == (0, [0])
+    st, seq_st = b.add_poa_group(["A" * 65, "ACGT", "ACGA", "ACGG", "ACGC"])
+    assert st == 0
+    assert seq_st == [2, 0, 0, 0, 3]  # too long; ...; exceeded_maximum_sequences_per_poa
+    b.generate_poa()
+    cons, cov, st = b.get_consensus()
+    assert cons[0] == "ACGTACGT" and cov[0] == [1] * 8 and st[0] == 0
+    r = oracle.poa_window([b"ACGT", b"ACGA", b"ACGG"], max_nodes=192, max_consensus=128)
+    assert (st[1], cons[1], cov[1]) == (r.status, r.consensus, r.coverage)
+
+
+def test_node_limit_error_matches_oracle():
+    # tiny node capacity forces node_count_exceeded_maximum_graph_size
+    wins = synth.poa_windows(61, 3, 100, 8, 20, 20, 20)
+    b = CudaPoaBatch(8, 130, MEM, max_nodes_per_window=140)
+    for w in wins:
+        b.add_poa_group(list(w))
+    b.generate_poa()
+    cons, cov, st = b.get_consensus()
+    for i, w in enumerate(wins):
+        r = oracle.poa_window(w, max_nodes=140, max_consensus=260, max_seqs=8)
+        assert (st[i], cons[i]) == (r.status, r.consensus)
+    assert any(s == 4 for s in st)
+
+
+def test_output_type_unavailable_and_reset():
+    b = CudaPoaBatch(4, 64, MEM, output_type="consensus")
+    b.add_poa_group(["ACGT", "ACGT"])
+    b.generate_poa()
+    with pytest.raises(RuntimeError):
+        b.get_msa()
+    assert b.total_poas == 1
+    b.reset()
+    assert b.total_poas == 0
+
+
+def test_zero_memory_throws():
+    with pytest.raises(RuntimeError):
+        CudaPoaBatch(5, 1024, 0)
