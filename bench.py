@@ -129,6 +129,7 @@ def main():
     # outputs + work counters (outside the timed region)
     cons, cov, status = batch.get_consensus()
     cells, final_nodes = batch.get_stats()
+    ticks = batch.get_phase_ticks()  # last launch, 100 MHz
     n_ok = int(sum(1 for s in status if s == 0))
     sb = score_bits // 8
     cells_total = int(cells.sum())
@@ -166,7 +167,7 @@ def main():
         parity = {"windows_checked": k, "bit_exact_vs_oracle": bool(ok)}
         if not args.no_cpu and world == 1:
             th = cpu_threads()
-            ns = args.cpu_sample or min(nwin, max(th * 4, 16))
+            ns = args.cpu_sample or min(nwin, max(th * 48, 64))
             tc = time.perf_counter()
             ccons, cst, _, used = oracle.poa_batch(windows[:ns], nthreads=th, banded=cfg["banded"],
                                                    band_width=cfg["bw"], score_bits=score_bits, max_nodes=mn,
@@ -212,7 +213,9 @@ def main():
                        "windows_ok": n_ok, "dp_cells_per_step": cells_total,
                        "gcups": round(cells_total / kernel_s / 1e9, 3),
                        "mean_final_nodes": round(float(np.mean(final_nodes)), 1),
-                       "gather_ms": gather_ms, "input_gen_s": round(gen_s, 2)},
+                       "gather_ms": gather_ms, "input_gen_s": round(gen_s, 2),
+                       "phase_ms_mean_per_window": {name: round(float(ticks[:, i].mean()) / 1e5, 3)
+                                                    for i, name in enumerate(batch.PHASES)}},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "poa_window_kernel", "kernel_ms": round(kernel_ms, 3),

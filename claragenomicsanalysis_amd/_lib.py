@@ -59,6 +59,8 @@ def _declare(L):
     L.gwamd_poa_get_graphs.argtypes = [vp, P(i32), P(i32), P(vp), P(vp), P(vp), P(vp), P(i32)]
     L.gwamd_poa_get_stats.restype = i32
     L.gwamd_poa_get_stats.argtypes = [vp, P(i64), P(i32)]
+    L.gwamd_poa_get_phase_ticks.restype = i32
+    L.gwamd_poa_get_phase_ticks.argtypes = [vp, P(i64)]
     L.gwamd_poa_get_types.restype = i32
     L.gwamd_poa_get_types.argtypes = [vp, P(i32), P(i32)]
     L.gwamd_poa_get_capacity.restype = i32

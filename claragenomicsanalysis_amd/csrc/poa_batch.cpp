@@ -465,6 +465,16 @@ public:
     int64_t device_bytes() const { return int64_t(d_slab_.n + d_seqs_.n + d_wts_.n + d_len_.n + d_off_.n + d_win_.n); }
     int32_t max_poas() const { return max_poas_; }
 
+    void get_phases(int64_t* out)
+    {
+        ScopedDevice dev(device_id_);
+        if (poa_count_ == 0)
+            return;
+        GWAMD_HIP_CHECK(hipMemcpyAsync(out, bufs_.phase, size_t(poa_count_) * 8 * gwamd::poa::kPhases,
+                                       hipMemcpyDeviceToHost, stream_));
+        GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+
     void get_stats(int64_t* cells, int32_t* final_nodes)
     {
         ScopedDevice dev(device_id_);
@@ -554,6 +564,7 @@ private:
             {reinterpret_cast<void**>(&bufs_.msa_len), align8(P * 4)},
             {reinterpret_cast<void**>(&bufs_.final_nodes), align8(P * 4)},
             {reinterpret_cast<void**>(&bufs_.cells), align8(P * 8)},
+            {reinterpret_cast<void**>(&bufs_.phase), align8(P * 8 * gwamd::poa::kPhases)},
             {msa ? reinterpret_cast<void**>(&bufs_.edge_cov) : &dummy, msa ? align8(P * mn * E * S * 2) : 0},
             {msa ? reinterpret_cast<void**>(&bufs_.edge_cov_cnt) : &dummy, msa ? align8(P * mn * E * 2) : 0},
             {msa ? &bufs_.seq_begin : &dummy, msa ? align8(P * S * sz) : 0},
@@ -958,6 +969,14 @@ int32_t gwamd_poa_get_stats(gwamd_poa_batch* batch, int64_t* cells, int32_t* fin
     return guarded([&] {
         batch->impl->get_stats(cells, final_nodes);
         return 0;
+    });
+}
+
+int32_t gwamd_poa_get_phase_ticks(gwamd_poa_batch* batch, int64_t* ticks)
+{
+    return guarded([&] {
+        batch->impl->get_phases(ticks);
+        return int32_t(gwamd::poa::kPhases);
     });
 }
 

@@ -101,6 +101,20 @@ struct Buffers
     int32_t* msa_len;   // per window
     int32_t* final_nodes;
     int64_t* cells;     // per window: sum over reads of (|V|+1)*(|r|+1) (or band cells)
+    int64_t* phase;     // per window kPhases counters of s_memrealtime ticks (100 MHz)
+};
+
+// Phase counters written per window (diagnostics, bench.py "phases").
+enum Phase
+{
+    kPhBackbone = 0,
+    kPhForward,
+    kPhTraceback,
+    kPhAdd,
+    kPhTopsort,
+    kPhOutput,
+    kPhTotal,
+    kPhases
 };
 
 struct Scores

@@ -44,6 +44,11 @@ struct WinGraph
     int32_t max_nodes;
 };
 
+__device__ __forceinline__ uint64_t now_ticks()
+{
+    return __builtin_amdgcn_s_memrealtime();
+}
+
 __device__ __forceinline__ int uniform(int x)
 {
     return __builtin_amdgcn_readfirstlane(x);
@@ -975,6 +980,14 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
     uint16_t* ecovc  = MSA ? b.edge_cov_cnt + w * mn * kMaxEdges : nullptr;
     SizeT* seq_begin = MSA ? static_cast<SizeT*>(b.seq_begin) + size_t(w) * d.max_seqs : nullptr;
 
+    uint64_t ph[kPhases] = {0, 0, 0, 0, 0, 0, 0};
+    const uint64_t t_begin = now_ticks();
+    uint64_t t_mark        = t_begin;
+    auto lap = [&](int p) {
+        uint64_t t = now_ticks();
+        ph[p] += t - t_mark;
+        t_mark = t;
+    };
     const WindowDesc wd = b.windows[w];
     const int nseq      = wd.num_seqs;
     int status          = kSuccess;
@@ -988,6 +1001,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
         const int8_t* w0    = b.wts + b.seq_off[wd.first_seq];
         build_backbone<SizeT, MSA>(g, seq0, w0, len0, lane, ecov, ecovc, seq_begin, d.max_seqs);
         node_count = len0;
+        lap(kPhBackbone);
         for (int s = 1; s < nseq; s++)
         {
             if (node_count >= d.max_nodes) // cudapoa_kernels.cuh:222-227
@@ -1016,6 +1030,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
                 cells += int64_t(V + 1) * (d.band_width + kBandPad);
                 nw_forward_banded<ScoreT, SizeT>(g, V, lds_read, L, S, B, sc, lane);
                 __syncthreads();
+                lap(kPhForward);
                 if (lane == 0)
                     sh_alen = traceback_banded<ScoreT, SizeT>(g, V, lds_read, L, S, B, sc, ag, ar, d.aln_cap);
             }
@@ -1024,11 +1039,13 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
                 cells += int64_t(V + 1) * (L + 1);
                 nw_forward_full<ScoreT, SizeT>(g, V, lds_read, L, S, d.score_stride, sc, lane);
                 __syncthreads();
+                lap(kPhForward);
                 if (lane == 0)
                     sh_alen = traceback_full<ScoreT, SizeT>(g, V, lds_read, L, S, d.score_stride, sc, ag, ar,
                                                             d.aln_cap);
             }
             __syncthreads();
+            lap(kPhTraceback);
             alen = sh_alen;
             if (alen == -1)
             {
@@ -1040,8 +1057,10 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
                 int nc     = node_count;
                 uint8_t rc = add_alignment<SizeT, MSA>(g, nc, ag, ar, alen, read_g, wts_g, s, ecov, ecovc, seq_begin,
                                                        d.max_seqs);
+                lap(kPhAdd);
                 if (rc == kSuccess)
                     topsort_kahn<SizeT>(g, nc, cscore);
+                lap(kPhTopsort);
                 sh_status = rc;
                 sh_len    = nc;
             }
@@ -1176,8 +1195,15 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
             b.msa_status[w] = uint8_t(mst);
         }
     }
+    lap(kPhOutput);
     if (lane == 0)
     {
+        if (b.phase)
+        {
+            ph[kPhTotal] = now_ticks() - t_begin;
+            for (int p = 0; p < kPhases; p++)
+                b.phase[size_t(w) * kPhases + p] = int64_t(ph[p]);
+        }
         b.final_nodes[w] = node_count;
         b.cells[w]       = cells;
     }

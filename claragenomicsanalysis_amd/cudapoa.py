@@ -269,6 +269,15 @@ class CudaPoaBatch:
                                              fn.ctypes.data_as(C.POINTER(C.c_int32))))
         return cells[:n], fn[:n]
 
+    PHASES = ("backbone", "forward", "traceback", "add", "topsort", "output", "total")
+
+    def get_phase_ticks(self):
+        """Per-window in-kernel phase timers (s_memrealtime ticks at 100 MHz), shape (n, 7)."""
+        n = self.total_poas
+        out = np.zeros((max(n, 1), len(self.PHASES)), np.int64)
+        _check(self._lib.gwamd_poa_get_phase_ticks(self._handle, out.ctypes.data_as(C.POINTER(C.c_int64))))
+        return out[:n]
+
     def get_types(self):
         sb, zb = C.c_int32(), C.c_int32()
         self._lib.gwamd_poa_get_types(self._handle, C.byref(sb), C.byref(zb))

@@ -109,6 +109,10 @@ int32_t gwamd_poa_synchronize(gwamd_poa_batch* batch);
 /* Per-window DP cells (sum over reads of (|V|+1)*(|r|+1), banded: band cells)
  * and final node counts of the last generate; arrays sized get_total_poas(). */
 int32_t gwamd_poa_get_stats(gwamd_poa_batch* batch, int64_t* cells, int32_t* final_nodes);
+/* Per-window phase timers of the last launch (s_memrealtime ticks, 100 MHz):
+ * backbone, forward DP, traceback, add, topsort, output, total; ticks receives
+ * 7 * get_total_poas() values.  Returns the number of phases. */
+int32_t gwamd_poa_get_phase_ticks(gwamd_poa_batch* batch, int64_t* ticks);
 /* Score/size types chosen by create_batch (16 or 32 bits each). */
 int32_t gwamd_poa_get_types(const gwamd_poa_batch* batch, int32_t* score_bits, int32_t* size_bits);
 /* Device bytes allocated by the batch and its window capacity (max_poas). */

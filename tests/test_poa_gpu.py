@@ -20,7 +20,9 @@ def _batch(name):
     return [b for b in GOLD["batch"] if b["name"] == name][0]
 
 
-def run_gpu(windows, max_seq, max_seqs, banded=False, bw=256, output_type="consensus", mem=MEM, **kw):
+def run_gpu(windows, max_seq, max_seqs, banded=False, bw=None, output_type="consensus", mem=MEM, **kw):
+    if bw is None:  # BatchSize requires band width <= max_sequence_size (batch.hpp:126)
+        bw = 256 if max_seq >= 256 else 128
     b = CudaPoaBatch(max_seqs, max_seq, mem, output_type=output_type, cuda_banded_alignment=banded,
                      alignment_band_width=bw, **kw)
     for w in windows:
@@ -76,7 +78,7 @@ def test_kat_python_simple():
 @pytest.mark.parametrize("L,nreads,nwin,err", [(60, 6, 32, 5), (300, 12, 24, 20), (1000, 32, 8, 50)])
 def test_full_parity_synthetic(L, nreads, nwin, err):
     wins = synth.poa_windows(7, nwin, L, nreads, err, err, err)
-    max_seq = L + err + 8
+    max_seq = max(L + err + 8, 128)
     b = run_gpu(wins, max_seq, nreads)
     cons, cov, st = b.get_consensus()
     cells, _ = b.get_stats()
@@ -147,23 +149,24 @@ def test_graph_parity():
 
 
 def test_single_read_and_status_codes():
-    b = CudaPoaBatch(4, 64, MEM)
+    b = CudaPoaBatch(4, 128, MEM, alignment_band_width=128)
     st, seq_st = b.add_poa_group(["ACGTACGT"])
     assert (st, seq_st) == (0, [0])
-    st, seq_st = b.add_poa_group(["A" * 65, "ACGT", "ACGA", "ACGG", "ACGC"])
+    st, seq_st = b.add_poa_group(["A" * 129, "ACGT", "ACGA", "ACGG", "ACGC", "ACGT"])
     assert st == 0
-    assert seq_st == [2, 0, 0, 0, 3]  # too long; ...; exceeded_maximum_sequences_per_poa
+    # too long (not added); four added; exceeded_maximum_sequences_per_poa (cudapoa_batch.cuh:490-510)
+    assert seq_st == [2, 0, 0, 0, 0, 3]
     b.generate_poa()
     cons, cov, st = b.get_consensus()
     assert cons[0] == "ACGTACGT" and cov[0] == [1] * 8 and st[0] == 0
-    r = oracle.poa_window([b"ACGT", b"ACGA", b"ACGG"], max_nodes=192, max_consensus=128)
+    r = oracle.poa_window([b"ACGT", b"ACGA", b"ACGG", b"ACGC"], max_nodes=384, max_consensus=256)
     assert (st[1], cons[1], cov[1]) == (r.status, r.consensus, r.coverage)
 
 
 def test_node_limit_error_matches_oracle():
     # tiny node capacity forces node_count_exceeded_maximum_graph_size
     wins = synth.poa_windows(61, 3, 100, 8, 20, 20, 20)
-    b = CudaPoaBatch(8, 130, MEM, max_nodes_per_window=140)
+    b = CudaPoaBatch(8, 130, MEM, max_nodes_per_window=140, alignment_band_width=128)
     for w in wins:
         b.add_poa_group(list(w))
     b.generate_poa()
@@ -175,7 +178,7 @@ def test_node_limit_error_matches_oracle():
 
 
 def test_output_type_unavailable_and_reset():
-    b = CudaPoaBatch(4, 64, MEM, output_type="consensus")
+    b = CudaPoaBatch(4, 128, MEM, output_type="consensus", alignment_band_width=128)
     b.add_poa_group(["ACGT", "ACGT"])
     b.generate_poa()
     with pytest.raises(RuntimeError):
