@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <iomanip>
 #include <sstream>
@@ -198,6 +199,7 @@ public:
         dims_.score_rows    = dims_.max_nodes + 2;
         dims_.aln_cap       = dims_.max_nodes + bs_.max_sequence_size + 4;
         dims_.want_consensus = (output_mask_ & OutputType::consensus) ? 1 : 0;
+        plan_lds_kernel();
         const int64_t own = own_bytes_per_window(sz, sbytes, msa);
         if (own > 0)
             max_poas = std::min<int64_t>(max_poas, int64_t(max_mem) / own);
@@ -219,7 +221,7 @@ public:
     ~PoaBatch() override
     {
         (void)hipSetDevice(device_id_);
-        for (auto* b : {&d_seqs_, &d_wts_, &d_len_, &d_off_, &d_win_, &d_slab_})
+        for (auto* b : {&d_seqs_, &d_wts_, &d_len_, &d_off_, &d_win_, &d_slab_, &d_codes_})
             if (b->p)
                 (void)hipFree(b->p);
     }
@@ -462,7 +464,8 @@ public:
     const std::vector<int32_t>& host_final_nodes() const { return h_final_nodes_; }
     int32_t window_num_seqs(int32_t w) const { return h_win_.as<const gwamd::poa::WindowDesc>()[w].num_seqs; }
     int8_t output_mask() const { return output_mask_; }
-    int64_t device_bytes() const { return int64_t(d_slab_.n + d_seqs_.n + d_wts_.n + d_len_.n + d_off_.n + d_win_.n); }
+    int64_t device_bytes() const { return int64_t(d_slab_.n + d_codes_.n + d_seqs_.n + d_wts_.n + d_len_.n + d_off_.n + d_win_.n); }
+    int32_t kernel_kind() const { return dims_.lds_kernel ? 2 : 1; }
     int32_t max_poas() const { return max_poas_; }
 
     void get_phases(int64_t* out)
@@ -494,7 +497,9 @@ private:
         b += align8(mn) + 4 * align8(mn * 2) + align8(mn * E * 2);   // base, counts, coverage, in_w
         b += 3 * align8(mn * E * sz) + 2 * align8(mn * sz);           // in_e, out_e, aln, sorted, pos
         b += 2 * align8(int64_t(dims_.aln_cap) * sz);                 // ag, ar
-        b += int64_t(dims_.score_rows) * dims_.score_stride * sbytes; // scores
+        b += int64_t(dims_.score_rows) * dims_.score_stride * sbytes; // scores (LDS kernel: spill rows)
+        if (dims_.lds_kernel)
+            b += int64_t(dims_.score_rows) * dims_.code_stride;           // traceback codes
         b += align8(mn * 4) + align8(mn * 4 * sz);                    // cscore, cpred
         b += align8(dims_.max_consensus) + align8(int64_t(dims_.max_consensus) * 2) + 32; // outputs
         b += int64_t(S) * dims_.max_seq_len * 2 + S * 12;             // inputs
@@ -502,6 +507,41 @@ private:
             b += align8(mn * E * S * 2) + align8(mn * E * 2) + align8(S * sz) +
                  align8(S * int64_t(dims_.max_consensus));
         return b;
+    }
+
+    // LDS-resident kernel (poa_window_kernel_lds): full alignment with 16-bit
+    // scores and node ids.  LDS image: read | ring (>= one traceback tile) |
+    // row program | extra predecessor list, sized to keep 4 workgroups per CU
+    // (40 KiB) when the window limits allow it.
+    void plan_lds_kernel()
+    {
+        dims_.lds_kernel = 0;
+        const char* env  = std::getenv("GWAMD_POA_KERNEL");
+        if (env && std::string(env) == "v1")
+            return;
+        if (banded_ || score_bits_ != 16 || size_bits_ != 16)
+            return;
+        auto a16             = [](int64_t v) { return (v + 15) & ~int64_t(15); };
+        const int ring_rows  = 8;
+        const int64_t read_b = a16(int64_t(dims_.max_seq_len) + 32);
+        const int64_t ring_b = std::max<int64_t>(int64_t(ring_rows) * dims_.score_stride * 2,
+                                                 int64_t(gwamd::poa::kTileRows) * gwamd::poa::kTileCols);
+        const int64_t rec_b  = a16(int64_t(dims_.max_nodes + 1) * 4);
+        const int64_t fixed  = read_b + ring_b + rec_b;
+        const int64_t target = 40960;
+        int64_t xl_cap       = std::max<int64_t>(1024, (target - fixed) / 2);
+        xl_cap               = std::min<int64_t>(xl_cap, 65535);
+        const int64_t total  = fixed + a16(xl_cap * 2);
+        if (total > 65536)
+            return;
+        dims_.lds_kernel    = 1;
+        dims_.lds_ring_off  = int32_t(read_b);
+        dims_.lds_ring_rows = ring_rows;
+        dims_.lds_rec_off   = int32_t(read_b + ring_b);
+        dims_.lds_xl_off    = int32_t(read_b + ring_b + rec_b);
+        dims_.lds_xl_cap    = int32_t(xl_cap);
+        dims_.lds_bytes     = int32_t(total);
+        dims_.code_stride   = int32_t(a16(int64_t(dims_.max_seq_len) + 16));
     }
 
     // Non-score bytes of the reference slab for max_poas windows
@@ -588,6 +628,13 @@ private:
             cur += it.bytes;
         }
         bufs_.scores = base + sc_off;
+        if (dims_.lds_kernel)
+        {
+            const size_t code_bytes = size_t(P) * size_t(dims_.score_rows) * size_t(dims_.code_stride);
+            GWAMD_HIP_CHECK(hipMalloc(&d_codes_.p, code_bytes));
+            d_codes_.n   = code_bytes;
+            bufs_.codes = static_cast<uint8_t*>(d_codes_.p);
+        }
         // inputs (allocate_block.hpp:84: max_poas * max_seqs * max_seq bytes)
         const int64_t in_bytes = P * S * dims_.max_seq_len + 64;
         d_seqs_.n              = size_t(in_bytes);
@@ -696,7 +743,7 @@ private:
     int32_t bid_        = 0;
     gwamd::poa::Dims dims_{};
     gwamd::poa::Buffers bufs_{};
-    DevBuf d_seqs_, d_wts_, d_len_, d_off_, d_win_, d_slab_;
+    DevBuf d_seqs_, d_wts_, d_len_, d_off_, d_win_, d_slab_, d_codes_;
     PinnedBuf h_seqs_, h_wts_, h_len_, h_off_, h_win_;
     std::vector<uint8_t> h_cons_, h_status_, h_msa_, h_msa_status_, h_g_bases_, h_g_in_e_raw_;
     std::vector<uint16_t> h_cov_, h_g_in_cnt_, h_g_in_w_;
@@ -984,7 +1031,7 @@ int32_t gwamd_poa_get_types(const gwamd_poa_batch* batch, int32_t* score_bits, i
 {
     *score_bits = batch->impl->score_bits();
     *size_bits  = batch->impl->size_bits();
-    return 0;
+    return batch->impl->kernel_kind();
 }
 
 int32_t gwamd_poa_get_capacity(const gwamd_poa_batch* batch, int64_t* device_bytes, int32_t* max_poas)

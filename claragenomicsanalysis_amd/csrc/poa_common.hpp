@@ -57,7 +57,20 @@ struct Dims
     int32_t aln_cap;       // traceback buffer capacity
     int32_t band_width;    // banded mode only
     int32_t want_consensus; // MSA kernels also emit the consensus when set
+    // LDS-resident kernel (full alignment, 16-bit scores): layout of the
+    // per-workgroup LDS image and the traceback-code matrix
+    int32_t lds_kernel;     // 1: launch the LDS-resident kernel
+    int32_t lds_bytes;      // dynamic LDS per workgroup
+    int32_t lds_ring_off;   // E-domain score rows ring (int16)
+    int32_t lds_ring_rows;  // power of two
+    int32_t lds_rec_off;    // per-row program (u32 per row)
+    int32_t lds_xl_off;     // extra predecessor rows (u16)
+    int32_t lds_xl_cap;
+    int32_t code_stride;    // bytes per traceback-code row
 };
+
+constexpr int kTileRows = 128; // traceback tile (codes) rows
+constexpr int kTileCols = 128; // traceback tile columns (bytes)
 
 // Device pointers of one batch (all batch-wide; per-window slots are derived
 // in-kernel).  SizeT-typed arrays are passed as void* and cast in the kernel.
@@ -84,7 +97,8 @@ struct Buffers
     void* pos;
     void* ag;
     void* ar;
-    void* scores;
+    void* scores;       // v1: score matrix; LDS kernel: E-domain spill rows
+    uint8_t* codes;     // LDS kernel: traceback codes, one byte per cell
     // consensus / topsort / msa scratch
     int32_t* cscore;
     void* cpred;

@@ -18,928 +18,143 @@
 #include <climits>
 #include <cstdint>
 
-#include "poa_common.hpp"
+#include "poa_device.hpp"
 
 namespace gwamd
 {
 namespace poa
 {
 
-constexpr int32_t kNeg = -(1 << 29); // "minus infinity" for int32 DP temporaries
-
-template <typename SizeT>
-struct WinGraph
-{
-    uint8_t* base;
-    uint16_t* in_cnt;
-    uint16_t* out_cnt;
-    uint16_t* aln_cnt;
-    uint16_t* cov;
-    uint16_t* in_w;
-    SizeT* in_e;
-    SizeT* out_e;
-    SizeT* aln;
-    SizeT* sorted;
-    SizeT* pos;
-    int32_t max_nodes;
-};
-
-__device__ __forceinline__ uint64_t now_ticks()
-{
-    return __builtin_amdgcn_s_memrealtime();
-}
-
-__device__ __forceinline__ int uniform(int x)
-{
-    return __builtin_amdgcn_readfirstlane(x);
-}
-
-// Exclusive max-scan across the 64 lanes (lane 0 gets kNeg).
-__device__ __forceinline__ int wave_excl_max(int v, int lane)
-{
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1)
-    {
-        int t = __shfl_up(v, d, kWave);
-        if (lane >= d)
-            v = max(v, t);
-    }
-    int e = __shfl_up(v, 1, kWave);
-    return lane == 0 ? kNeg : e;
-}
-
-__device__ __forceinline__ int wave_max(int v)
-{
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1)
-        v = max(v, __shfl_xor(v, d, kWave));
-    return v;
-}
-
-// Row of the score matrix for predecessor slot p of node (cudapoa_nw.cuh:103).
-template <typename SizeT>
-__device__ __forceinline__ int pred_row(const WinGraph<SizeT>& g, int node, int p)
-{
-    return int(g.pos[int(g.in_e[node * kMaxEdges + p])]) + 1;
-}
-
-// ---------------------------------------------------------------------------
-// Backbone from read 0 (cudapoa_kernels.cuh:171-209), lane-parallel.
+// Consensus and/or MSA of one finished window (cudapoa_generate_consensus.cuh:
+// 279-347, cudapoa_generate_msa.cuh:121-224).
 template <typename SizeT, bool MSA>
-__device__ void build_backbone(WinGraph<SizeT>& g, const uint8_t* seq, const int8_t* w, int len, int lane,
-                               uint16_t* ecov, uint16_t* ecov_cnt, SizeT* seq_begin, int max_seqs)
+__device__ void finish_window(const Buffers& b, const Dims& d, int w, int lane, WinGraph<SizeT>& g, int status,
+                              int nseq, int node_count, int32_t* cscore, SizeT* cpred, uint16_t* ecov,
+                              uint16_t* ecovc, SizeT* seq_begin, int& sh_len, int& sh_status)
 {
-    if (lane == 0)
+    uint8_t* cons_out = b.cons + size_t(w) * d.max_consensus;
+    const int graph_status = status;
+    if (!MSA || d.want_consensus)
     {
-        g.base[0]    = seq[0];
-        g.sorted[0]  = 0;
-        g.in_cnt[0]  = 0;
-        g.aln_cnt[0] = 0;
-        g.pos[0]     = 0;
-        g.in_w[0]    = uint16_t(int(w[0]));
-        g.cov[0]     = 1;
-        if (MSA)
-            seq_begin[0] = 0;
-    }
-    for (int n = 1 + lane; n < len; n += kWave)
-    {
-        g.base[n]                    = seq[n];
-        g.sorted[n]                  = SizeT(n);
-        g.out_e[(n - 1) * kMaxEdges] = SizeT(n);
-        g.out_cnt[n - 1]             = 1;
-        g.in_e[n * kMaxEdges]        = SizeT(n - 1);
-        g.in_w[n * kMaxEdges]        = uint16_t(int(w[n - 1]) + int(w[n]));
-        g.in_cnt[n]                  = 1;
-        g.aln_cnt[n]                 = 0;
-        g.pos[n]                     = SizeT(n);
-        g.cov[n]                     = 1;
-        if (MSA)
-        {
-            ecov[size_t(n - 1) * kMaxEdges * max_seqs] = 0;
-            ecov_cnt[(n - 1) * kMaxEdges]              = 1;
-        }
-    }
-    __syncthreads();
-    if (lane == 0 && len >= 1)
-        g.out_cnt[len - 1] = 0; // written last, as in the reference (:179 then loop)
-    __syncthreads();
-}
-
-// ---------------------------------------------------------------------------
-// Full-matrix NW forward pass (cudapoa_nw.cuh:165-327).  Rows are stored with
-// column j at index j + kColShift; lanes whose 8 columns all lie beyond the
-// read are masked (those cells never feed a valid cell).
-template <typename ScoreT>
-struct Pack8;
-template <>
-struct Pack8<int16_t>
-{
-    __device__ static void load(const int16_t* p, int (&v)[8])
-    {
-        uint4 q = *reinterpret_cast<const uint4*>(p);
-        v[0]    = int(int16_t(q.x & 0xffff));
-        v[1]    = int(int16_t(q.x >> 16));
-        v[2]    = int(int16_t(q.y & 0xffff));
-        v[3]    = int(int16_t(q.y >> 16));
-        v[4]    = int(int16_t(q.z & 0xffff));
-        v[5]    = int(int16_t(q.z >> 16));
-        v[6]    = int(int16_t(q.w & 0xffff));
-        v[7]    = int(int16_t(q.w >> 16));
-    }
-    __device__ static void store(int16_t* p, const int (&v)[8])
-    {
-        uint4 q;
-        q.x = (uint32_t(uint16_t(v[0]))) | (uint32_t(uint16_t(v[1])) << 16);
-        q.y = (uint32_t(uint16_t(v[2]))) | (uint32_t(uint16_t(v[3])) << 16);
-        q.z = (uint32_t(uint16_t(v[4]))) | (uint32_t(uint16_t(v[5])) << 16);
-        q.w = (uint32_t(uint16_t(v[6]))) | (uint32_t(uint16_t(v[7])) << 16);
-        *reinterpret_cast<uint4*>(p) = q;
-    }
-};
-template <>
-struct Pack8<int32_t>
-{
-    __device__ static void load(const int32_t* p, int (&v)[8])
-    {
-        int4 a = *reinterpret_cast<const int4*>(p);
-        int4 b = *reinterpret_cast<const int4*>(p + 4);
-        v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w;
-        v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
-    }
-    __device__ static void store(int32_t* p, const int (&v)[8])
-    {
-        *reinterpret_cast<int4*>(p)     = make_int4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<int4*>(p + 4) = make_int4(v[4], v[5], v[6], v[7]);
-    }
-};
-
-template <typename ScoreT, typename SizeT>
-__device__ void nw_forward_full(const WinGraph<SizeT>& g, int V, const uint8_t* read, int L, ScoreT* S, int stride,
-                                const Scores sc, int lane)
-{
-    const int gap = sc.gap;
-    // row 0: H[0][j] = j * gap (cudapoa_nw.cuh:176-179)
-    for (int j = lane; j <= L; j += kWave)
-        S[j + kColShift] = ScoreT(j * gap);
-
-    for (int r = 1; r <= V; r++)
-    {
-        const int node = uniform(int(g.sorted[r - 1]));
-        const int np   = uniform(int(g.in_cnt[node]));
-        const int gb   = uniform(int(g.base[node]));
-        ScoreT* row    = S + size_t(r) * stride + kColShift;
-        // column 0 (:187-210)
-        int c0;
-        if (np == 0)
-            c0 = gap;
-        else
-        {
-            c0 = kNeg;
-            for (int p = 0; p < np; p++)
-            {
-                int pr = uniform(pred_row(g, node, p));
-                c0     = max(c0, int(S[size_t(pr) * stride + kColShift]));
-            }
-            c0 += gap;
-        }
+        uint16_t* cov_out = b.cov + size_t(w) * d.max_consensus;
         if (lane == 0)
-            row[0] = ScoreT(c0);
-
-        int carry = c0; // E-domain carry: E[j] = H[j] - j*gap; E[0] = H[0]
-        for (int cb = 0; cb < L; cb += kChunk)
         {
-            const int jb     = cb + lane * kCellsPerLane; // lane cells: columns jb+1 .. jb+8
-            const bool active = jb < L;
-            int D[8];
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-                D[k] = kNeg;
-            if (active)
+            int len = 0;
+            int cst = graph_status;
+            if (cst == kSuccess && nseq > 0)
             {
-                const uint2 rc = *reinterpret_cast<const uint2*>(read + jb);
-                int sig[8];
-#pragma unroll
-                for (int k = 0; k < 8; k++)
-                {
-                    uint32_t ch = ((k < 4 ? rc.x : rc.y) >> (8 * (k & 3))) & 0xff;
-                    sig[k]      = (int(ch) == gb) ? sc.match : sc.mismatch;
-                }
-                const int npp = np == 0 ? 1 : np;
-                for (int p = 0; p < npp; p++)
-                {
-                    const int pr    = np == 0 ? 0 : uniform(pred_row(g, node, p));
-                    const ScoreT* P = S + size_t(pr) * stride + kColShift;
-                    int cur[8];
-                    Pack8<ScoreT>::load(P + jb + 1, cur); // columns jb+1..jb+8 (16-B aligned)
-                    int prev = int(P[jb]);                // column jb
-#pragma unroll
-                    for (int k = 0; k < 8; k++)
-                    {
-                        D[k] = max(D[k], max(prev + sig[k], cur[k] + gap));
-                        prev = cur[k];
-                    }
-                }
+                int r = consensus_raw<SizeT>(g, node_count, cscore, cpred, cons_out, cov_out, d.max_consensus);
+                if (r < 0)
+                    cst = -r;
+                else
+                    len = r;
             }
-            // horizontal closure as a running maximum in the E domain
-            int E[8];
-            int m = kNeg;
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-            {
-                int e = D[k] - (jb + k + 1) * gap;
-                m     = max(m, e);
-                E[k]  = m;
-            }
-            const int below = max(wave_excl_max(m, lane), carry);
-            if (active)
-            {
-                int H[8];
-#pragma unroll
-                for (int k = 0; k < 8; k++)
-                    H[k] = max(E[k], below) + (jb + k + 1) * gap;
-                Pack8<ScoreT>::store(row + jb + 1, H);
-            }
-            carry = max(carry, wave_max(m));
+            sh_len    = len;
+            sh_status = cst;
         }
-    }
-}
-
-// Traceback (cudapoa_nw.cuh:329-462), lane 0 only.  Writes the reversed
-// alignment and returns its length, or -1 at the loop bound.
-template <typename ScoreT, typename SizeT>
-__device__ int traceback_full(const WinGraph<SizeT>& g, int V, const uint8_t* read, int L, const ScoreT* S,
-                              int stride, const Scores sc, SizeT* ag, SizeT* ar, int aln_cap)
-{
-    auto H = [&](int i, int j) { return int(S[size_t(i) * stride + kColShift + j]); };
-    int i = 0, j = L;
-    int best = INT_MIN;
-    for (int idx = 1; idx <= V; idx++)
-    {
-        if (g.out_cnt[int(g.sorted[idx - 1])] == 0)
-        {
-            int s = H(idx, j);
-            if (best < s)
-            {
-                best = s;
-                i    = idx;
-            }
-        }
-    }
-    int prev_i = 0, prev_j = 0, n = 0, loops = 0;
-    const int bound = L + V + 2;
-    while (!(i == 0 && j == 0) && loops < bound)
-    {
-        loops++;
-        const int sij = H(i, j);
-        bool found    = false;
-        int node      = 0, np = 0;
-        if (i != 0)
-        {
-            node = int(g.sorted[i - 1]);
-            np   = int(g.in_cnt[node]);
-        }
-        if (i != 0 && j != 0)
-        {
-            const int cost = (g.base[node] == read[j - 1]) ? sc.match : sc.mismatch;
-            int pi         = (np == 0) ? 0 : pred_row(g, node, 0);
-            if (sij == H(pi, j - 1) + cost)
-            {
-                prev_i = pi, prev_j = j - 1, found = true;
-            }
-            for (int p = 1; !found && p < np; p++)
-            {
-                pi = pred_row(g, node, p);
-                if (sij == H(pi, j - 1) + cost)
-                    prev_i = pi, prev_j = j - 1, found = true;
-            }
-        }
-        if (!found && i != 0)
-        {
-            int pi = (np == 0) ? 0 : pred_row(g, node, 0);
-            if (sij == H(pi, j) + sc.gap)
-                prev_i = pi, prev_j = j, found = true;
-            for (int p = 1; !found && p < np; p++)
-            {
-                pi = pred_row(g, node, p);
-                if (sij == H(pi, j) + sc.gap)
-                    prev_i = pi, prev_j = j, found = true;
-            }
-        }
-        if (!found && j != 0 && sij == H(i, j - 1) + sc.gap)
-            prev_i = i, prev_j = j - 1, found = true;
-        if (n < aln_cap)
-        {
-            ag[n] = SizeT(i == prev_i ? -1 : int(g.sorted[i - 1]));
-            ar[n] = SizeT(j == prev_j ? -1 : j - 1);
-        }
-        n++;
-        i = prev_i;
-        j = prev_j;
-    }
-    if (loops >= bound || n > aln_cap)
-        return -1;
-    return n;
-}
-
-// ---------------------------------------------------------------------------
-// Banded NW (cudapoa_nw_banded.cuh:28-487).  The flat row layout (stride
-// bw + 8, column c at index c - band_start, column 0 written at band_start but
-// read from index 0) is reproduced exactly; see DESIGN.md.
-struct Band
-{
-    int bw, stride, max_column;
-    float gradient;
-    __device__ int start(int row) const
-    {
-        int s = int(float(row) * gradient) - bw / 2;
-        s     = max(s, 0);
-        if (s + bw > max_column)
-            s = max_column - bw + 4;
-        s = max(s, 0);
-        return s - (s % 4);
-    }
-};
-
-template <typename ScoreT>
-__device__ __forceinline__ ScoreT band_get(const ScoreT* S, const Band& B, int row, int col, ScoreT minv)
-{
-    int bs = B.start(row);
-    if ((col > bs + B.bw || col < bs) && col != 0)
-        return minv;
-    int idx = (col == 0) ? 0 : col - bs;
-    return S[int64_t(row) * B.stride + idx];
-}
-
-template <typename ScoreT>
-__device__ __forceinline__ void band_set(ScoreT* S, const Band& B, int row, int col, ScoreT v)
-{
-    int bs  = B.start(row);
-    int idx = (col == 0) ? bs : col - bs;
-    S[int64_t(row) * B.stride + idx] = v;
-}
-
-template <typename ScoreT>
-__device__ __forceinline__ ScoreT score_min()
-{
-    return sizeof(ScoreT) == 2 ? ScoreT(INT16_MIN) : ScoreT(INT32_MIN);
-}
-
-template <typename ScoreT>
-__device__ __forceinline__ ScoreT band_min_value(const Scores sc)
-{
-    // cudapoa_nw_banded.cuh:197
-    int a = min(min(sc.gap, sc.mismatch), -sc.match) - 1;
-    return ScoreT(2 * (a < 0 ? -a : a) + int(score_min<ScoreT>()));
-}
-
-template <typename ScoreT, typename SizeT>
-__device__ void nw_forward_banded(const WinGraph<SizeT>& g, int V, const uint8_t* read, int L, ScoreT* S,
-                                  const Band& B, const Scores sc, int lane)
-{
-    const ScoreT minv = band_min_value<ScoreT>(sc);
-    const int gap     = sc.gap;
-    // horizontal boundary (:212-216)
-    for (int j = lane; j < B.stride; j += kWave)
-        band_set(S, B, 0, j, ScoreT(j * gap));
-    __syncthreads();
-    // vertical boundary (:219-245): serial over rows (reads earlier rows' col 0)
-    if (lane == 0)
-    {
-        for (int r = 0; r < V; r++)
-        {
-            band_set(S, B, 0, 0, ScoreT(0));
-            int node = int(g.sorted[r]);
-            int np   = int(g.in_cnt[node]);
-            if (np == 0)
-                band_set(S, B, r + 1, 0, ScoreT(gap));
-            else
-            {
-                int pen = int(score_min<ScoreT>());
-                for (int p = 0; p < np; p++)
-                    pen = max(pen, int(band_get(S, B, pred_row(g, node, p), 0, minv)));
-                band_set(S, B, r + 1, 0, ScoreT(pen + gap));
-            }
-        }
-    }
-    __syncthreads();
-    for (int r = 1; r <= V; r++)
-    {
-        const int node = uniform(int(g.sorted[r - 1]));
-        const int np   = uniform(int(g.in_cnt[node]));
-        const int gb   = uniform(int(g.base[node]));
-        const int bs   = B.start(r);
-        ScoreT* row    = S + int64_t(r) * B.stride;
-        // initialize_band (:90-105)
-        if (lane == 0)
-            row[(bs == 0) ? 1 : 0] = minv;
-        if (lane < kBandPad)
-            row[B.bw + lane] = minv;
         __syncthreads();
-        int carry = int(band_get(S, B, r, 0, minv));
-        // 64 lanes x 4 cells = 256 columns per pass (reference: 32 x 4 per pass;
-        // the closure is exact so the pass width does not change any cell)
-        for (int base_pos = bs; base_pos < bs + B.bw; base_pos += kWave * 4)
+        const int len = sh_len;
+        // reverse in place to host order (cudapoa_batch.cuh:241-246 does this on the host)
+        for (int k = lane; k < len / 2; k += kWave)
         {
-            const int rp      = base_pos + lane * 4;
-            const bool active = rp < bs + B.bw;
-            int v[4];
-            if (active)
-            {
-                int prof[4];
-#pragma unroll
-                for (int c = 0; c < 4; c++)
-                    prof[c] = (int(read[rp + c]) == gb) ? sc.match : sc.mismatch;
-                const int npp = np == 0 ? 1 : np;
-                for (int p = 0; p < npp; p++)
-                {
-                    const int pr  = np == 0 ? 0 : uniform(pred_row(g, node, p));
-                    const int pbs = B.start(pr);
-                    const int pbe = pbs + B.bw + 4;
-                    int t[4];
-                    if ((rp + 1 > pbe || rp + 1 < pbs) && rp + 1 != 0)
-                    {
-#pragma unroll
-                        for (int c = 0; c < 4; c++)
-                            t[c] = int(minv);
-                    }
-                    else
-                    {
-                        const int idx   = (rp == 0) ? 0 : rp - pbs;
-                        const ScoreT* q = S + int64_t(pr) * B.stride + idx;
-                        t[0]            = int(ScoreT(max(int(q[0]) + prof[0], int(q[1]) + gap)));
-                        t[1]            = int(ScoreT(max(int(q[1]) + prof[1], int(q[2]) + gap)));
-                        t[2]            = int(ScoreT(max(int(q[2]) + prof[2], int(q[3]) + gap)));
-                        t[3]            = int(ScoreT(max(int(q[3]) + prof[3], int(q[4]) + gap)));
-                    }
-                    if (p == 0)
-                    {
-#pragma unroll
-                        for (int c = 0; c < 4; c++)
-                            v[c] = t[c];
-                    }
-                    else
-                    {
-#pragma unroll
-                        for (int c = 0; c < 4; c++)
-                            v[c] = max(v[c], t[c]);
-                    }
-                }
-            }
-            else
-            {
-#pragma unroll
-                for (int c = 0; c < 4; c++)
-                    v[c] = kNeg;
-            }
-            int E[4];
-            int m = kNeg;
-#pragma unroll
-            for (int c = 0; c < 4; c++)
-            {
-                int e = v[c] - (rp + c + 1) * gap;
-                m     = max(m, e);
-                E[c]  = m;
-            }
-            const int below = max(wave_excl_max(m, lane), carry - (base_pos)*gap);
-            int H[4];
-#pragma unroll
-            for (int c = 0; c < 4; c++)
-                H[c] = max(E[c], below) + (rp + c + 1) * gap;
-            if (active)
-            {
-                ScoreT* dst = row + (rp + 1 - bs);
-#pragma unroll
-                for (int c = 0; c < 4; c++)
-                    dst[c] = ScoreT(H[c]);
-            }
-            // carry = H at the pass's last column (lane 63's 4th cell)
-            carry = __shfl(H[3], kWave - 1, kWave);
-            carry = int(ScoreT(carry));
+            uint8_t c0  = cons_out[k];
+            uint8_t c1  = cons_out[len - 1 - k];
+            uint16_t v0 = cov_out[k];
+            uint16_t v1 = cov_out[len - 1 - k];
+            cons_out[k] = c1, cons_out[len - 1 - k] = c0;
+            cov_out[k] = v1, cov_out[len - 1 - k] = v0;
+        }
+        if (lane == 0)
+        {
+            b.cons_len[w] = len;
+            b.status[w]   = uint8_t(sh_status);
+            if (len < d.max_consensus)
+                cons_out[len] = 0;
         }
         __syncthreads();
     }
-}
-
-template <typename ScoreT, typename SizeT>
-__device__ int traceback_banded(const WinGraph<SizeT>& g, int V, const uint8_t* read, int L, const ScoreT* S,
-                                const Band& B, const Scores sc, SizeT* ag, SizeT* ar, int aln_cap)
-{
-    const ScoreT minv = band_min_value<ScoreT>(sc);
-    auto H            = [&](int i, int j) { return int(band_get(S, B, i, j, minv)); };
-    int i = 0, j = L;
-    int best = int(score_min<ScoreT>());
-    for (int idx = 1; idx <= V; idx++)
+    if (MSA)
     {
-        if (g.out_cnt[int(g.sorted[idx - 1])] == 0)
+        uint8_t* msa_out = b.msa + size_t(w) * d.max_seqs * d.max_consensus;
+        if (lane == 0)
         {
-            int s = H(idx, j);
-            if (best < s)
-                best = s, i = idx;
-        }
-    }
-    int prev_i = 0, prev_j = 0, n = 0, loops = 0;
-    const int bound = L + V + 2;
-    while (!(i == 0 && j == 0) && loops < bound)
-    {
-        loops++;
-        const int sij = H(i, j);
-        bool found    = false;
-        int node = 0, np = 0;
-        if (i != 0)
-        {
-            node = int(g.sorted[i - 1]);
-            np   = int(g.in_cnt[node]);
-        }
-        if (i != 0 && j != 0)
-        {
-            const int cost = (g.base[node] == read[j - 1]) ? sc.match : sc.mismatch;
-            int pi         = (np == 0) ? 0 : pred_row(g, node, 0);
-            if (sij == H(pi, j - 1) + cost)
-                prev_i = pi, prev_j = j - 1, found = true;
-            for (int p = 1; !found && p < np; p++)
+            int msa_len = 0;
+            int mst     = graph_status;
+            if (mst == kSuccess && nseq > 0)
             {
-                pi = pred_row(g, node, p);
-                if (sij == H(pi, j - 1) + cost)
-                    prev_i = pi, prev_j = j - 1, found = true;
-            }
-        }
-        if (!found && i != 0)
-        {
-            int pi = (np == 0) ? 0 : pred_row(g, node, 0);
-            if (sij == H(pi, j) + sc.gap)
-                prev_i = pi, prev_j = j, found = true;
-            for (int p = 1; !found && p < np; p++)
-            {
-                pi = pred_row(g, node, p);
-                if (sij == H(pi, j) + sc.gap)
-                    prev_i = pi, prev_j = j, found = true;
-            }
-        }
-        if (!found && sij == H(i, j - 1) + sc.gap)
-            prev_i = i, prev_j = j - 1, found = true;
-        if (n < aln_cap)
-        {
-            ag[n] = SizeT(i == prev_i ? -1 : int(g.sorted[i - 1]));
-            ar[n] = SizeT(j == prev_j ? -1 : j - 1);
-        }
-        n++;
-        i = prev_i;
-        j = prev_j;
-    }
-    if (loops >= bound || n > aln_cap)
-        return -1;
-    return n;
-}
-
-// ---------------------------------------------------------------------------
-// addAlignmentToGraph (cudapoa_add_alignment.cuh:59-279), lane 0.
-template <typename SizeT, bool MSA>
-__device__ uint8_t add_alignment(WinGraph<SizeT>& g, int& node_count, const SizeT* ag, const SizeT* ar, int alen,
-                                 const uint8_t* read, const int8_t* w, int s, uint16_t* ecov, uint16_t* ecov_cnt,
-                                 SizeT* seq_begin, int max_seqs)
-{
-    int head = -1, curr = -1;
-    uint16_t prev_w = 0;
-    int nc          = node_count;
-    for (int k = alen - 1; k >= 0; k--)
-    {
-        const int rp = int(ar[k]);
-        if (rp == -1)
-            continue;
-        const int8_t nw  = w[rp];
-        const uint8_t rb = read[rp];
-        const int gid    = int(ag[k]);
-        bool fresh       = false;
-        if (gid == -1)
-        {
-            curr = nc++;
-            if (nc >= g.max_nodes)
-            {
-                node_count = nc;
-                return kNodeCountExceeded;
-            }
-            fresh = true;
-        }
-        else if (g.base[gid] == rb)
-        {
-            curr = gid;
-        }
-        else
-        {
-            const int na = int(g.aln_cnt[gid]);
-            int hit      = -1;
-            for (int n = 0; n < na; n++)
-            {
-                int aid = int(g.aln[gid * kMaxAlignments + n]);
-                if (g.base[aid] == rb)
+                if (!topsort_racon<SizeT>(g, node_count, cscore, cpred, 4 * d.max_nodes))
+                    mst = kGenericError;
+                else
                 {
-                    hit = aid;
-                    break;
-                }
-            }
-            if (hit != -1)
-                curr = hit;
-            else
-            {
-                curr = nc++;
-                if (nc >= g.max_nodes)
-                {
-                    node_count = nc;
-                    return kNodeCountExceeded;
-                }
-                g.base[curr]    = rb;
-                g.out_cnt[curr] = 0;
-                g.in_cnt[curr]  = 0;
-                g.aln_cnt[curr] = 0;
-                g.cov[curr]     = 0;
-                int cnt         = 0;
-                for (int n = 0; n < na; n++)
-                {
-                    int aid                                  = int(g.aln[gid * kMaxAlignments + n]);
-                    int ac                                   = int(g.aln_cnt[aid]);
-                    g.aln[aid * kMaxAlignments + ac]         = SizeT(curr);
-                    g.aln_cnt[aid]                           = uint16_t(ac + 1);
-                    g.aln[curr * kMaxAlignments + cnt]       = SizeT(aid);
-                    cnt++;
-                }
-                g.aln[gid * kMaxAlignments + na]   = SizeT(curr);
-                g.aln_cnt[gid]                     = uint16_t(na + 1);
-                g.aln[curr * kMaxAlignments + cnt] = SizeT(gid);
-                cnt++;
-                g.aln_cnt[curr] = uint16_t(cnt);
-            }
-        }
-        if (fresh)
-        {
-            g.base[curr]    = rb;
-            g.out_cnt[curr] = 0;
-            g.in_cnt[curr]  = 0;
-            g.aln_cnt[curr] = 0;
-            g.cov[curr]     = 0;
-        }
-        if (MSA && rp == 0)
-            seq_begin[s] = SizeT(curr);
-        if (head != -1)
-        {
-            bool exists  = false;
-            const int ic = int(g.in_cnt[curr]);
-            for (int e = 0; e < ic; e++)
-            {
-                if (int(g.in_e[curr * kMaxEdges + e]) == head)
-                {
-                    exists = true;
-                    g.in_w[curr * kMaxEdges + e] =
-                        uint16_t(int(g.in_w[curr * kMaxEdges + e]) + (int(prev_w) + int(nw)));
-                }
-            }
-            if (!exists)
-            {
-                g.in_e[curr * kMaxEdges + ic] = SizeT(head);
-                g.in_w[curr * kMaxEdges + ic] = uint16_t(int(prev_w) + int(nw));
-                g.in_cnt[curr]                = uint16_t(ic + 1);
-                const int oc                  = int(g.out_cnt[head]);
-                g.out_e[head * kMaxEdges + oc] = SizeT(curr);
-                if (MSA)
-                {
-                    ecov_cnt[head * kMaxEdges + oc]                       = 1;
-                    ecov[size_t(head * kMaxEdges + oc) * max_seqs]        = uint16_t(s);
-                }
-                g.out_cnt[head] = uint16_t(oc + 1);
-                if (oc + 1 >= kMaxEdges || ic + 1 >= kMaxEdges)
-                {
-                    node_count = nc;
-                    return kEdgeCountExceeded;
-                }
-            }
-            else if (MSA)
-            {
-                const int oc = int(g.out_cnt[head]);
-                for (int e = 0; e < oc; e++)
-                {
-                    if (int(g.out_e[head * kMaxEdges + e]) == curr)
+                    // getNodeIDToMSAPosDevice (cudapoa_generate_msa.cuh:27-45); the racon stack
+                    // region is free again and holds node -> column
+                    SizeT* mpos = cpred;
+                    for (int r = 0; r < node_count; r++)
                     {
-                        int c                                                  = int(ecov_cnt[head * kMaxEdges + e]);
-                        ecov[size_t(head * kMaxEdges + e) * max_seqs + c]      = uint16_t(s);
-                        ecov_cnt[head * kMaxEdges + e]                         = uint16_t(c + 1);
+                        const int id = int(g.sorted[r]);
+                        mpos[id]     = SizeT(msa_len);
+                        const int ac = int(g.aln_cnt[id]);
+                        for (int a = 0; a < ac; a++)
+                            mpos[int(g.sorted[++r])] = SizeT(msa_len);
+                        msa_len++;
+                    }
+                    if (msa_len >= d.max_consensus)
+                        mst = kExceededMaxSeqSize;
+                }
+            }
+            sh_len    = msa_len;
+            sh_status = mst;
+        }
+        __syncthreads();
+        const int msa_len = sh_len;
+        const int mst     = sh_status;
+        if (mst == kSuccess && nseq > 0)
+        {
+            const SizeT* mpos = cpred;
+            // generateMSADevice (cudapoa_generate_msa.cuh:47-118): one lane per read
+            for (int s = lane; s < nseq; s += kWave)
+            {
+                uint8_t* row = msa_out + size_t(s) * d.max_consensus;
+                int node     = int(seq_begin[s]);
+                int filled   = 0;
+                while (true)
+                {
+                    const int mp = int(mpos[node]);
+                    row[mp]      = g.base[node];
+                    for (int i = filled; i < mp; i++)
+                        row[i] = '-';
+                    filled   = mp + 1;
+                    bool end = true;
+                    for (int e = 0; e < int(g.out_cnt[node]) && end; e++)
+                    {
+                        const int to = int(g.out_e[node * kMaxEdges + e]);
+                        const int cc = int(ecovc[node * kMaxEdges + e]);
+                        for (int m = 0; m < cc; m++)
+                        {
+                            if (int(ecov[size_t(node * kMaxEdges + e) * d.max_seqs + m]) == s)
+                            {
+                                end  = false;
+                                node = to;
+                                break;
+                            }
+                        }
+                    }
+                    if (end)
+                    {
+                        for (int i = filled; i < msa_len; i++)
+                            row[i] = '-';
                         break;
                     }
                 }
+                row[msa_len] = 0;
             }
         }
-        head = curr;
-        g.cov[head]++;
-        prev_w = uint16_t(int(nw));
-    }
-    node_count = nc;
-    return kSuccess;
-}
-
-// Kahn topological sort (cudapoa_topsort.cuh:38-88), lane 0.
-template <typename SizeT>
-__device__ void topsort_kahn(WinGraph<SizeT>& g, int n, int32_t* local)
-{
-    int k = 0;
-    for (int v = 0; v < n; v++)
-    {
-        local[v] = g.in_cnt[v];
-        if (local[v] == 0)
+        if (lane == 0)
         {
-            g.pos[v]      = SizeT(k);
-            g.sorted[k++] = SizeT(v);
+            b.msa_len[w]    = msa_len;
+            b.msa_status[w] = uint8_t(mst);
         }
     }
-    for (int q = 0; q < k; q++)
-    {
-        const int v  = int(g.sorted[q]);
-        const int oc = int(g.out_cnt[v]);
-        for (int e = 0; e < oc; e++)
-        {
-            const int o = int(g.out_e[v * kMaxEdges + e]);
-            if (--local[o] == 0)
-            {
-                g.pos[o]      = SizeT(k);
-                g.sorted[k++] = SizeT(o);
-            }
-        }
-    }
-}
-
-// racon/SPOA DFS sort (cudapoa_topsort.cuh:94-189), lane 0.  marks packs
-// node_marks (bits 0-1) and check_aligned_nodes (bit 2).
-template <typename SizeT>
-__device__ bool topsort_racon(WinGraph<SizeT>& g, int n, int32_t* marks, SizeT* stack, int stack_cap)
-{
-    for (int i = 0; i < g.max_nodes; i++)
-        marks[i] = 4; // mark 0, check = true
-    int top = -1, k = 0;
-    for (int v = 0; v < n; v++)
-    {
-        if ((marks[v] & 3) != 0)
-            continue;
-        stack[++top] = SizeT(v);
-        while (top != -1)
-        {
-            const int id = int(stack[top]);
-            bool valid   = true;
-            if ((marks[id] & 3) != 2)
-            {
-                for (int e = 0; e < int(g.in_cnt[id]); e++)
-                {
-                    int b = int(g.in_e[id * kMaxEdges + e]);
-                    if ((marks[b] & 3) != 2)
-                    {
-                        if (top + 1 >= stack_cap)
-                            return false;
-                        stack[++top] = SizeT(b);
-                        valid        = false;
-                    }
-                }
-                if (marks[id] & 4)
-                {
-                    for (int a = 0; a < int(g.aln_cnt[id]); a++)
-                    {
-                        int aid = int(g.aln[id * kMaxAlignments + a]);
-                        if ((marks[aid] & 3) != 2)
-                        {
-                            if (top + 1 >= stack_cap)
-                                return false;
-                            stack[++top] = SizeT(aid);
-                            marks[aid] &= 3; // check = false
-                            valid = false;
-                        }
-                    }
-                }
-                if (valid)
-                {
-                    marks[id] = (marks[id] & 4) | 2;
-                    if (marks[id] & 4)
-                    {
-                        g.sorted[k] = SizeT(id);
-                        g.pos[id]   = SizeT(k);
-                        k++;
-                        for (int a = 0; a < int(g.aln_cnt[id]); a++)
-                        {
-                            int aid     = int(g.aln[id * kMaxAlignments + a]);
-                            g.sorted[k] = SizeT(aid);
-                            g.pos[aid]  = SizeT(k);
-                            k++;
-                        }
-                    }
-                }
-                else
-                    marks[id] = (marks[id] & 4) | 1;
-            }
-            if (valid)
-                top--;
-        }
-    }
-    return true;
-}
-
-// Heaviest bundle (cudapoa_generate_consensus.cuh:28-276), lane 0.  Writes the
-// consensus backwards (as the reference kernel) and returns its length or -status.
-template <typename SizeT>
-__device__ int branch_completion(const WinGraph<SizeT>& g, int n, int max_pos, int32_t* score, SizeT* pred)
-{
-    int node = int(g.sorted[max_pos]);
-    for (int oe = 0; oe < int(g.out_cnt[node]); oe++)
-    {
-        const int o = int(g.out_e[node * kMaxEdges + oe]);
-        for (int ie = 0; ie < int(g.in_cnt[o]); ie++)
-        {
-            int id = int(g.in_e[o * kMaxEdges + ie]);
-            if (id != node)
-                score[id] = -1;
-        }
-    }
-    int max_score = 0, max_id = 0;
-    for (int r = max_pos + 1; r < n; r++)
-    {
-        node       = int(g.sorted[r]);
-        pred[node] = SizeT(-1);
-        int s      = -1;
-        for (int e = 0; e < int(g.in_cnt[node]); e++)
-        {
-            const int b = int(g.in_e[node * kMaxEdges + e]);
-            if (score[b] == -1)
-                continue;
-            const int w = int(g.in_w[node * kMaxEdges + e]);
-            if (s < w || (s == w && score[int(pred[node])] <= score[b]))
-            {
-                s          = w;
-                pred[node] = SizeT(b);
-            }
-        }
-        if (int(pred[node]) != -1)
-            s += score[int(pred[node])];
-        if (max_score <= s)
-            max_score = s, max_id = node;
-        score[node] = s;
-    }
-    return max_id;
-}
-
-template <typename SizeT>
-__device__ int consensus_raw(const WinGraph<SizeT>& g, int n, int32_t* score, SizeT* pred, uint8_t* cons,
-                             uint16_t* cov, int max_cons)
-{
-    for (int i = 0; i < n; i++)
-    {
-        pred[i]  = SizeT(-1);
-        score[i] = -1;
-    }
-    int max_id = 0, max_score = -1;
-    for (int r = 0; r < n; r++)
-    {
-        const int node = int(g.sorted[r]);
-        int s          = score[node];
-        for (int e = 0; e < int(g.in_cnt[node]); e++)
-        {
-            const int w = int(g.in_w[node * kMaxEdges + e]);
-            const int b = int(g.in_e[node * kMaxEdges + e]);
-            if (s < w || (s == w && score[int(pred[node])] <= score[b]))
-            {
-                s          = w;
-                pred[node] = SizeT(b);
-            }
-        }
-        if (int(pred[node]) != -1)
-            s += score[int(pred[node])];
-        if (max_score <= s)
-            max_id = node, max_score = s;
-        score[node] = s;
-    }
-    int loops = 0;
-    if (g.out_cnt[max_id] != 0)
-    {
-        while (g.out_cnt[max_id] != 0 && loops < n)
-        {
-            max_id = branch_completion(g, n, int(g.pos[max_id]), score, pred);
-            loops++;
-        }
-    }
-    if (loops >= n)
-        return -int(kLoopCountExceeded);
-    auto node_cov = [&](int id) {
-        uint16_t c = g.cov[id];
-        for (int a = 0; a < int(g.aln_cnt[id]); a++)
-            c = uint16_t(c + g.cov[int(g.aln[id * kMaxAlignments + a])]);
-        return c;
-    };
-    int cpos = 0, count = 0;
-    while (int(pred[max_id]) != -1)
-    {
-        cons[cpos] = g.base[max_id];
-        cov[cpos]  = node_cov(max_id);
-        max_id     = int(pred[max_id]);
-        cpos       = min(cpos + 1, max_cons - 1);
-        count++;
-    }
-    cons[cpos] = g.base[max_id];
-    cov[cpos]  = node_cov(max_id);
-    if (count >= max_cons - 1)
-        return -int(kExceededMaxSeqSize);
-    return cpos + 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -1072,129 +287,573 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
         }
     }
 
-    uint8_t* cons_out = b.cons + size_t(w) * d.max_consensus;
-    const int graph_status = status;
-    if (!MSA || d.want_consensus)
+    finish_window<SizeT, MSA>(b, d, w, lane, g, status, nseq, node_count, cscore, cpred, ecov, ecovc, seq_begin,
+                              sh_len, sh_status);
+    lap(kPhOutput);
+    if (lane == 0)
     {
-        uint16_t* cov_out = b.cov + size_t(w) * d.max_consensus;
-        if (lane == 0)
+        if (b.phase)
         {
-            int len = 0;
-            int cst = graph_status;
-            if (cst == kSuccess && nseq > 0)
-            {
-                int r = consensus_raw<SizeT>(g, node_count, cscore, cpred, cons_out, cov_out, d.max_consensus);
-                if (r < 0)
-                    cst = -r;
-                else
-                    len = r;
-            }
-            sh_len    = len;
-            sh_status = cst;
+            ph[kPhTotal] = now_ticks() - t_begin;
+            for (int p = 0; p < kPhases; p++)
+                b.phase[size_t(w) * kPhases + p] = int64_t(ph[p]);
         }
-        __syncthreads();
-        const int len = sh_len;
-        // reverse in place to host order (cudapoa_batch.cuh:241-246 does this on the host)
-        for (int k = lane; k < len / 2; k += kWave)
-        {
-            uint8_t c0  = cons_out[k];
-            uint8_t c1  = cons_out[len - 1 - k];
-            uint16_t v0 = cov_out[k];
-            uint16_t v1 = cov_out[len - 1 - k];
-            cons_out[k] = c1, cons_out[len - 1 - k] = c0;
-            cov_out[k] = v1, cov_out[len - 1 - k] = v0;
-        }
-        if (lane == 0)
-        {
-            b.cons_len[w] = len;
-            b.status[w]   = uint8_t(sh_status);
-            if (len < d.max_consensus)
-                cons_out[len] = 0;
-        }
-        __syncthreads();
+        b.final_nodes[w] = node_count;
+        b.cells[w]       = cells;
     }
-    if (MSA)
+}
+
+
+// ===========================================================================
+// LDS-resident kernel (full alignment, 16-bit scores and node ids).
+//
+// Differences from poa_window_kernel, same results:
+//  * scores are kept in the E domain, E[i][j] = H[i][j] - j*gap, so the
+//    horizontal gap closure is a plain prefix maximum and row 0 is all zeros;
+//  * only the last kRing rows live in LDS (a ring); a row is also written to
+//    HBM ("spilled") only if a later row reads it from farther back than the
+//    ring (measured predecessor distances are <= 10 rows);
+//  * instead of the score matrix the forward pass writes one traceback code
+//    per cell (direction + predecessor slot, chosen with the reference's tie
+//    order, cudapoa_nw.cuh:361-443), and the traceback walks those codes from
+//    128x128 tiles staged in LDS;
+//  * the per-read row program (base, predecessor rows, sink/spill flags) is
+//    built in LDS once per read, so the row loop touches HBM only for the
+//    code stores.
+// ===========================================================================
+
+constexpr uint32_t kRecEscape = 63; // np field: predecessor rows read from the graph in HBM
+
+__device__ __forceinline__ int dpp_max(int v, int ctrl, int row_mask)
+{
+    // lanes without a source (or masked rows) keep kNeg, the max identity
+    switch (ctrl)
     {
-        uint8_t* msa_out = b.msa + size_t(w) * d.max_seqs * d.max_consensus;
+    case 0x111: return max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x111, 0xf, 0xf, false));
+    case 0x112: return max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x112, 0xf, 0xf, false));
+    case 0x114: return max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x114, 0xf, 0xf, false));
+    case 0x118: return max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x118, 0xf, 0xf, false));
+    default: return v;
+    }
+}
+
+// Inclusive max-scan over the wave with DPP (row_shr 1/2/4/8, row_bcast 15/31).
+__device__ __forceinline__ int wave_incl_max_dpp(int v)
+{
+    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x111, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x112, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x114, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x118, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x142, 0xa, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+
+// Exclusive wave sum of small non-negative ints (row-program offsets).
+__device__ __forceinline__ int wave_excl_sum(int v, int lane, int& total)
+{
+    int x = v;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1)
+    {
+        int t = __shfl_up(x, d, kWave);
+        if (lane >= d)
+            x += t;
+    }
+    total = __shfl(x, kWave - 1, kWave);
+    return x - v;
+}
+
+struct RowProg
+{
+    const uint32_t* rec;
+    const uint16_t* xl;
+    int ring_mask;
+};
+
+// k-th predecessor row of row r (0 = the virtual row 0)
+template <typename SizeT>
+__device__ __forceinline__ int prog_pred(const RowProg& P, const WinGraph<SizeT>& g, int r, uint32_t rec, int k)
+{
+    const int np = (rec >> 8) & 63;
+    if (np == 1)
+        return r - int(rec >> 16);
+    if (np == int(kRecEscape))
+        return pred_row(g, int(g.sorted[r - 1]), k);
+    return int(P.xl[(rec >> 16) + k]);
+}
+
+template <typename SizeT>
+__device__ __forceinline__ int prog_np(const WinGraph<SizeT>& g, int r, uint32_t rec)
+{
+    const int np = (rec >> 8) & 63;
+    return np == int(kRecEscape) ? int(g.in_cnt[int(g.sorted[r - 1])]) : np;
+}
+
+// Row program for rows 1..V (built after every topological sort).
+template <typename SizeT>
+__device__ void build_row_program(const WinGraph<SizeT>& g, int V, uint32_t* rec, uint16_t* xl, int xl_cap,
+                                  int ring_rows, int lane)
+{
+    int xbase = 0;
+    for (int r0 = 1; r0 <= V; r0 += kWave)
+    {
+        const int r      = r0 + lane;
+        const bool valid = r <= V;
+        int node = 0, np = 0, base = 0, sink = 0;
+        if (valid)
+        {
+            node = int(g.sorted[r - 1]);
+            np   = int(g.in_cnt[node]);
+            base = int(g.base[node]);
+            sink = g.out_cnt[node] == 0 ? 1 : 0;
+        }
+        int total      = 0;
+        const int excl = wave_excl_sum(np >= 2 ? np : 0, lane, total);
+        if (valid)
+        {
+            uint32_t v = uint32_t(base) | (uint32_t(sink) << 14);
+            if (np == 1)
+            {
+                const int p = pred_row(g, node, 0);
+                v |= (1u << 8) | (uint32_t(r - p) << 16);
+            }
+            else if (np >= 2)
+            {
+                const int off = xbase + excl;
+                if (off + np <= xl_cap)
+                {
+                    for (int k = 0; k < np; k++)
+                        xl[off + k] = uint16_t(pred_row(g, node, k));
+                    v |= (uint32_t(np) << 8) | (uint32_t(off) << 16);
+                }
+                else
+                    v |= kRecEscape << 8;
+            }
+            rec[r] = v;
+        }
+        xbase += total;
+    }
+    __syncthreads();
+    // spill marks: a row read from >= ring_rows rows later must also go to HBM
+    for (int r = 1 + lane; r <= V; r += kWave)
+    {
+        const uint32_t v = rec[r];
+        RowProg P{rec, xl, ring_rows - 1};
+        const int np = prog_np(g, r, v);
+        for (int k = 0; k < np; k++)
+        {
+            const int p = prog_pred(P, g, r, v, k);
+            if (p != 0 && r - p >= ring_rows)
+                atomicOr(&rec[p], 1u << 15);
+        }
+    }
+    __syncthreads();
+}
+
+// Loads 8 E values (columns jb+1..jb+8) and E[jb] of predecessor row p.
+__device__ __forceinline__ void load_pred8(const int16_t* ring, int ring_stride, int ring_mask, const int16_t* spill,
+                                           int stride, int r, int p, int jb, int (&cur)[8], int& prev)
+{
+    if (p == 0)
+    {
+#pragma unroll
+        for (int c = 0; c < 8; c++)
+            cur[c] = 0;
+        prev = 0;
+        return;
+    }
+    const int16_t* row = (r - p <= ring_mask) ? ring + size_t(p & ring_mask) * ring_stride
+                                              : spill + size_t(p) * stride;
+    Pack8<int16_t>::load(row + jb + kColShift + 1, cur);
+    prev = int(row[jb + kColShift]);
+}
+
+// Forward pass; returns the end row (first sink with the strictly greatest
+// last-column score, cudapoa_nw.cuh:332-349 with rows in the current
+// topological order).
+template <typename SizeT>
+__device__ int nw_forward_lds(const WinGraph<SizeT>& g, const RowProg& P, int V, const uint8_t* read, int L,
+                              int16_t* ring, int ring_stride, int16_t* spill, int stride, uint8_t* codes,
+                              int code_stride, const Scores sc, int lane)
+{
+    const int gap  = sc.gap;
+    const int s_eq = sc.match - gap; // diagonal step in the E domain
+    const int s_ne = sc.mismatch - gap;
+    const int mask = P.ring_mask;
+    // row 0 (E == 0 everywhere) in ring slot 0
+    for (int j = lane; j < ring_stride; j += kWave)
+        ring[j] = 0;
+    int best_row = 0;
+    int best_val = INT_MIN;
+    const int last_lane = (L - 1) / kCellsPerLane % kWave; // lane owning column L in the last chunk
+    const int last_c    = (L - 1) % kCellsPerLane;
+    for (int r = 1; r <= V; r++)
+    {
+        const uint32_t rec = P.rec[r];
+        const int base     = int(rec & 0xff);
+        const int np       = uniform(prog_np(g, r, rec));
+        const bool spill_r = (rec >> 15) & 1;
+        int16_t* row       = ring + size_t(r & mask) * ring_stride;
+        int16_t* srow      = spill + size_t(r) * stride;
+        uint8_t* crow      = codes + size_t(r) * code_stride;
+        // column 0: vertical from the first predecessor with the largest E[.][0]
+        int c0, c0k = 0;
+        if (np == 0)
+            c0 = gap;
+        else
+        {
+            c0 = kNeg;
+            for (int k = 0; k < np; k++)
+            {
+                const int p = uniform(prog_pred(P, g, r, rec, k));
+                int v;
+                if (p == 0)
+                    v = 0;
+                else if (r - p <= mask)
+                    v = int(ring[size_t(p & mask) * ring_stride + kColShift]);
+                else
+                    v = int(spill[size_t(p) * stride + kColShift]);
+                if (v > c0)
+                    c0 = v, c0k = k;
+            }
+            c0 += gap;
+        }
         if (lane == 0)
         {
-            int msa_len = 0;
-            int mst     = graph_status;
-            if (mst == kSuccess && nseq > 0)
+            row[kColShift]  = int16_t(c0);
+            crow[kColShift] = uint8_t(1 | (c0k << 2));
+            if (spill_r)
+                srow[kColShift] = int16_t(c0);
+        }
+        const int p0 = np == 0 ? 0 : uniform(prog_pred(P, g, r, rec, 0));
+        int carry    = c0;
+        int endv     = (L == 0) ? c0 : kNeg;
+        for (int cb = 0; cb < L; cb += kChunk)
+        {
+            const int jb      = cb + lane * kCellsPerLane;
+            const bool active = jb < L;
+            int sig[8], dg0[8], vt0[8], D[8];
+            if (active)
             {
-                if (!topsort_racon<SizeT>(g, node_count, cscore, cpred, 4 * d.max_nodes))
-                    mst = kGenericError;
-                else
+                const uint2 rc = *reinterpret_cast<const uint2*>(read + jb);
+#pragma unroll
+                for (int c = 0; c < 8; c++)
                 {
-                    // getNodeIDToMSAPosDevice (cudapoa_generate_msa.cuh:27-45); the racon stack
-                    // region is free again and holds node -> column
-                    SizeT* mpos = cpred;
-                    for (int r = 0; r < node_count; r++)
+                    const int ch = int(((c < 4 ? rc.x : rc.y) >> (8 * (c & 3))) & 0xff);
+                    sig[c]       = (ch == base) ? s_eq : s_ne;
+                }
+                int cur[8], prev;
+                load_pred8(ring, ring_stride, mask, spill, stride, r, p0, jb, cur, prev);
+#pragma unroll
+                for (int c = 0; c < 8; c++)
+                {
+                    dg0[c] = prev + sig[c];
+                    vt0[c] = cur[c] + gap;
+                    D[c]   = max(dg0[c], vt0[c]);
+                    prev   = cur[c];
+                }
+                for (int k = 1; k < np; k++)
+                {
+                    const int p = uniform(prog_pred(P, g, r, rec, k));
+                    load_pred8(ring, ring_stride, mask, spill, stride, r, p, jb, cur, prev);
+#pragma unroll
+                    for (int c = 0; c < 8; c++)
                     {
-                        const int id = int(g.sorted[r]);
-                        mpos[id]     = SizeT(msa_len);
-                        const int ac = int(g.aln_cnt[id]);
-                        for (int a = 0; a < ac; a++)
-                            mpos[int(g.sorted[++r])] = SizeT(msa_len);
-                        msa_len++;
+                        D[c] = max(D[c], max(prev + sig[c], cur[c] + gap));
+                        prev = cur[c];
                     }
-                    if (msa_len >= d.max_consensus)
-                        mst = kExceededMaxSeqSize;
                 }
             }
-            sh_len    = msa_len;
-            sh_status = mst;
-        }
-        __syncthreads();
-        const int msa_len = sh_len;
-        const int mst     = sh_status;
-        if (mst == kSuccess && nseq > 0)
-        {
-            const SizeT* mpos = cpred;
-            // generateMSADevice (cudapoa_generate_msa.cuh:47-118): one lane per read
-            for (int s = lane; s < nseq; s += kWave)
+            else
             {
-                uint8_t* row = msa_out + size_t(s) * d.max_consensus;
-                int node     = int(seq_begin[s]);
-                int filled   = 0;
-                while (true)
+#pragma unroll
+                for (int c = 0; c < 8; c++)
+                    D[c] = dg0[c] = vt0[c] = kNeg;
+            }
+            // prefix maximum across the row
+            int E[8];
+            int m = kNeg;
+#pragma unroll
+            for (int c = 0; c < 8; c++)
+            {
+                m    = max(m, D[c]);
+                E[c] = m;
+            }
+            const int incl  = wave_incl_max_dpp(m);
+            const int excl  = __builtin_amdgcn_update_dpp(kNeg, incl, 0x138, 0xf, 0xf, false); // wave_shr:1
+            const int below = max(excl, carry);
+#pragma unroll
+            for (int c = 0; c < 8; c++)
+                E[c] = max(E[c], below);
+            carry = max(carry, __builtin_amdgcn_readlane(incl, kWave - 1));
+            if (active)
+            {
+                // traceback codes: diagonal over predecessors in slot order, then
+                // vertical, then horizontal (cudapoa_nw.cuh:361-443)
+                int code[8];
+                int kd[8], kv[8];
+#pragma unroll
+                for (int c = 0; c < 8; c++)
+                    kd[c] = kv[c] = -1;
+                if (np >= 2)
                 {
-                    const int mp = int(mpos[node]);
-                    row[mp]      = g.base[node];
-                    for (int i = filled; i < mp; i++)
-                        row[i] = '-';
-                    filled   = mp + 1;
-                    bool end = true;
-                    for (int e = 0; e < int(g.out_cnt[node]) && end; e++)
+                    for (int k = 1; k < np; k++)
                     {
-                        const int to = int(g.out_e[node * kMaxEdges + e]);
-                        const int cc = int(ecovc[node * kMaxEdges + e]);
-                        for (int m = 0; m < cc; m++)
+                        const int p = uniform(prog_pred(P, g, r, rec, k));
+                        int cur[8], prev;
+                        load_pred8(ring, ring_stride, mask, spill, stride, r, p, jb, cur, prev);
+#pragma unroll
+                        for (int c = 0; c < 8; c++)
                         {
-                            if (int(ecov[size_t(node * kMaxEdges + e) * d.max_seqs + m]) == s)
-                            {
-                                end  = false;
-                                node = to;
-                                break;
-                            }
+                            if (kd[c] < 0 && prev + sig[c] == E[c])
+                                kd[c] = k;
+                            if (kv[c] < 0 && cur[c] + gap == E[c])
+                                kv[c] = k;
+                            prev = cur[c];
                         }
                     }
-                    if (end)
-                    {
-                        for (int i = filled; i < msa_len; i++)
-                            row[i] = '-';
-                        break;
-                    }
                 }
-                row[msa_len] = 0;
+#pragma unroll
+                for (int c = 0; c < 8; c++)
+                {
+                    int cd;
+                    if (dg0[c] == E[c])
+                        cd = 0;
+                    else if (kd[c] >= 0)
+                        cd = kd[c] << 2;
+                    else if (vt0[c] == E[c])
+                        cd = 1;
+                    else if (kv[c] >= 0)
+                        cd = 1 | (kv[c] << 2);
+                    else
+                        cd = 2;
+                    code[c] = cd;
+                }
+                Pack8<int16_t>::store(row + jb + kColShift + 1, E);
+                if (spill_r)
+                    Pack8<int16_t>::store(srow + jb + kColShift + 1, E);
+                uint64_t cw = 0;
+#pragma unroll
+                for (int c = 0; c < 8; c++)
+                    cw |= uint64_t(code[c]) << (8 * c);
+                __builtin_nontemporal_store(cw, reinterpret_cast<uint64_t*>(crow + jb + kColShift + 1));
+                if (lane == last_lane && cb + kChunk >= L)
+                {
+#pragma unroll
+                    for (int c = 0; c < 8; c++)
+                        if (c == last_c)
+                            endv = E[c];
+                }
             }
         }
-        if (lane == 0)
+        if (rec & (1u << 14))
         {
-            b.msa_len[w]    = msa_len;
-            b.msa_status[w] = uint8_t(mst);
+            const int v = __builtin_amdgcn_readlane(endv, last_lane);
+            if (best_val < v)
+                best_val = v, best_row = r;
         }
     }
+    return best_row;
+}
+
+// Traceback over the code matrix (lane-uniform walk, tiles staged in LDS by
+// the whole wave).  Emits reversed (row or -1, read position or -1) pairs;
+// rows are converted to node ids afterwards.
+template <typename SizeT>
+__device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V, int L, int end_row,
+                               const uint8_t* codes, int code_stride, uint8_t* tile, SizeT* ag, SizeT* ar,
+                               int aln_cap, int lane)
+{
+    int i = end_row, j = L;
+    int ti0 = INT_MIN / 2, tj0 = INT_MIN / 2;
+    int n = 0, loops = 0;
+    const int bound = L + V + 2;
+    while (!(i == 0 && j == 0) && loops < bound)
+    {
+        loops++;
+        int pi, pj;
+        if (i == 0)
+        {
+            pi = 0;
+            pj = j - 1;
+        }
+        else
+        {
+            const int cj = j + kColShift;
+            if (i < ti0 || i >= ti0 + kTileRows || cj < tj0 || cj >= tj0 + kTileCols)
+            {
+                ti0 = max(0, i - (kTileRows - 1));
+                tj0 = max(0, cj - (kTileCols - 16)) & ~15;
+                __syncthreads();
+                for (int t = lane; t < kTileRows * (kTileCols / 16); t += kWave)
+                {
+                    const int tr = t / (kTileCols / 16);
+                    const int tc = (t % (kTileCols / 16)) * 16;
+                    const int rr = ti0 + tr;
+                    uint4 v      = make_uint4(0, 0, 0, 0);
+                    if (rr <= V && tj0 + tc + 16 <= code_stride)
+                        v = *reinterpret_cast<const uint4*>(codes + size_t(rr) * code_stride + tj0 + tc);
+                    *reinterpret_cast<uint4*>(tile + tr * kTileCols + tc) = v;
+                }
+                __syncthreads();
+            }
+            const int code = int(tile[(i - ti0) * kTileCols + (cj - tj0)]);
+            const int dir  = code & 3;
+            if (dir == 2)
+            {
+                pi = i;
+                pj = j - 1;
+            }
+            else
+            {
+                const uint32_t rec = P.rec[i];
+                pi                 = prog_pred(P, g, i, rec, code >> 2);
+                pj                 = dir == 0 ? j - 1 : j;
+            }
+        }
+        if (lane == 0 && n < aln_cap)
+        {
+            ag[n] = SizeT(i == pi ? -1 : i);
+            ar[n] = SizeT(j == pj ? -1 : j - 1);
+        }
+        n++;
+        i = pi;
+        j = pj;
+    }
+    if (loops >= bound || n > aln_cap)
+        return -1;
+    return n;
+}
+
+template <bool MSA>
+__global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d, Scores sc)
+{
+    using SizeT  = int16_t;
+    extern __shared__ __align__(16) uint8_t lds[];
+    __shared__ int sh_alen;
+    __shared__ int sh_status;
+    __shared__ int sh_len;
+
+    const int w = blockIdx.x;
+    if (w >= b.num_windows)
+        return;
+    const int lane = threadIdx.x;
+
+    uint8_t* lread   = lds;
+    int16_t* ring    = reinterpret_cast<int16_t*>(lds + d.lds_ring_off);
+    uint32_t* rec    = reinterpret_cast<uint32_t*>(lds + d.lds_rec_off);
+    uint16_t* xl     = reinterpret_cast<uint16_t*>(lds + d.lds_xl_off);
+    uint8_t* tile    = lds + d.lds_ring_off; // traceback tiles reuse the ring
+    const int rstride = d.score_stride;      // ring / spill row stride (elements)
+    RowProg P{rec, xl, d.lds_ring_rows - 1};
+
+    const size_t mn = size_t(d.max_nodes);
+    WinGraph<SizeT> g;
+    g.base      = b.base + w * mn;
+    g.in_cnt    = b.in_cnt + w * mn;
+    g.out_cnt   = b.out_cnt + w * mn;
+    g.aln_cnt   = b.aln_cnt + w * mn;
+    g.cov       = b.node_cov + w * mn;
+    g.in_w      = b.in_w + w * mn * kMaxEdges;
+    g.in_e      = static_cast<SizeT*>(b.in_e) + w * mn * kMaxEdges;
+    g.out_e     = static_cast<SizeT*>(b.out_e) + w * mn * kMaxEdges;
+    g.aln       = static_cast<SizeT*>(b.aln) + w * mn * kMaxAlignments;
+    g.sorted    = static_cast<SizeT*>(b.sorted) + w * mn;
+    g.pos       = static_cast<SizeT*>(b.pos) + w * mn;
+    g.max_nodes = d.max_nodes;
+
+    SizeT* ag        = static_cast<SizeT*>(b.ag) + size_t(w) * d.aln_cap;
+    SizeT* ar        = static_cast<SizeT*>(b.ar) + size_t(w) * d.aln_cap;
+    int16_t* spill   = static_cast<int16_t*>(b.scores) + size_t(w) * d.score_rows * size_t(rstride);
+    uint8_t* codes   = b.codes + size_t(w) * d.score_rows * size_t(d.code_stride);
+    int32_t* cscore  = b.cscore + w * mn;
+    SizeT* cpred     = static_cast<SizeT*>(b.cpred) + w * mn * 4;
+    uint16_t* ecov   = MSA ? b.edge_cov + w * mn * kMaxEdges * d.max_seqs : nullptr;
+    uint16_t* ecovc  = MSA ? b.edge_cov_cnt + w * mn * kMaxEdges : nullptr;
+    SizeT* seq_begin = MSA ? static_cast<SizeT*>(b.seq_begin) + size_t(w) * d.max_seqs : nullptr;
+
+    uint64_t ph[kPhases] = {0, 0, 0, 0, 0, 0, 0};
+    const uint64_t t_begin = now_ticks();
+    uint64_t t_mark        = t_begin;
+    auto lap = [&](int p) {
+        uint64_t t = now_ticks();
+        ph[p] += t - t_mark;
+        t_mark = t;
+    };
+    const WindowDesc wd = b.windows[w];
+    const int nseq      = wd.num_seqs;
+    int status          = kSuccess;
+    int64_t cells       = 0;
+    int node_count      = 0;
+
+    if (nseq > 0)
+    {
+        const int len0      = b.seq_len[wd.first_seq];
+        const uint8_t* seq0 = b.seqs + b.seq_off[wd.first_seq];
+        const int8_t* w0    = b.wts + b.seq_off[wd.first_seq];
+        build_backbone<SizeT, MSA>(g, seq0, w0, len0, lane, ecov, ecovc, seq_begin, d.max_seqs);
+        node_count = len0;
+        lap(kPhBackbone);
+        for (int s = 1; s < nseq; s++)
+        {
+            if (node_count >= d.max_nodes)
+            {
+                status = kNodeCountExceeded;
+                break;
+            }
+            const int L           = b.seq_len[wd.first_seq + s];
+            const int64_t off     = b.seq_off[wd.first_seq + s];
+            const uint8_t* read_g = b.seqs + off;
+            const int8_t* wts_g   = b.wts + off;
+            const int padded      = (L + 16 + 15) & ~15;
+            for (int j = lane; j < padded; j += kWave)
+                lread[j] = j < L ? read_g[j] : 0;
+            const int V = node_count;
+            build_row_program<SizeT>(g, V, rec, xl, d.lds_xl_cap, d.lds_ring_rows, lane);
+            cells += int64_t(V + 1) * (L + 1);
+            const int end_row = nw_forward_lds<SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride, codes,
+                                                      d.code_stride, sc, lane);
+            __syncthreads();
+            lap(kPhForward);
+            const int alen = traceback_codes<SizeT>(g, P, V, L, end_row, codes, d.code_stride, tile, ag, ar,
+                                                    d.aln_cap, lane);
+            __syncthreads();
+            // rows -> node ids
+            for (int k = lane; k < alen; k += kWave)
+            {
+                const int rr = int(ag[k]);
+                if (rr > 0)
+                    ag[k] = g.sorted[rr - 1];
+            }
+            __syncthreads();
+            lap(kPhTraceback);
+            if (alen == -1)
+            {
+                status = kLoopCountExceeded;
+                break;
+            }
+            if (lane == 0)
+            {
+                int nc     = node_count;
+                uint8_t rc = add_alignment<SizeT, MSA>(g, nc, ag, ar, alen, read_g, wts_g, s, ecov, ecovc, seq_begin,
+                                                       d.max_seqs);
+                lap(kPhAdd);
+                if (rc == kSuccess)
+                    topsort_kahn<SizeT>(g, nc, cscore);
+                lap(kPhTopsort);
+                sh_status = rc;
+                sh_len    = nc;
+            }
+            __syncthreads();
+            status     = sh_status;
+            node_count = sh_len;
+            if (status != kSuccess)
+                break;
+        }
+    }
+    finish_window<SizeT, MSA>(b, d, w, lane, g, status, nseq, node_count, cscore, cpred, ecov, ecovc, seq_begin,
+                              sh_len, sh_status);
     lap(kPhOutput);
     if (lane == 0)
     {
@@ -1222,6 +881,15 @@ extern "C" hipError_t gwamd_internal_poa_launch(const gwamd::poa::Buffers* b, co
     if (b->num_windows <= 0)
         return hipSuccess;
     dim3 grid(b->num_windows), block(kWave);
+    if (d->lds_kernel && !banded && score_bits == 16 && size_bits == 16)
+    {
+        if (msa)
+            hipLaunchKernelGGL((poa_window_kernel_lds<true>), grid, block, size_t(d->lds_bytes), stream, *b, *d, *sc);
+        else
+            hipLaunchKernelGGL((poa_window_kernel_lds<false>), grid, block, size_t(d->lds_bytes), stream, *b, *d,
+                               *sc);
+        return hipGetLastError();
+    }
     const int lds_bytes = (d->max_seq_len > d->band_width + kBandPad ? d->max_seq_len : d->band_width + kBandPad) + 32;
     const size_t lds    = size_t((lds_bytes + 15) & ~15);
 #define GWAMD_LAUNCH(ST, ZT, BD, MS)                                                                          \

@@ -279,9 +279,15 @@ class CudaPoaBatch:
         return out[:n]
 
     def get_types(self):
+        """(score bits, size bits) chosen by create_batch (cudapoa_limits.hpp:28-53)."""
         sb, zb = C.c_int32(), C.c_int32()
         self._lib.gwamd_poa_get_types(self._handle, C.byref(sb), C.byref(zb))
         return sb.value, zb.value
+
+    def kernel_variant(self):
+        """1: global-memory kernel, 2: LDS-resident kernel."""
+        sb, zb = C.c_int32(), C.c_int32()
+        return self._lib.gwamd_poa_get_types(self._handle, C.byref(sb), C.byref(zb))
 
     def get_capacity(self):
         nb, mp = C.c_int64(), C.c_int32()

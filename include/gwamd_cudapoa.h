@@ -113,7 +113,8 @@ int32_t gwamd_poa_get_stats(gwamd_poa_batch* batch, int64_t* cells, int32_t* fin
  * backbone, forward DP, traceback, add, topsort, output, total; ticks receives
  * 7 * get_total_poas() values.  Returns the number of phases. */
 int32_t gwamd_poa_get_phase_ticks(gwamd_poa_batch* batch, int64_t* ticks);
-/* Score/size types chosen by create_batch (16 or 32 bits each). */
+/* Score/size types chosen by create_batch (16 or 32 bits each); returns the
+ * kernel variant (1: global-memory kernel, 2: LDS-resident kernel). */
 int32_t gwamd_poa_get_types(const gwamd_poa_batch* batch, int32_t* score_bits, int32_t* size_bits);
 /* Device bytes allocated by the batch and its window capacity (max_poas). */
 int32_t gwamd_poa_get_capacity(const gwamd_poa_batch* batch, int64_t* device_bytes, int32_t* max_poas);

@@ -191,3 +191,29 @@ def test_output_type_unavailable_and_reset():
 def test_zero_memory_throws():
     with pytest.raises(RuntimeError):
         CudaPoaBatch(5, 1024, 0)
+
+
+@pytest.mark.parametrize("variant", ["v1", "lds"])
+def test_kernel_variants_agree_with_oracle(variant, monkeypatch):
+    # the global-memory kernel and the LDS-resident kernel give identical outputs
+    if variant == "v1":
+        monkeypatch.setenv("GWAMD_POA_KERNEL", "v1")
+    else:
+        monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    wins = synth.poa_windows(71, 12, 700, 16, 40, 40, 40)
+    b = run_gpu(wins, 800, 16)
+    assert b.kernel_variant() == (1 if variant == "v1" else 2)
+    cons, cov, st = b.get_consensus()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 800, 16)
+        assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), i
+
+
+def test_lds_kernel_empty_and_tiny_reads():
+    wins = [[b"ACGTACGTAC", b"", b"ACG", b"A", b"ACGTTCGTAC"], [b"GATTACA", b"GATTACA", b"TTT"]]
+    b = run_gpu(wins, 128, 8)
+    assert b.kernel_variant() == 2
+    cons, cov, st = b.get_consensus()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 128, 8)
+        assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), i
