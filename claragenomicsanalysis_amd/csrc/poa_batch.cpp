@@ -195,7 +195,7 @@ public:
         dims_.max_consensus = bs_.max_consensus_size;
         dims_.band_width    = bs_.alignment_band_width;
         dims_.score_stride  = banded_ ? bs_.alignment_band_width + gwamd::poa::kBandPad
-                                      : int32_t(align8(int64_t(bs_.max_sequence_size) + 16));
+                                      : int32_t(align8(int64_t(bs_.max_sequence_size) + 48));
         dims_.score_rows    = dims_.max_nodes + 2;
         dims_.aln_cap       = dims_.max_nodes + bs_.max_sequence_size + 4;
         dims_.want_consensus = (output_mask_ & OutputType::consensus) ? 1 : 0;
@@ -523,7 +523,7 @@ private:
             return;
         auto a16             = [](int64_t v) { return (v + 15) & ~int64_t(15); };
         const int ring_rows  = 8;
-        const int64_t read_b = a16(int64_t(dims_.max_seq_len) + 32);
+        const int64_t read_b = a16(int64_t(dims_.max_seq_len) + 48);
         const int64_t ring_b = std::max<int64_t>(int64_t(ring_rows) * dims_.score_stride * 2,
                                                  int64_t(gwamd::poa::kTileRows) * gwamd::poa::kTileCols);
         const int64_t rec_b  = a16(int64_t(dims_.max_nodes + 1) * 4);
@@ -541,7 +541,7 @@ private:
         dims_.lds_xl_off    = int32_t(read_b + ring_b + rec_b);
         dims_.lds_xl_cap    = int32_t(xl_cap);
         dims_.lds_bytes     = int32_t(total);
-        dims_.code_stride   = int32_t(a16(int64_t(dims_.max_seq_len) + 16));
+        dims_.code_stride   = int32_t(a16(int64_t(dims_.max_seq_len) + 48));
     }
 
     // Non-score bytes of the reference slab for max_poas windows

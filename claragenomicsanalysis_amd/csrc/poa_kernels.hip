@@ -25,6 +25,33 @@ namespace gwamd
 namespace poa
 {
 
+// Per-window phase timers (s_memrealtime, 100 MHz) kept in registers.
+struct PhaseTimer
+{
+    uint64_t t0, mark;
+    uint64_t v[kPhases - 1];
+    __device__ PhaseTimer() : t0(now_ticks()), mark(t0)
+    {
+#pragma unroll
+        for (int i = 0; i < kPhases - 1; i++)
+            v[i] = 0;
+    }
+    template <int P>
+    __device__ void lap()
+    {
+        const uint64_t t = now_ticks();
+        v[P] += t - mark;
+        mark = t;
+    }
+    __device__ void store(int64_t* out) const
+    {
+#pragma unroll
+        for (int i = 0; i < kPhases - 1; i++)
+            out[i] = int64_t(v[i]);
+        out[kPhTotal] = int64_t(now_ticks() - t0);
+    }
+};
+
 // Consensus and/or MSA of one finished window (cudapoa_generate_consensus.cuh:
 // 279-347, cudapoa_generate_msa.cuh:121-224).
 template <typename SizeT, bool MSA>
@@ -195,14 +222,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
     uint16_t* ecovc  = MSA ? b.edge_cov_cnt + w * mn * kMaxEdges : nullptr;
     SizeT* seq_begin = MSA ? static_cast<SizeT*>(b.seq_begin) + size_t(w) * d.max_seqs : nullptr;
 
-    uint64_t ph[kPhases] = {0, 0, 0, 0, 0, 0, 0};
-    const uint64_t t_begin = now_ticks();
-    uint64_t t_mark        = t_begin;
-    auto lap = [&](int p) {
-        uint64_t t = now_ticks();
-        ph[p] += t - t_mark;
-        t_mark = t;
-    };
+    PhaseTimer ph;
     const WindowDesc wd = b.windows[w];
     const int nseq      = wd.num_seqs;
     int status          = kSuccess;
@@ -216,7 +236,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
         const int8_t* w0    = b.wts + b.seq_off[wd.first_seq];
         build_backbone<SizeT, MSA>(g, seq0, w0, len0, lane, ecov, ecovc, seq_begin, d.max_seqs);
         node_count = len0;
-        lap(kPhBackbone);
+        ph.lap<kPhBackbone>();
         for (int s = 1; s < nseq; s++)
         {
             if (node_count >= d.max_nodes) // cudapoa_kernels.cuh:222-227
@@ -245,7 +265,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
                 cells += int64_t(V + 1) * (d.band_width + kBandPad);
                 nw_forward_banded<ScoreT, SizeT>(g, V, lds_read, L, S, B, sc, lane);
                 __syncthreads();
-                lap(kPhForward);
+                ph.lap<kPhForward>();
                 if (lane == 0)
                     sh_alen = traceback_banded<ScoreT, SizeT>(g, V, lds_read, L, S, B, sc, ag, ar, d.aln_cap);
             }
@@ -254,13 +274,13 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
                 cells += int64_t(V + 1) * (L + 1);
                 nw_forward_full<ScoreT, SizeT>(g, V, lds_read, L, S, d.score_stride, sc, lane);
                 __syncthreads();
-                lap(kPhForward);
+                ph.lap<kPhForward>();
                 if (lane == 0)
                     sh_alen = traceback_full<ScoreT, SizeT>(g, V, lds_read, L, S, d.score_stride, sc, ag, ar,
                                                             d.aln_cap);
             }
             __syncthreads();
-            lap(kPhTraceback);
+            ph.lap<kPhTraceback>();
             alen = sh_alen;
             if (alen == -1)
             {
@@ -272,10 +292,10 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
                 int nc     = node_count;
                 uint8_t rc = add_alignment<SizeT, MSA>(g, nc, ag, ar, alen, read_g, wts_g, s, ecov, ecovc, seq_begin,
                                                        d.max_seqs);
-                lap(kPhAdd);
+                ph.lap<kPhAdd>();
                 if (rc == kSuccess)
                     topsort_kahn<SizeT>(g, nc, cscore);
-                lap(kPhTopsort);
+                ph.lap<kPhTopsort>();
                 sh_status = rc;
                 sh_len    = nc;
             }
@@ -289,15 +309,11 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
 
     finish_window<SizeT, MSA>(b, d, w, lane, g, status, nseq, node_count, cscore, cpred, ecov, ecovc, seq_begin,
                               sh_len, sh_status);
-    lap(kPhOutput);
+    ph.lap<kPhOutput>();
     if (lane == 0)
     {
         if (b.phase)
-        {
-            ph[kPhTotal] = now_ticks() - t_begin;
-            for (int p = 0; p < kPhases; p++)
-                b.phase[size_t(w) * kPhases + p] = int64_t(ph[p]);
-        }
+            ph.store(b.phase + size_t(w) * kPhases);
         b.final_nodes[w] = node_count;
         b.cells[w]       = cells;
     }
@@ -376,6 +392,8 @@ template <typename SizeT>
 __device__ __forceinline__ int prog_pred(const RowProg& P, const WinGraph<SizeT>& g, int r, uint32_t rec, int k)
 {
     const int np = (rec >> 8) & 63;
+    if (np == 0)
+        return 0; // source node: the virtual row 0
     if (np == 1)
         return r - int(rec >> 16);
     if (np == int(kRecEscape))
@@ -451,50 +469,89 @@ __device__ void build_row_program(const WinGraph<SizeT>& g, int V, uint32_t* rec
     __syncthreads();
 }
 
-// Loads 8 E values (columns jb+1..jb+8) and E[jb] of predecessor row p.
-__device__ __forceinline__ void load_pred8(const int16_t* ring, int ring_stride, int ring_mask, const int16_t* spill,
-                                           int stride, int r, int p, int jb, int (&cur)[8], int& prev)
+__device__ __forceinline__ void unpack8(uint4 q, int* v)
+{
+    v[0] = int(int16_t(q.x & 0xffff));
+    v[1] = int(int16_t(q.x >> 16));
+    v[2] = int(int16_t(q.y & 0xffff));
+    v[3] = int(int16_t(q.y >> 16));
+    v[4] = int(int16_t(q.z & 0xffff));
+    v[5] = int(int16_t(q.z >> 16));
+    v[6] = int(int16_t(q.w & 0xffff));
+    v[7] = int(int16_t(q.w >> 16));
+}
+
+__device__ __forceinline__ uint4 pack8(const int* v)
+{
+    uint4 q;
+    q.x = (uint32_t(uint16_t(v[0]))) | (uint32_t(uint16_t(v[1])) << 16);
+    q.y = (uint32_t(uint16_t(v[2]))) | (uint32_t(uint16_t(v[3])) << 16);
+    q.z = (uint32_t(uint16_t(v[4]))) | (uint32_t(uint16_t(v[5])) << 16);
+    q.w = (uint32_t(uint16_t(v[6]))) | (uint32_t(uint16_t(v[7])) << 16);
+    return q;
+}
+
+// Loads CPL E values (columns jb+1..jb+CPL) and E[jb] of predecessor row p:
+// from the LDS ring when p is among the last ring rows, from the HBM spill
+// copy otherwise, or zeros for the virtual row 0.  The two memory paths are
+// kept apart so the ring path compiles to ds_read_b128.
+template <int CPL>
+__device__ __forceinline__ void load_pred(const int16_t* ring, int ring_stride, int ring_mask, const int16_t* spill,
+                                          int stride, int r, int p, int jb, int (&cur)[CPL], int& prev)
 {
     if (p == 0)
     {
 #pragma unroll
-        for (int c = 0; c < 8; c++)
+        for (int c = 0; c < CPL; c++)
             cur[c] = 0;
         prev = 0;
-        return;
     }
-    const int16_t* row = (r - p <= ring_mask) ? ring + size_t(p & ring_mask) * ring_stride
-                                              : spill + size_t(p) * stride;
-    Pack8<int16_t>::load(row + jb + kColShift + 1, cur);
-    prev = int(row[jb + kColShift]);
+    else if (r - p <= ring_mask)
+    {
+        const int16_t* row = ring + (p & ring_mask) * ring_stride + jb + kColShift;
+#pragma unroll
+        for (int q = 0; q < CPL / 8; q++)
+            unpack8(*reinterpret_cast<const uint4*>(row + 1 + 8 * q), cur + 8 * q);
+        prev = int(row[0]);
+    }
+    else
+    {
+        const int16_t* row = spill + size_t(p) * stride + jb + kColShift;
+#pragma unroll
+        for (int q = 0; q < CPL / 8; q++)
+            unpack8(*reinterpret_cast<const uint4*>(row + 1 + 8 * q), cur + 8 * q);
+        prev = int(row[0]);
+    }
 }
 
 // Forward pass; returns the end row (first sink with the strictly greatest
 // last-column score, cudapoa_nw.cuh:332-349 with rows in the current
-// topological order).
-template <typename SizeT>
+// topological order).  Each lane owns CPL consecutive columns; one pass of
+// the wave covers 64*CPL columns (a whole 1-kb read in one pass at CPL=24).
+template <int CPL, typename SizeT>
 __device__ int nw_forward_lds(const WinGraph<SizeT>& g, const RowProg& P, int V, const uint8_t* read, int L,
                               int16_t* ring, int ring_stride, int16_t* spill, int stride, uint8_t* codes,
                               int code_stride, const Scores sc, int lane)
 {
-    const int gap  = sc.gap;
-    const int s_eq = sc.match - gap; // diagonal step in the E domain
-    const int s_ne = sc.mismatch - gap;
-    const int mask = P.ring_mask;
+    constexpr int kPass = kWave * CPL;
+    const int gap       = sc.gap;
+    const int s_eq      = sc.match - gap; // diagonal step in the E domain
+    const int s_ne      = sc.mismatch - gap;
+    const int mask      = P.ring_mask;
     // row 0 (E == 0 everywhere) in ring slot 0
     for (int j = lane; j < ring_stride; j += kWave)
         ring[j] = 0;
-    int best_row = 0;
-    int best_val = INT_MIN;
-    const int last_lane = (L - 1) / kCellsPerLane % kWave; // lane owning column L in the last chunk
-    const int last_c    = (L - 1) % kCellsPerLane;
+    int best_row        = 0;
+    int best_val        = INT_MIN;
+    const int last_lane = ((L - 1) / CPL) % kWave; // lane owning column L in the last pass
+    const int last_c    = (L - 1) % CPL;
     for (int r = 1; r <= V; r++)
     {
         const uint32_t rec = P.rec[r];
         const int base     = int(rec & 0xff);
         const int np       = uniform(prog_np(g, r, rec));
         const bool spill_r = (rec >> 15) & 1;
-        int16_t* row       = ring + size_t(r & mask) * ring_stride;
+        int16_t* row       = ring + (r & mask) * ring_stride;
         int16_t* srow      = spill + size_t(r) * stride;
         uint8_t* crow      = codes + size_t(r) * code_stride;
         // column 0: vertical from the first predecessor with the largest E[.][0]
@@ -511,7 +568,7 @@ __device__ int nw_forward_lds(const WinGraph<SizeT>& g, const RowProg& P, int V,
                 if (p == 0)
                     v = 0;
                 else if (r - p <= mask)
-                    v = int(ring[size_t(p & mask) * ring_stride + kColShift]);
+                    v = int(ring[(p & mask) * ring_stride + kColShift]);
                 else
                     v = int(spill[size_t(p) * stride + kColShift]);
                 if (v > c0)
@@ -529,38 +586,42 @@ __device__ int nw_forward_lds(const WinGraph<SizeT>& g, const RowProg& P, int V,
         const int p0 = np == 0 ? 0 : uniform(prog_pred(P, g, r, rec, 0));
         int carry    = c0;
         int endv     = (L == 0) ? c0 : kNeg;
-        for (int cb = 0; cb < L; cb += kChunk)
+        for (int cb = 0; cb < L; cb += kPass)
         {
-            const int jb      = cb + lane * kCellsPerLane;
+            const int jb      = cb + lane * CPL;
             const bool active = jb < L;
-            int sig[8], dg0[8], vt0[8], D[8];
+            int sig[CPL], dg0[CPL], vt0[CPL], E[CPL];
             if (active)
             {
-                const uint2 rc = *reinterpret_cast<const uint2*>(read + jb);
 #pragma unroll
-                for (int c = 0; c < 8; c++)
+                for (int q = 0; q < CPL / 8; q++)
                 {
-                    const int ch = int(((c < 4 ? rc.x : rc.y) >> (8 * (c & 3))) & 0xff);
-                    sig[c]       = (ch == base) ? s_eq : s_ne;
-                }
-                int cur[8], prev;
-                load_pred8(ring, ring_stride, mask, spill, stride, r, p0, jb, cur, prev);
+                    const uint2 rc = *reinterpret_cast<const uint2*>(read + jb + 8 * q);
 #pragma unroll
-                for (int c = 0; c < 8; c++)
+                    for (int c = 0; c < 8; c++)
+                    {
+                        const int ch    = int(((c < 4 ? rc.x : rc.y) >> (8 * (c & 3))) & 0xff);
+                        sig[8 * q + c] = (ch == base) ? s_eq : s_ne;
+                    }
+                }
+                int cur[CPL], prev;
+                load_pred<CPL>(ring, ring_stride, mask, spill, stride, r, p0, jb, cur, prev);
+#pragma unroll
+                for (int c = 0; c < CPL; c++)
                 {
                     dg0[c] = prev + sig[c];
                     vt0[c] = cur[c] + gap;
-                    D[c]   = max(dg0[c], vt0[c]);
+                    E[c]   = max(dg0[c], vt0[c]);
                     prev   = cur[c];
                 }
                 for (int k = 1; k < np; k++)
                 {
                     const int p = uniform(prog_pred(P, g, r, rec, k));
-                    load_pred8(ring, ring_stride, mask, spill, stride, r, p, jb, cur, prev);
+                    load_pred<CPL>(ring, ring_stride, mask, spill, stride, r, p, jb, cur, prev);
 #pragma unroll
-                    for (int c = 0; c < 8; c++)
+                    for (int c = 0; c < CPL; c++)
                     {
-                        D[c] = max(D[c], max(prev + sig[c], cur[c] + gap));
+                        E[c] = max(E[c], max(prev + sig[c], cur[c] + gap));
                         prev = cur[c];
                     }
                 }
@@ -568,80 +629,75 @@ __device__ int nw_forward_lds(const WinGraph<SizeT>& g, const RowProg& P, int V,
             else
             {
 #pragma unroll
-                for (int c = 0; c < 8; c++)
-                    D[c] = dg0[c] = vt0[c] = kNeg;
+                for (int c = 0; c < CPL; c++)
+                    E[c] = dg0[c] = vt0[c] = sig[c] = kNeg;
             }
-            // prefix maximum across the row
-            int E[8];
+            // prefix maximum across the row (the horizontal gap closure)
             int m = kNeg;
 #pragma unroll
-            for (int c = 0; c < 8; c++)
+            for (int c = 0; c < CPL; c++)
             {
-                m    = max(m, D[c]);
+                m    = max(m, E[c]);
                 E[c] = m;
             }
             const int incl  = wave_incl_max_dpp(m);
             const int excl  = __builtin_amdgcn_update_dpp(kNeg, incl, 0x138, 0xf, 0xf, false); // wave_shr:1
             const int below = max(excl, carry);
 #pragma unroll
-            for (int c = 0; c < 8; c++)
+            for (int c = 0; c < CPL; c++)
                 E[c] = max(E[c], below);
             carry = max(carry, __builtin_amdgcn_readlane(incl, kWave - 1));
             if (active)
             {
                 // traceback codes: diagonal over predecessors in slot order, then
                 // vertical, then horizontal (cudapoa_nw.cuh:361-443)
-                int code[8];
-                int kd[8], kv[8];
-#pragma unroll
-                for (int c = 0; c < 8; c++)
-                    kd[c] = kv[c] = -1;
-                if (np >= 2)
+                int code[CPL];
+                if (np <= 1)
                 {
-                    for (int k = 1; k < np; k++)
+#pragma unroll
+                    for (int c = 0; c < CPL; c++)
+                        code[c] = dg0[c] == E[c] ? 0 : (vt0[c] == E[c] ? 1 : 2);
+                }
+                else
+                {
+                    int cd[CPL], cv[CPL];
+#pragma unroll
+                    for (int c = 0; c < CPL; c++)
+                        cd[c] = cv[c] = 255;
+                    for (int k = np - 1; k >= 0; k--)
                     {
                         const int p = uniform(prog_pred(P, g, r, rec, k));
-                        int cur[8], prev;
-                        load_pred8(ring, ring_stride, mask, spill, stride, r, p, jb, cur, prev);
+                        int cur[CPL], prev;
+                        load_pred<CPL>(ring, ring_stride, mask, spill, stride, r, p, jb, cur, prev);
 #pragma unroll
-                        for (int c = 0; c < 8; c++)
+                        for (int c = 0; c < CPL; c++)
                         {
-                            if (kd[c] < 0 && prev + sig[c] == E[c])
-                                kd[c] = k;
-                            if (kv[c] < 0 && cur[c] + gap == E[c])
-                                kv[c] = k;
-                            prev = cur[c];
+                            cd[c] = (prev + sig[c] == E[c]) ? (k << 2) : cd[c];
+                            cv[c] = (cur[c] + gap == E[c]) ? (1 | (k << 2)) : cv[c];
+                            prev  = cur[c];
                         }
                     }
+#pragma unroll
+                    for (int c = 0; c < CPL; c++)
+                        code[c] = cd[c] != 255 ? cd[c] : (cv[c] != 255 ? cv[c] : 2);
                 }
 #pragma unroll
-                for (int c = 0; c < 8; c++)
+                for (int q = 0; q < CPL / 8; q++)
                 {
-                    int cd;
-                    if (dg0[c] == E[c])
-                        cd = 0;
-                    else if (kd[c] >= 0)
-                        cd = kd[c] << 2;
-                    else if (vt0[c] == E[c])
-                        cd = 1;
-                    else if (kv[c] >= 0)
-                        cd = 1 | (kv[c] << 2);
-                    else
-                        cd = 2;
-                    code[c] = cd;
-                }
-                Pack8<int16_t>::store(row + jb + kColShift + 1, E);
-                if (spill_r)
-                    Pack8<int16_t>::store(srow + jb + kColShift + 1, E);
-                uint64_t cw = 0;
-#pragma unroll
-                for (int c = 0; c < 8; c++)
-                    cw |= uint64_t(code[c]) << (8 * c);
-                __builtin_nontemporal_store(cw, reinterpret_cast<uint64_t*>(crow + jb + kColShift + 1));
-                if (lane == last_lane && cb + kChunk >= L)
-                {
+                    const uint4 ev = pack8(E + 8 * q);
+                    *reinterpret_cast<uint4*>(row + jb + kColShift + 1 + 8 * q) = ev;
+                    if (spill_r)
+                        *reinterpret_cast<uint4*>(srow + jb + kColShift + 1 + 8 * q) = ev;
+                    uint64_t cw = 0;
 #pragma unroll
                     for (int c = 0; c < 8; c++)
+                        cw |= uint64_t(code[8 * q + c]) << (8 * c);
+                    __builtin_nontemporal_store(cw, reinterpret_cast<uint64_t*>(crow + jb + kColShift + 1 + 8 * q));
+                }
+                if (lane == last_lane && cb + kPass >= L)
+                {
+#pragma unroll
+                    for (int c = 0; c < CPL; c++)
                         if (c == last_c)
                             endv = E[c];
                 }
@@ -726,7 +782,7 @@ __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V
     return n;
 }
 
-template <bool MSA>
+template <bool MSA, int CPL>
 __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d, Scores sc)
 {
     using SizeT  = int16_t;
@@ -773,14 +829,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
     uint16_t* ecovc  = MSA ? b.edge_cov_cnt + w * mn * kMaxEdges : nullptr;
     SizeT* seq_begin = MSA ? static_cast<SizeT*>(b.seq_begin) + size_t(w) * d.max_seqs : nullptr;
 
-    uint64_t ph[kPhases] = {0, 0, 0, 0, 0, 0, 0};
-    const uint64_t t_begin = now_ticks();
-    uint64_t t_mark        = t_begin;
-    auto lap = [&](int p) {
-        uint64_t t = now_ticks();
-        ph[p] += t - t_mark;
-        t_mark = t;
-    };
+    PhaseTimer ph;
     const WindowDesc wd = b.windows[w];
     const int nseq      = wd.num_seqs;
     int status          = kSuccess;
@@ -794,7 +843,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
         const int8_t* w0    = b.wts + b.seq_off[wd.first_seq];
         build_backbone<SizeT, MSA>(g, seq0, w0, len0, lane, ecov, ecovc, seq_begin, d.max_seqs);
         node_count = len0;
-        lap(kPhBackbone);
+        ph.lap<kPhBackbone>();
         for (int s = 1; s < nseq; s++)
         {
             if (node_count >= d.max_nodes)
@@ -806,16 +855,16 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
             const int64_t off     = b.seq_off[wd.first_seq + s];
             const uint8_t* read_g = b.seqs + off;
             const int8_t* wts_g   = b.wts + off;
-            const int padded      = (L + 16 + 15) & ~15;
+            const int padded      = (L + 32 + 15) & ~15;
             for (int j = lane; j < padded; j += kWave)
                 lread[j] = j < L ? read_g[j] : 0;
             const int V = node_count;
             build_row_program<SizeT>(g, V, rec, xl, d.lds_xl_cap, d.lds_ring_rows, lane);
             cells += int64_t(V + 1) * (L + 1);
-            const int end_row = nw_forward_lds<SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride, codes,
+            const int end_row = nw_forward_lds<CPL, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride, codes,
                                                       d.code_stride, sc, lane);
             __syncthreads();
-            lap(kPhForward);
+            ph.lap<kPhForward>();
             const int alen = traceback_codes<SizeT>(g, P, V, L, end_row, codes, d.code_stride, tile, ag, ar,
                                                     d.aln_cap, lane);
             __syncthreads();
@@ -827,7 +876,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
                     ag[k] = g.sorted[rr - 1];
             }
             __syncthreads();
-            lap(kPhTraceback);
+            ph.lap<kPhTraceback>();
             if (alen == -1)
             {
                 status = kLoopCountExceeded;
@@ -838,10 +887,10 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
                 int nc     = node_count;
                 uint8_t rc = add_alignment<SizeT, MSA>(g, nc, ag, ar, alen, read_g, wts_g, s, ecov, ecovc, seq_begin,
                                                        d.max_seqs);
-                lap(kPhAdd);
+                ph.lap<kPhAdd>();
                 if (rc == kSuccess)
                     topsort_kahn<SizeT>(g, nc, cscore);
-                lap(kPhTopsort);
+                ph.lap<kPhTopsort>();
                 sh_status = rc;
                 sh_len    = nc;
             }
@@ -854,15 +903,11 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
     }
     finish_window<SizeT, MSA>(b, d, w, lane, g, status, nseq, node_count, cscore, cpred, ecov, ecovc, seq_begin,
                               sh_len, sh_status);
-    lap(kPhOutput);
+    ph.lap<kPhOutput>();
     if (lane == 0)
     {
         if (b.phase)
-        {
-            ph[kPhTotal] = now_ticks() - t_begin;
-            for (int p = 0; p < kPhases; p++)
-                b.phase[size_t(w) * kPhases + p] = int64_t(ph[p]);
-        }
+            ph.store(b.phase + size_t(w) * kPhases);
         b.final_nodes[w] = node_count;
         b.cells[w]       = cells;
     }
@@ -883,12 +928,28 @@ extern "C" hipError_t gwamd_internal_poa_launch(const gwamd::poa::Buffers* b, co
     dim3 grid(b->num_windows), block(kWave);
     if (d->lds_kernel && !banded && score_bits == 16 && size_bits == 16)
     {
-        if (msa)
-            hipLaunchKernelGGL((poa_window_kernel_lds<true>), grid, block, size_t(d->lds_bytes), stream, *b, *d, *sc);
-        else
-            hipLaunchKernelGGL((poa_window_kernel_lds<false>), grid, block, size_t(d->lds_bytes), stream, *b, *d,
-                               *sc);
-        return hipGetLastError();
+        const size_t lb = size_t(d->lds_bytes);
+#define GWAMD_LDS_LAUNCH(CPL)                                                                                  \
+    if (msa)                                                                                                   \
+        hipLaunchKernelGGL((poa_window_kernel_lds<true, CPL>), grid, block, lb, stream, *b, *d, *sc);          \
+    else                                                                                                       \
+        hipLaunchKernelGGL((poa_window_kernel_lds<false, CPL>), grid, block, lb, stream, *b, *d, *sc);         \
+    return hipGetLastError();
+        // columns per lane: one wave pass covers the longest read when possible
+        if (d->max_seq_len <= 512)
+        {
+            GWAMD_LDS_LAUNCH(8)
+        }
+        if (d->max_seq_len <= 1024)
+        {
+            GWAMD_LDS_LAUNCH(16)
+        }
+        if (d->max_seq_len <= 1536)
+        {
+            GWAMD_LDS_LAUNCH(24)
+        }
+        GWAMD_LDS_LAUNCH(32)
+#undef GWAMD_LDS_LAUNCH
     }
     const int lds_bytes = (d->max_seq_len > d->band_width + kBandPad ? d->max_seq_len : d->band_width + kBandPad) + 32;
     const size_t lds    = size_t((lds_bytes + 15) & ~15);
