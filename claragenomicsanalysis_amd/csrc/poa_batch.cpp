@@ -524,14 +524,16 @@ private:
         auto a16             = [](int64_t v) { return (v + 15) & ~int64_t(15); };
         const int ring_rows  = 8;
         const int64_t read_b = a16(int64_t(dims_.max_seq_len) + 48);
-        const int64_t ring_b = std::max<int64_t>(int64_t(ring_rows) * dims_.score_stride * 2,
-                                                 int64_t(gwamd::poa::kTileRows) * gwamd::poa::kTileCols);
+        // the ring region also holds one traceback tile and the add-alignment scratch
+        const int64_t add_b  = 5 * a16(dims_.max_seq_len + 16) + 2 * (int64_t(dims_.max_nodes) + dims_.max_seq_len);
+        const int64_t ring_b = std::max<int64_t>({int64_t(ring_rows) * dims_.score_stride * 2,
+                                                  int64_t(gwamd::poa::kTileRows) * gwamd::poa::kTileCols, add_b});
         const int64_t rec_b  = a16(int64_t(dims_.max_nodes + 1) * 4);
         const int64_t fixed  = read_b + ring_b + rec_b;
-        const int64_t target = 40960;
+        const int64_t target = 40960 - 256 - 16; // keep 4 workgroups per CU incl. static LDS
         int64_t xl_cap       = std::max<int64_t>(1024, (target - fixed) / 2);
         xl_cap               = std::min<int64_t>(xl_cap, 65535);
-        const int64_t total  = fixed + a16(xl_cap * 2);
+        const int64_t total  = fixed + a16(xl_cap * 2) + 16;
         if (total > 65536)
             return;
         dims_.lds_kernel    = 1;
@@ -541,6 +543,7 @@ private:
         dims_.lds_xl_off    = int32_t(read_b + ring_b + rec_b);
         dims_.lds_xl_cap    = int32_t(xl_cap);
         dims_.lds_bytes     = int32_t(total);
+        dims_.lds_sh_off    = int32_t(total - 16);
         dims_.code_stride   = int32_t(a16(int64_t(dims_.max_seq_len) + 48));
     }
 

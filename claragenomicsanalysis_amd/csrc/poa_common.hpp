@@ -67,6 +67,7 @@ struct Dims
     int32_t lds_xl_off;     // extra predecessor rows (u16)
     int32_t lds_xl_cap;
     int32_t code_stride;    // bytes per traceback-code row
+    int32_t lds_sh_off;     // small shared ints (add/topsort control)
 };
 
 constexpr int kTileRows = 128; // traceback tile (codes) rows

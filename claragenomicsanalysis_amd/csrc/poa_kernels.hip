@@ -418,19 +418,23 @@ __device__ void build_row_program(const WinGraph<SizeT>& g, int V, uint32_t* rec
     {
         const int r      = r0 + lane;
         const bool valid = r <= V;
-        int node = 0, np = 0, base = 0, sink = 0;
+        int node = 0, np = 0, base = 0, sink = 0, spill = 0;
         if (valid)
         {
-            node = int(g.sorted[r - 1]);
-            np   = int(g.in_cnt[node]);
-            base = int(g.base[node]);
-            sink = g.out_cnt[node] == 0 ? 1 : 0;
+            node         = int(g.sorted[r - 1]);
+            np           = int(g.in_cnt[node]);
+            base         = int(g.base[node]);
+            const int oc = int(g.out_cnt[node]);
+            sink         = oc == 0 ? 1 : 0;
+            // spill: a successor reads this row from >= ring_rows rows later
+            for (int e = 0; e < oc; e++)
+                spill |= (int(g.pos[int(g.out_e[node * kMaxEdges + e])]) + 1 - r) >= ring_rows ? 1 : 0;
         }
         int total      = 0;
         const int excl = wave_excl_sum(np >= 2 ? np : 0, lane, total);
         if (valid)
         {
-            uint32_t v = uint32_t(base) | (uint32_t(sink) << 14);
+            uint32_t v = uint32_t(base) | (uint32_t(sink) << 14) | (uint32_t(spill) << 15);
             if (np == 1)
             {
                 const int p = pred_row(g, node, 0);
@@ -451,20 +455,6 @@ __device__ void build_row_program(const WinGraph<SizeT>& g, int V, uint32_t* rec
             rec[r] = v;
         }
         xbase += total;
-    }
-    __syncthreads();
-    // spill marks: a row read from >= ring_rows rows later must also go to HBM
-    for (int r = 1 + lane; r <= V; r += kWave)
-    {
-        const uint32_t v = rec[r];
-        RowProg P{rec, xl, ring_rows - 1};
-        const int np = prog_np(g, r, v);
-        for (int k = 0; k < np; k++)
-        {
-            const int p = prog_pred(P, g, r, v, k);
-            if (p != 0 && r - p >= ring_rows)
-                atomicOr(&rec[p], 1u << 15);
-        }
     }
     __syncthreads();
 }
@@ -499,6 +489,14 @@ template <int CPL>
 __device__ __forceinline__ void load_pred(const int16_t* ring, int ring_stride, int ring_mask, const int16_t* spill,
                                           int stride, int r, int p, int jb, int (&cur)[CPL], int& prev)
 {
+    // The ring slot is always read (a valid LDS address even when the row is
+    // not there) so the compiler never merges the LDS and HBM paths into one
+    // flat pointer; the rare far predecessor then overrides from HBM.
+    const int16_t* lrow = ring + (p & ring_mask) * ring_stride + jb + kColShift;
+#pragma unroll
+    for (int q = 0; q < CPL / 8; q++)
+        unpack8(*reinterpret_cast<const uint4*>(lrow + 1 + 8 * q), cur + 8 * q);
+    prev = int(lrow[0]);
     if (p == 0)
     {
 #pragma unroll
@@ -506,21 +504,13 @@ __device__ __forceinline__ void load_pred(const int16_t* ring, int ring_stride, 
             cur[c] = 0;
         prev = 0;
     }
-    else if (r - p <= ring_mask)
+    else if (r - p > ring_mask)
     {
-        const int16_t* row = ring + (p & ring_mask) * ring_stride + jb + kColShift;
+        const int16_t* grow = spill + size_t(p) * stride + jb + kColShift;
 #pragma unroll
         for (int q = 0; q < CPL / 8; q++)
-            unpack8(*reinterpret_cast<const uint4*>(row + 1 + 8 * q), cur + 8 * q);
-        prev = int(row[0]);
-    }
-    else
-    {
-        const int16_t* row = spill + size_t(p) * stride + jb + kColShift;
-#pragma unroll
-        for (int q = 0; q < CPL / 8; q++)
-            unpack8(*reinterpret_cast<const uint4*>(row + 1 + 8 * q), cur + 8 * q);
-        prev = int(row[0]);
+            unpack8(*reinterpret_cast<const uint4*>(grow + 1 + 8 * q), cur + 8 * q);
+        prev = int(grow[0]);
     }
 }
 
@@ -564,12 +554,10 @@ __device__ int nw_forward_lds(const WinGraph<SizeT>& g, const RowProg& P, int V,
             for (int k = 0; k < np; k++)
             {
                 const int p = uniform(prog_pred(P, g, r, rec, k));
-                int v;
+                int v = int(ring[(p & mask) * ring_stride + kColShift]);
                 if (p == 0)
                     v = 0;
-                else if (r - p <= mask)
-                    v = int(ring[(p & mask) * ring_stride + kColShift]);
-                else
+                else if (r - p > mask)
                     v = int(spill[size_t(p) * stride + kColShift]);
                 if (v > c0)
                     c0 = v, c0k = k;
@@ -782,6 +770,331 @@ __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V
     return n;
 }
 
+// ---------------------------------------------------------------------------
+// Wave-parallel addAlignmentToGraph (cudapoa_add_alignment.cuh:59-279).
+//
+// The traceback visits every read position exactly once, in increasing
+// order, so element rp of the sequential loop is read base rp and its head is
+// element rp-1's node.  When every element's node is distinct and no two
+// elements touch the same aligned-node group, the sequential loop's writes are
+// independent and are done by one lane per element; the new node ids are a
+// prefix sum, and the first error (node or edge limit) is found by a min
+// over positions.  Otherwise nothing is written and -1 is returned so the
+// caller runs the sequential restatement.
+#define GWAMD_LDS __attribute__((address_space(3)))
+struct AddScratch
+{
+    GWAMD_LDS uint16_t* gid;   // [max_seq] aligned graph node per read position (0xffff = none)
+    GWAMD_LDS uint16_t* curr;  // [max_seq] node the read base lands on
+    GWAMD_LDS uint8_t* kind;   // [max_seq] 0 same base, 1 aligned hit, 2 new, 3 new + ring; bit 2: edge exists
+    GWAMD_LDS uint16_t* owner; // [max_nodes + max_seq] element that claimed a node (last writer wins)
+    GWAMD_LDS int* sh;         // [0] conflict
+};
+
+template <typename SizeT, bool MSA>
+__device__ int add_alignment_parallel(WinGraph<SizeT>& g, int& node_count, const SizeT* ag, const SizeT* ar,
+                                      int alen, int L, const uint8_t* read, const int8_t* w, int s, uint16_t* ecov,
+                                      uint16_t* ecov_cnt, SizeT* seq_begin, int max_seqs, const AddScratch& X,
+                                      int lane)
+{
+    const int nc0 = node_count;
+    int err       = INT_MAX; // first error in read order: (pos << 8) | status
+    if (lane == 0)
+        X.sh[0] = 0;
+    for (int k = lane; k < alen; k += kWave)
+    {
+        const int rp = int(ar[k]);
+        if (rp >= 0 && rp < L)
+            X.gid[rp] = uint16_t(int(ag[k]) < 0 ? 0xffff : int(ag[k]));
+    }
+    __syncthreads();
+    // kinds and existing targets
+    for (int rp = lane; rp < L; rp += kWave)
+    {
+        const int gid    = int(X.gid[rp]);
+        const uint8_t rb = read[rp];
+        int kind = 2, curr = 0;
+        if (gid != 0xffff)
+        {
+            if (g.base[gid] == rb)
+                kind = 0, curr = gid;
+            else
+            {
+                kind         = 3;
+                const int na = int(g.aln_cnt[gid]);
+                for (int n = 0; n < na; n++)
+                {
+                    const int aid = int(g.aln[gid * kMaxAlignments + n]);
+                    if (g.base[aid] == rb)
+                    {
+                        kind = 1, curr = aid;
+                        break;
+                    }
+                }
+            }
+        }
+        X.kind[rp] = uint8_t(kind);
+        X.curr[rp] = uint16_t(curr);
+    }
+    __syncthreads();
+    // new node ids: prefix sum over new-node elements in read order
+    int nnew = 0;
+    for (int r0 = 0; r0 < L; r0 += kWave)
+    {
+        const int rp     = r0 + lane;
+        const bool isnew = rp < L && X.kind[rp] >= 2;
+        int total        = 0;
+        const int excl   = wave_excl_sum(isnew ? 1 : 0, lane, total);
+        if (isnew)
+        {
+            const int id = nc0 + nnew + excl;
+            X.curr[rp]   = uint16_t(id);
+            if (id + 1 >= g.max_nodes)
+                err = min(err, (rp << 8) | int(kNodeCountExceeded));
+        }
+        nnew += total;
+    }
+    __syncthreads();
+    // independence checks without atomics: every element claims its node (and,
+    // for aligned hits / ring updates, its aligned group); after a barrier an
+    // element that no longer owns a claimed node has a conflicting partner.
+    for (int rp = lane; rp < L; rp += kWave)
+        X.owner[int(X.curr[rp])] = uint16_t(rp);
+    __syncthreads();
+    bool conflict = false;
+    for (int rp = lane; rp < L; rp += kWave)
+        conflict |= int(X.owner[int(X.curr[rp])]) != rp;
+    __syncthreads();
+    for (int rp = lane; rp < L; rp += kWave)
+    {
+        const int kind = X.kind[rp];
+        if (kind == 1 || kind == 3)
+        {
+            const int gid = int(X.gid[rp]);
+            X.owner[gid]  = uint16_t(rp);
+            const int na  = int(g.aln_cnt[gid]);
+            for (int n = 0; n < na; n++)
+                X.owner[int(g.aln[gid * kMaxAlignments + n])] = uint16_t(rp);
+        }
+    }
+    __syncthreads();
+    for (int rp = lane; rp < L; rp += kWave)
+    {
+        const int kind = X.kind[rp];
+        if (kind == 1 || kind == 3)
+        {
+            const int gid = int(X.gid[rp]);
+            conflict |= int(X.owner[gid]) != rp;
+            const int na = int(g.aln_cnt[gid]);
+            for (int n = 0; n < na; n++)
+                conflict |= int(X.owner[int(g.aln[gid * kMaxAlignments + n])]) != rp;
+        }
+    }
+    if (conflict)
+        X.sh[0] = 1;
+    __syncthreads();
+    if (X.sh[0])
+        return -1;
+    // edge existence and edge-limit errors
+    for (int rp = lane + 1; rp < L; rp += kWave)
+    {
+        const int head = int(X.curr[rp - 1]);
+        const int curr = int(X.curr[rp]);
+        const int kind = X.kind[rp];
+        bool exists    = false;
+        int ic         = 0;
+        if (kind < 2)
+        {
+            ic = int(g.in_cnt[curr]);
+            for (int e = 0; e < ic; e++)
+                exists |= int(g.in_e[curr * kMaxEdges + e]) == head;
+        }
+        if (!exists)
+        {
+            const int oc = X.kind[rp - 1] >= 2 ? 0 : int(g.out_cnt[head]);
+            if (oc + 1 >= kMaxEdges || ic + 1 >= kMaxEdges)
+                err = min(err, (rp << 8) | int(kEdgeCountExceeded));
+        }
+        else
+            X.kind[rp] = uint8_t(kind | 4);
+    }
+    err = -wave_max(-err); // wave-wide minimum
+    if (err != INT_MAX)
+        return err & 0xff;
+    __syncthreads();
+    // writes 1: new nodes and aligned rings (one lane per element)
+    for (int rp = lane; rp < L; rp += kWave)
+    {
+        const int kind = X.kind[rp] & 3;
+        if (kind < 2)
+            continue;
+        const int curr  = int(X.curr[rp]);
+        g.base[curr]    = read[rp];
+        g.out_cnt[curr] = 0;
+        g.in_cnt[curr]  = 0;
+        g.aln_cnt[curr] = 0;
+        g.cov[curr]     = 0;
+        if (kind == 3)
+        {
+            const int gid = int(X.gid[rp]);
+            const int na  = int(g.aln_cnt[gid]);
+            int cnt       = 0;
+            for (int n = 0; n < na; n++)
+            {
+                const int aid                      = int(g.aln[gid * kMaxAlignments + n]);
+                const int ac                       = int(g.aln_cnt[aid]);
+                g.aln[aid * kMaxAlignments + ac]   = SizeT(curr);
+                g.aln_cnt[aid]                     = uint16_t(ac + 1);
+                g.aln[curr * kMaxAlignments + cnt] = SizeT(aid);
+                cnt++;
+            }
+            g.aln[gid * kMaxAlignments + na]   = SizeT(curr);
+            g.aln_cnt[gid]                     = uint16_t(na + 1);
+            g.aln[curr * kMaxAlignments + cnt] = SizeT(gid);
+            g.aln_cnt[curr]                    = uint16_t(cnt + 1);
+        }
+    }
+    __syncthreads();
+    // writes 2: the edge head -> curr and the coverage of curr
+    for (int rp = lane; rp < L; rp += kWave)
+    {
+        const int curr = int(X.curr[rp]);
+        if (MSA && rp == 0)
+            seq_begin[s] = SizeT(curr);
+        if (rp > 0)
+        {
+            const int head = int(X.curr[rp - 1]);
+            const int wsum = int(uint16_t(int(w[rp - 1]))) + int(w[rp]);
+            if (X.kind[rp] & 4)
+            {
+                const int ic = int(g.in_cnt[curr]);
+                for (int e = 0; e < ic; e++)
+                    if (int(g.in_e[curr * kMaxEdges + e]) == head)
+                        g.in_w[curr * kMaxEdges + e] = uint16_t(int(g.in_w[curr * kMaxEdges + e]) + wsum);
+                if (MSA)
+                {
+                    const int oc = int(g.out_cnt[head]);
+                    for (int e = 0; e < oc; e++)
+                    {
+                        if (int(g.out_e[head * kMaxEdges + e]) == curr)
+                        {
+                            const int c                                       = int(ecov_cnt[head * kMaxEdges + e]);
+                            ecov[size_t(head * kMaxEdges + e) * max_seqs + c] = uint16_t(s);
+                            ecov_cnt[head * kMaxEdges + e]                    = uint16_t(c + 1);
+                            break;
+                        }
+                    }
+                }
+            }
+            else
+            {
+                const int ic                   = int(g.in_cnt[curr]);
+                g.in_e[curr * kMaxEdges + ic]  = SizeT(head);
+                g.in_w[curr * kMaxEdges + ic]  = uint16_t(wsum);
+                g.in_cnt[curr]                 = uint16_t(ic + 1);
+                const int oc                   = int(g.out_cnt[head]);
+                g.out_e[head * kMaxEdges + oc] = SizeT(curr);
+                if (MSA)
+                {
+                    ecov_cnt[head * kMaxEdges + oc]                = 1;
+                    ecov[size_t(head * kMaxEdges + oc) * max_seqs] = uint16_t(s);
+                }
+                g.out_cnt[head] = uint16_t(oc + 1);
+            }
+        }
+        g.cov[curr]++;
+    }
+    node_count = nc0 + nnew;
+    __syncthreads();
+    return kSuccess;
+}
+
+// ---------------------------------------------------------------------------
+// Kahn topological sort (cudapoa_topsort.cuh:38-88) over an LDS copy of the
+// out-edge lists (CSR): the adjacency is staged wave-parallel, the sources
+// are compacted in id order in parallel, and lane 0 runs the FIFO on LDS.
+// Returns false (nothing written) when the scratch is too small.
+template <typename SizeT>
+__device__ bool topsort_lds(WinGraph<SizeT>& g, int n, GWAMD_LDS uint8_t* scratch, int scratch_bytes,
+                            GWAMD_LDS int* sh, int lane)
+{
+    GWAMD_LDS uint32_t* off   = (GWAMD_LDS uint32_t*)(scratch);
+    GWAMD_LDS uint16_t* queue = (GWAMD_LDS uint16_t*)(scratch + (n + 1) * 4);
+    GWAMD_LDS uint8_t* cnt    = scratch + (n + 1) * 4 + n * 2;
+    const int head_bytes      = ((n + 1) * 4 + n * 2 + n + 15) & ~15;
+    GWAMD_LDS uint16_t* edges = (GWAMD_LDS uint16_t*)(scratch + head_bytes);
+    if (head_bytes > scratch_bytes)
+        return false;
+    const int edge_cap = (scratch_bytes - head_bytes) / 2;
+    int ebase          = 0;
+    for (int v0 = 0; v0 < n; v0 += kWave)
+    {
+        const int v  = v0 + lane;
+        const int oc = v < n ? int(g.out_cnt[v]) : 0;
+        int total    = 0;
+        const int ex = wave_excl_sum(oc, lane, total);
+        if (v < n)
+        {
+            off[v] = uint32_t(ebase + ex);
+            cnt[v] = uint8_t(g.in_cnt[v]);
+        }
+        ebase += total;
+    }
+    if (ebase > edge_cap)
+        return false;
+    if (lane == 0)
+        off[n] = uint32_t(ebase);
+    __syncthreads();
+    for (int v = lane; v < n; v += kWave)
+    {
+        const int o  = int(off[v]);
+        const int oc = int(off[v + 1]) - o;
+        for (int e = 0; e < oc; e++)
+            edges[o + e] = uint16_t(int(g.out_e[v * kMaxEdges + e]));
+    }
+    // sources in id order
+    int k = 0;
+    for (int v0 = 0; v0 < n; v0 += kWave)
+    {
+        const int v    = v0 + lane;
+        const bool src = v < n && cnt[v] == 0;
+        int total      = 0;
+        const int ex   = wave_excl_sum(src ? 1 : 0, lane, total);
+        if (src)
+            queue[k + ex] = uint16_t(v);
+        k += total;
+    }
+    __syncthreads();
+    if (lane == 0)
+    {
+        int tail = k;
+        for (int q = 0; q < tail; q++)
+        {
+            const int v  = int(queue[q]);
+            const int e1 = int(off[v + 1]);
+            for (int e = int(off[v]); e < e1; e++)
+            {
+                const int o = int(edges[e]);
+                const int c = int(cnt[o]) - 1;
+                cnt[o]      = uint8_t(c);
+                if (c == 0)
+                    queue[tail++] = uint16_t(o);
+            }
+        }
+        sh[0] = tail;
+    }
+    __syncthreads();
+    const int m = sh[0];
+    for (int q = lane; q < m; q += kWave)
+    {
+        const int v = int(queue[q]);
+        g.sorted[q] = SizeT(v);
+        g.pos[v]    = SizeT(q);
+    }
+    __syncthreads();
+    return true;
+}
+
 template <bool MSA, int CPL>
 __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d, Scores sc)
 {
@@ -803,6 +1116,17 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
     uint8_t* tile    = lds + d.lds_ring_off; // traceback tiles reuse the ring
     const int rstride = d.score_stride;      // ring / spill row stride (elements)
     RowProg P{rec, xl, d.lds_ring_rows - 1};
+    AddScratch AX;
+    {
+        // add-alignment scratch lives in the ring region (free between reads)
+        GWAMD_LDS uint8_t* a = (GWAMD_LDS uint8_t*)(lds) + d.lds_ring_off;
+        const int ms         = (d.max_seq_len + 16) & ~15;
+        AX.gid               = (GWAMD_LDS uint16_t*)(a);
+        AX.curr              = (GWAMD_LDS uint16_t*)(a + 2 * ms);
+        AX.kind              = a + 4 * ms;
+        AX.owner             = (GWAMD_LDS uint16_t*)(a + 5 * ms);
+        AX.sh                = (GWAMD_LDS int*)((GWAMD_LDS uint8_t*)(lds) + d.lds_sh_off);
+    }
 
     const size_t mn = size_t(d.max_nodes);
     WinGraph<SizeT> g;
@@ -882,23 +1206,36 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
                 status = kLoopCountExceeded;
                 break;
             }
-            if (lane == 0)
             {
-                int nc     = node_count;
-                uint8_t rc = add_alignment<SizeT, MSA>(g, nc, ag, ar, alen, read_g, wts_g, s, ecov, ecovc, seq_begin,
-                                                       d.max_seqs);
+                int nc = node_count;
+                int rc = add_alignment_parallel<SizeT, MSA>(g, nc, ag, ar, alen, L, lread, wts_g, s, ecov, ecovc,
+                                                             seq_begin, d.max_seqs, AX, lane);
+                if (rc < 0)
+                {
+                    if (lane == 0)
+                    {
+                        sh_status = add_alignment<SizeT, MSA>(g, nc, ag, ar, alen, read_g, wts_g, s, ecov, ecovc,
+                                                              seq_begin, d.max_seqs);
+                        sh_len    = nc;
+                    }
+                    __syncthreads();
+                    rc = sh_status;
+                    nc = sh_len;
+                }
                 ph.lap<kPhAdd>();
-                if (rc == kSuccess)
-                    topsort_kahn<SizeT>(g, nc, cscore);
+                status     = rc;
+                node_count = nc;
+                if (status != kSuccess)
+                    break;
+                if (!topsort_lds<SizeT>(g, node_count, (GWAMD_LDS uint8_t*)(lds) + d.lds_ring_off,
+                                        d.lds_bytes - d.lds_ring_off, AX.sh, lane))
+                {
+                    if (lane == 0)
+                        topsort_kahn<SizeT>(g, node_count, cscore);
+                    __syncthreads();
+                }
                 ph.lap<kPhTopsort>();
-                sh_status = rc;
-                sh_len    = nc;
             }
-            __syncthreads();
-            status     = sh_status;
-            node_count = sh_len;
-            if (status != kSuccess)
-                break;
         }
     }
     finish_window<SizeT, MSA>(b, d, w, lane, g, status, nseq, node_count, cscore, cpred, ecov, ecovc, seq_begin,
