@@ -701,6 +701,300 @@ __device__ int nw_forward_lds(const WinGraph<SizeT>& g, const RowProg& P, int V,
     return best_row;
 }
 
+// ---------------------------------------------------------------------------
+// Packed 16-bit forward pass.  E values are int16 (the E-domain bounds of a
+// window that selects 16-bit scores fit: cudapoa_limits.hpp:28-53), two cells
+// per 32-bit register, so the diagonal/vertical/max work runs on v_pk_*
+// instructions.  Cells beyond the read may wrap; they only feed cells further
+// right, never a cell <= L.
+typedef short pk_s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short pk_u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(pk_s16x2, a),
+                                                                  __builtin_bit_cast(pk_s16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(pk_u16x2, a) + __builtin_bit_cast(pk_u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(pk_u16x2, a) - __builtin_bit_cast(pk_u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_min_u(uint32_t a, uint32_t b)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(pk_u16x2, a),
+                                                                  __builtin_bit_cast(pk_u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(pk_u16x2, a) * __builtin_bit_cast(pk_u16x2, b) +
+                                            __builtin_bit_cast(pk_u16x2, c));
+}
+__device__ __forceinline__ uint32_t pk_bcast(int v) { return (uint32_t(uint16_t(v)) * 0x10001u); }
+
+// loads the packed E values of predecessor row p (NR registers) and E_p[jb]
+template <int NR>
+__device__ __forceinline__ void load_pred_pk(const int16_t* ring, int ring_stride, int ring_mask, const int16_t* spill,
+                                             int stride, int r, int p, int jb, uint32_t (&P)[NR], uint32_t& prev)
+{
+    const int16_t* lrow = ring + (p & ring_mask) * ring_stride + jb + kColShift;
+#pragma unroll
+    for (int q = 0; q < NR / 4; q++)
+    {
+        const uint4 v = *reinterpret_cast<const uint4*>(lrow + 1 + 8 * q);
+        P[4 * q] = v.x, P[4 * q + 1] = v.y, P[4 * q + 2] = v.z, P[4 * q + 3] = v.w;
+    }
+    prev = uint32_t(uint16_t(lrow[0]));
+    if (p == 0)
+    {
+#pragma unroll
+        for (int i = 0; i < NR; i++)
+            P[i] = 0;
+        prev = 0;
+    }
+    else if (r - p > ring_mask)
+    {
+        const int16_t* grow = spill + size_t(p) * stride + jb + kColShift;
+#pragma unroll
+        for (int q = 0; q < NR / 4; q++)
+        {
+            const uint4 v = *reinterpret_cast<const uint4*>(grow + 1 + 8 * q);
+            P[4 * q] = v.x, P[4 * q + 1] = v.y, P[4 * q + 2] = v.z, P[4 * q + 3] = v.w;
+        }
+        prev = uint32_t(uint16_t(grow[0]));
+    }
+}
+
+// diagonal sources E_p[j-1] for the lane's cells: element 2i-1 and 2i
+template <int NR>
+__device__ __forceinline__ void diag_src(const uint32_t (&P)[NR], uint32_t prev, uint32_t (&Dg)[NR])
+{
+    Dg[0] = __builtin_amdgcn_alignbyte(P[0], prev << 16, 2);
+#pragma unroll
+    for (int i = 1; i < NR; i++)
+        Dg[i] = __builtin_amdgcn_alignbyte(P[i], P[i - 1], 2);
+}
+
+template <int CPL, typename SizeT>
+__device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int V, const uint8_t* read, int L,
+                                 int16_t* ring, int ring_stride, int16_t* spill, int stride, uint8_t* codes,
+                                 int code_stride, const Scores sc, int lane)
+{
+    constexpr int NR    = CPL / 2;
+    constexpr int kPass = kWave * CPL;
+    const int gap       = sc.gap;
+    const int s_eq      = sc.match - gap;
+    const int s_ne      = sc.mismatch - gap;
+    const uint32_t gap2 = pk_bcast(gap);
+    const int mask      = P.ring_mask;
+    for (int j = lane; j < ring_stride; j += kWave)
+        ring[j] = 0;
+    int best_row        = 0;
+    int best_val        = INT_MIN;
+    const int last_lane = ((L - 1) / CPL) % kWave;
+    const int last_c    = (L - 1) % CPL;
+    const int npass     = (L + kPass - 1) / kPass;
+    // per-read substitution profiles for A, C, G, T (single-pass reads)
+    uint32_t sig_acgt[4][NR];
+    {
+        const int jb = (lane * CPL < L) ? lane * CPL : 0; // inactive lanes read a valid address
+#pragma unroll
+        for (int i = 0; i < NR; i++)
+        {
+            const int c0 = int(read[jb + 2 * i]), c1 = int(read[jb + 2 * i + 1]);
+            const char bases[4] = {'A', 'C', 'G', 'T'};
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                sig_acgt[b][i] = uint32_t(uint16_t(c0 == bases[b] ? s_eq : s_ne)) |
+                                 (uint32_t(uint16_t(c1 == bases[b] ? s_eq : s_ne)) << 16);
+        }
+    }
+    for (int r = 1; r <= V; r++)
+    {
+        const uint32_t rec = P.rec[r];
+        const int base     = int(rec & 0xff);
+        const int np       = uniform(prog_np(g, r, rec));
+        const bool spill_r = (rec >> 15) & 1;
+        int16_t* row       = ring + (r & mask) * ring_stride;
+        int16_t* srow      = spill + size_t(r) * stride;
+        uint8_t* crow      = codes + size_t(r) * code_stride;
+        int c0, c0k = 0;
+        if (np == 0)
+            c0 = gap;
+        else
+        {
+            c0 = kNeg;
+            for (int k = 0; k < np; k++)
+            {
+                const int p = uniform(prog_pred(P, g, r, rec, k));
+                int v       = int(ring[(p & mask) * ring_stride + kColShift]);
+                if (p == 0)
+                    v = 0;
+                else if (r - p > mask)
+                    v = int(spill[size_t(p) * stride + kColShift]);
+                if (v > c0)
+                    c0 = v, c0k = k;
+            }
+            c0 += gap;
+        }
+        if (lane == 0)
+        {
+            row[kColShift]  = int16_t(c0);
+            crow[kColShift] = uint8_t(1 | (c0k << 2));
+            if (spill_r)
+                srow[kColShift] = int16_t(c0);
+        }
+        const int p0 = np == 0 ? 0 : uniform(prog_pred(P, g, r, rec, 0));
+        int carry    = c0;
+        int endv     = (L == 0) ? c0 : kNeg;
+        for (int pass = 0; pass < npass; pass++)
+        {
+            const int cb      = pass * kPass;
+            const int jb      = cb + lane * CPL;
+            const bool active = jb < L;
+            const int ja      = active ? jb : 0; // address used by inactive lanes
+            uint32_t sig[NR];
+            if (npass == 1 && (base == 'A' || base == 'C' || base == 'G' || base == 'T'))
+            {
+                const int bi = base == 'A' ? 0 : base == 'C' ? 1 : base == 'G' ? 2 : 3;
+                if (bi == 0)
+                {
+#pragma unroll
+                    for (int i = 0; i < NR; i++)
+                        sig[i] = sig_acgt[0][i];
+                }
+                else if (bi == 1)
+                {
+#pragma unroll
+                    for (int i = 0; i < NR; i++)
+                        sig[i] = sig_acgt[1][i];
+                }
+                else if (bi == 2)
+                {
+#pragma unroll
+                    for (int i = 0; i < NR; i++)
+                        sig[i] = sig_acgt[2][i];
+                }
+                else
+                {
+#pragma unroll
+                    for (int i = 0; i < NR; i++)
+                        sig[i] = sig_acgt[3][i];
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int i = 0; i < NR; i++)
+                {
+                    const int ch0 = int(read[ja + 2 * i]), ch1 = int(read[ja + 2 * i + 1]);
+                    sig[i]        = uint32_t(uint16_t(ch0 == base ? s_eq : s_ne)) |
+                             (uint32_t(uint16_t(ch1 == base ? s_eq : s_ne)) << 16);
+                }
+            }
+            uint32_t Pv[NR], prev, dg[NR], vt[NR], kd[NR], kv[NR], E[NR];
+            load_pred_pk<NR>(ring, ring_stride, mask, spill, stride, r, p0, ja, Pv, prev);
+            diag_src<NR>(Pv, prev, dg);
+#pragma unroll
+            for (int i = 0; i < NR; i++)
+            {
+                dg[i] = pk_add(dg[i], sig[i]);
+                vt[i] = pk_add(Pv[i], gap2);
+                kd[i] = kv[i] = 0;
+            }
+            for (int k = 1; k < np; k++)
+            {
+                const int p = uniform(prog_pred(P, g, r, rec, k));
+                uint32_t Q[NR], qprev, dq[NR];
+                load_pred_pk<NR>(ring, ring_stride, mask, spill, stride, r, p, ja, Q, qprev);
+                diag_src<NR>(Q, qprev, dq);
+                const uint32_t kk = pk_bcast(k);
+#pragma unroll
+                for (int i = 0; i < NR; i++)
+                {
+                    // running maxima with the first maximising predecessor slot
+                    const uint32_t d  = pk_add(dq[i], sig[i]);
+                    const uint32_t nd = pk_max(dg[i], d);
+                    kd[i]             = pk_mad(pk_min_u(pk_sub(nd, dg[i]), 0x00010001u), pk_sub(kk, kd[i]), kd[i]);
+                    dg[i]             = nd;
+                    const uint32_t v  = pk_add(Q[i], gap2);
+                    const uint32_t nv = pk_max(vt[i], v);
+                    kv[i]             = pk_mad(pk_min_u(pk_sub(nv, vt[i]), 0x00010001u), pk_sub(kk, kv[i]), kv[i]);
+                    vt[i]             = nv;
+                }
+            }
+            // in-lane prefix maximum
+            uint32_t c = 0x80008000u;
+#pragma unroll
+            for (int i = 0; i < NR; i++)
+            {
+                const uint32_t dmax = pk_max(dg[i], vt[i]);
+                uint32_t s          = pk_max(dmax, (dmax << 16) | 0x8000u);
+                s                   = pk_max(s, c);
+                E[i]                = s;
+                c                   = __builtin_amdgcn_perm(s, s, 0x07060706u);
+            }
+            const int m     = active ? int(int16_t(E[NR - 1] >> 16)) : kNeg;
+            const int incl  = wave_incl_max_dpp(m);
+            const int excl  = __builtin_amdgcn_update_dpp(kNeg, incl, 0x138, 0xf, 0xf, false);
+            const int below = max(excl, carry);
+            carry           = max(carry, __builtin_amdgcn_readlane(incl, kWave - 1));
+            const uint32_t b2 = pk_bcast(below);
+#pragma unroll
+            for (int i = 0; i < NR; i++)
+                E[i] = pk_max(E[i], b2);
+            if (active)
+            {
+                // codes: 0 diagonal, 1 vertical, 2 horizontal (+ slot << 2)
+                uint32_t code[NR];
+#pragma unroll
+                for (int i = 0; i < NR; i++)
+                {
+                    const uint32_t a  = pk_min_u(pk_sub(E[i], dg[i]), 0x00010001u); // 0: diagonal match
+                    const uint32_t bb = pk_min_u(pk_sub(E[i], vt[i]), 0x00010001u); // 0: vertical match
+                    const uint32_t cv = pk_mad(kv[i], 0x00040004u, 0x00010001u);     // 1 | kv << 2
+                    const uint32_t cvh = pk_mad(bb, pk_sub(0x00020002u, cv), cv);    // vertical or horizontal
+                    const uint32_t cd = kd[i] << 2;                                  // kd < 64: no cross-half carry
+                    code[i]           = pk_mad(a, pk_sub(cvh, cd), cd);
+                }
+#pragma unroll
+                for (int q = 0; q < NR / 4; q++)
+                {
+                    const uint4 ev = make_uint4(E[4 * q], E[4 * q + 1], E[4 * q + 2], E[4 * q + 3]);
+                    *reinterpret_cast<uint4*>(row + jb + kColShift + 1 + 8 * q) = ev;
+                    if (spill_r)
+                        *reinterpret_cast<uint4*>(srow + jb + kColShift + 1 + 8 * q) = ev;
+                    const uint32_t w0 = __builtin_amdgcn_perm(code[4 * q + 1], code[4 * q], 0x06040200u);
+                    const uint32_t w1 = __builtin_amdgcn_perm(code[4 * q + 3], code[4 * q + 2], 0x06040200u);
+                    __builtin_nontemporal_store(uint64_t(w0) | (uint64_t(w1) << 32),
+                                                reinterpret_cast<uint64_t*>(crow + jb + kColShift + 1 + 8 * q));
+                }
+                if (lane == last_lane && pass == npass - 1)
+                {
+#pragma unroll
+                    for (int i = 0; i < NR; i++)
+                    {
+                        if (2 * i == last_c)
+                            endv = int(int16_t(E[i] & 0xffff));
+                        if (2 * i + 1 == last_c)
+                            endv = int(int16_t(E[i] >> 16));
+                    }
+                }
+            }
+        }
+        if (rec & (1u << 14))
+        {
+            const int v = __builtin_amdgcn_readlane(endv, last_lane);
+            if (best_val < v)
+                best_val = v, best_row = r;
+        }
+    }
+    return best_row;
+}
+
 // Traceback over the code matrix (lane-uniform walk, tiles staged in LDS by
 // the whole wave).  Emits reversed (row or -1, read position or -1) pairs;
 // rows are converted to node ids afterwards.
@@ -1185,7 +1479,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
             const int V = node_count;
             build_row_program<SizeT>(g, V, rec, xl, d.lds_xl_cap, d.lds_ring_rows, lane);
             cells += int64_t(V + 1) * (L + 1);
-            const int end_row = nw_forward_lds<CPL, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride, codes,
+            const int end_row = nw_forward_lds_pk<CPL, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride, codes,
                                                       d.code_stride, sc, lane);
             __syncthreads();
             ph.lap<kPhForward>();
