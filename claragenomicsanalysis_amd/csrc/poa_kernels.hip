@@ -719,6 +719,9 @@ __device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b)
 {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(pk_u16x2, a) + __builtin_bit_cast(pk_u16x2, b));
 }
+// min/mad against 0/1 constants are rewritten by the compiler into per-half
+// compare + select sequences; the callers pass the constants through
+// opaque_u32() so the packed forms survive.
 __device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b)
 {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(pk_u16x2, a) - __builtin_bit_cast(pk_u16x2, b));
@@ -732,6 +735,11 @@ __device__ __forceinline__ uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c)
 {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(pk_u16x2, a) * __builtin_bit_cast(pk_u16x2, b) +
                                             __builtin_bit_cast(pk_u16x2, c));
+}
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t v)
+{
+    asm volatile("" : "+v"(v));
+    return v;
 }
 __device__ __forceinline__ uint32_t pk_bcast(int v) { return (uint32_t(uint16_t(v)) * 0x10001u); }
 
@@ -789,6 +797,9 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
     const int s_eq      = sc.match - gap;
     const int s_ne      = sc.mismatch - gap;
     const uint32_t gap2 = pk_bcast(gap);
+    const uint32_t one2 = opaque_u32(0x00010001u);
+    const uint32_t two2 = opaque_u32(0x00020002u);
+    const uint32_t four2 = opaque_u32(0x00040004u);
     const int mask      = P.ring_mask;
     for (int j = lane; j < ring_stride; j += kWave)
         ring[j] = 0;
@@ -918,11 +929,11 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
                     // running maxima with the first maximising predecessor slot
                     const uint32_t d  = pk_add(dq[i], sig[i]);
                     const uint32_t nd = pk_max(dg[i], d);
-                    kd[i]             = pk_mad(pk_min_u(pk_sub(nd, dg[i]), 0x00010001u), pk_sub(kk, kd[i]), kd[i]);
+                    kd[i]             = pk_mad(pk_min_u(pk_sub(nd, dg[i]), one2), pk_sub(kk, kd[i]), kd[i]);
                     dg[i]             = nd;
                     const uint32_t v  = pk_add(Q[i], gap2);
                     const uint32_t nv = pk_max(vt[i], v);
-                    kv[i]             = pk_mad(pk_min_u(pk_sub(nv, vt[i]), 0x00010001u), pk_sub(kk, kv[i]), kv[i]);
+                    kv[i]             = pk_mad(pk_min_u(pk_sub(nv, vt[i]), one2), pk_sub(kk, kv[i]), kv[i]);
                     vt[i]             = nv;
                 }
             }
@@ -953,10 +964,10 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
 #pragma unroll
                 for (int i = 0; i < NR; i++)
                 {
-                    const uint32_t a  = pk_min_u(pk_sub(E[i], dg[i]), 0x00010001u); // 0: diagonal match
-                    const uint32_t bb = pk_min_u(pk_sub(E[i], vt[i]), 0x00010001u); // 0: vertical match
-                    const uint32_t cv = pk_mad(kv[i], 0x00040004u, 0x00010001u);     // 1 | kv << 2
-                    const uint32_t cvh = pk_mad(bb, pk_sub(0x00020002u, cv), cv);    // vertical or horizontal
+                    const uint32_t a   = pk_min_u(pk_sub(E[i], dg[i]), one2); // 0: diagonal match
+                    const uint32_t bb  = pk_min_u(pk_sub(E[i], vt[i]), one2); // 0: vertical match
+                    const uint32_t cv  = pk_mad(kv[i], four2, one2);          // 1 | kv << 2
+                    const uint32_t cvh = pk_mad(bb, pk_sub(two2, cv), cv);    // vertical or horizontal
                     const uint32_t cd = kd[i] << 2;                                  // kd < 64: no cross-half carry
                     code[i]           = pk_mad(a, pk_sub(cvh, cd), cd);
                 }
