@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <iomanip>
@@ -530,11 +531,35 @@ private:
                                                   int64_t(gwamd::poa::kTileRows) * gwamd::poa::kTileCols, add_b});
         const int64_t rec_b  = a16(int64_t(dims_.max_nodes + 1) * 4);
         const int64_t fixed  = read_b + ring_b + rec_b;
-        const int64_t target = 40960 - 256 - 16; // keep 4 workgroups per CU incl. static LDS
-        int64_t xl_cap       = std::max<int64_t>(1024, (target - fixed) / 2);
+        const int64_t sh_b   = gwamd::poa::kShBytes;
+        const int64_t target = 40960 - 16; // keep 4 workgroups per CU incl. static LDS
+        int64_t xl_cap       = std::max<int64_t>(1024, (target - fixed - sh_b) / 2);
         xl_cap               = std::min<int64_t>(xl_cap, 65535);
-        const int64_t total  = fixed + a16(xl_cap * 2) + 16;
+        const int64_t total  = fixed + a16(xl_cap * 2) + sh_b;
         if (total > 65536)
+            return;
+        // forward pass shape: CPL columns per lane on NW waves; one pass
+        // covers NW*64*CPL read columns (GWAMD_POA_LDS_SHAPE="cpl,waves")
+        int cpl = 8, nw = 1;
+        const int ms = dims_.max_seq_len;
+        if (ms <= 4 * 512)
+            nw = (ms + 511) / 512;
+        else
+            nw = 4, cpl = 16;
+        if (const char* sh = std::getenv("GWAMD_POA_LDS_SHAPE"))
+        {
+            int c = 0, n = 0;
+            if (std::sscanf(sh, "%d,%d", &c, &n) == 2)
+            {
+                const bool known = (n == 1 && (c == 8 || c == 16 || c == 24 || c == 32)) ||
+                                   (c == 8 && n >= 2 && n <= 4) || (c == 16 && n == 4);
+                if (!known)
+                    throw std::invalid_argument("GWAMD_POA_LDS_SHAPE: unsupported columns/waves pair");
+                cpl = c, nw = n;
+            }
+        }
+        const int spans = ((ms + 64 * cpl * nw - 1) / (64 * cpl * nw)) * nw;
+        if (spans > gwamd::poa::kMaxSpans)
             return;
         dims_.lds_kernel    = 1;
         dims_.lds_ring_off  = int32_t(read_b);
@@ -543,7 +568,9 @@ private:
         dims_.lds_xl_off    = int32_t(read_b + ring_b + rec_b);
         dims_.lds_xl_cap    = int32_t(xl_cap);
         dims_.lds_bytes     = int32_t(total);
-        dims_.lds_sh_off    = int32_t(total - 16);
+        dims_.lds_sh_off    = int32_t(total - sh_b);
+        dims_.lds_cpl       = cpl;
+        dims_.lds_waves     = nw;
         dims_.code_stride   = int32_t(a16(int64_t(dims_.max_seq_len) + 48));
     }
 

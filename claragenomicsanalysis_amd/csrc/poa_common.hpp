@@ -67,8 +67,18 @@ struct Dims
     int32_t lds_xl_off;     // extra predecessor rows (u16)
     int32_t lds_xl_cap;
     int32_t code_stride;    // bytes per traceback-code row
-    int32_t lds_sh_off;     // small shared ints (add/topsort control)
+    int32_t lds_sh_off;     // small shared region (layout: kSh* below)
+    int32_t lds_cpl;        // forward pass: columns per lane
+    int32_t lds_waves;      // forward pass: waves per window
 };
+
+// Small shared region of the LDS kernel (kShBytes at Dims::lds_sh_off):
+// control ints, the forward pass span-total exchange ([2][waves] + end row)
+// and the per-span boundary column ([spans][ring rows] int16).
+constexpr int kShXchg    = 16;
+constexpr int kShBnd     = 64;
+constexpr int kShBytes   = 256;
+constexpr int kMaxSpans  = (kShBytes - kShBnd) / (2 * 8);
 
 constexpr int kTileRows = 128; // traceback tile (codes) rows
 constexpr int kTileCols = 128; // traceback tile columns (bytes)

@@ -38,6 +38,16 @@ __device__ __forceinline__ uint64_t now_ticks()
     return __builtin_amdgcn_s_memrealtime();
 }
 
+// Ordering point for code run by a single wave (LDS and global accesses of one
+// wave complete in issue order; this only stops the compiler from moving
+// memory operations across it).
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ int uniform(int x)
 {
     return __builtin_amdgcn_readfirstlane(x);
@@ -108,10 +118,10 @@ __device__ void build_backbone(WinGraph<SizeT>& g, const uint8_t* seq, const int
             ecov_cnt[(n - 1) * kMaxEdges]              = 1;
         }
     }
-    __syncthreads();
+    wave_sync();
     if (lane == 0 && len >= 1)
         g.out_cnt[len - 1] = 0; // written last, as in the reference (:179 then loop)
-    __syncthreads();
+    wave_sync();
 }
 
 // ---------------------------------------------------------------------------

@@ -79,7 +79,7 @@ __device__ void finish_window(const Buffers& b, const Dims& d, int w, int lane, 
             sh_len    = len;
             sh_status = cst;
         }
-        __syncthreads();
+        wave_sync();
         const int len = sh_len;
         // reverse in place to host order (cudapoa_batch.cuh:241-246 does this on the host)
         for (int k = lane; k < len / 2; k += kWave)
@@ -98,7 +98,7 @@ __device__ void finish_window(const Buffers& b, const Dims& d, int w, int lane, 
             if (len < d.max_consensus)
                 cons_out[len] = 0;
         }
-        __syncthreads();
+        wave_sync();
     }
     if (MSA)
     {
@@ -132,7 +132,7 @@ __device__ void finish_window(const Buffers& b, const Dims& d, int w, int lane, 
             sh_len    = msa_len;
             sh_status = mst;
         }
-        __syncthreads();
+        wave_sync();
         const int msa_len = sh_len;
         const int mst     = sh_status;
         if (mst == kSuccess && nseq > 0)
@@ -456,249 +456,7 @@ __device__ void build_row_program(const WinGraph<SizeT>& g, int V, uint32_t* rec
         }
         xbase += total;
     }
-    __syncthreads();
-}
-
-__device__ __forceinline__ void unpack8(uint4 q, int* v)
-{
-    v[0] = int(int16_t(q.x & 0xffff));
-    v[1] = int(int16_t(q.x >> 16));
-    v[2] = int(int16_t(q.y & 0xffff));
-    v[3] = int(int16_t(q.y >> 16));
-    v[4] = int(int16_t(q.z & 0xffff));
-    v[5] = int(int16_t(q.z >> 16));
-    v[6] = int(int16_t(q.w & 0xffff));
-    v[7] = int(int16_t(q.w >> 16));
-}
-
-__device__ __forceinline__ uint4 pack8(const int* v)
-{
-    uint4 q;
-    q.x = (uint32_t(uint16_t(v[0]))) | (uint32_t(uint16_t(v[1])) << 16);
-    q.y = (uint32_t(uint16_t(v[2]))) | (uint32_t(uint16_t(v[3])) << 16);
-    q.z = (uint32_t(uint16_t(v[4]))) | (uint32_t(uint16_t(v[5])) << 16);
-    q.w = (uint32_t(uint16_t(v[6]))) | (uint32_t(uint16_t(v[7])) << 16);
-    return q;
-}
-
-// Loads CPL E values (columns jb+1..jb+CPL) and E[jb] of predecessor row p:
-// from the LDS ring when p is among the last ring rows, from the HBM spill
-// copy otherwise, or zeros for the virtual row 0.  The two memory paths are
-// kept apart so the ring path compiles to ds_read_b128.
-template <int CPL>
-__device__ __forceinline__ void load_pred(const int16_t* ring, int ring_stride, int ring_mask, const int16_t* spill,
-                                          int stride, int r, int p, int jb, int (&cur)[CPL], int& prev)
-{
-    // The ring slot is always read (a valid LDS address even when the row is
-    // not there) so the compiler never merges the LDS and HBM paths into one
-    // flat pointer; the rare far predecessor then overrides from HBM.
-    const int16_t* lrow = ring + (p & ring_mask) * ring_stride + jb + kColShift;
-#pragma unroll
-    for (int q = 0; q < CPL / 8; q++)
-        unpack8(*reinterpret_cast<const uint4*>(lrow + 1 + 8 * q), cur + 8 * q);
-    prev = int(lrow[0]);
-    if (p == 0)
-    {
-#pragma unroll
-        for (int c = 0; c < CPL; c++)
-            cur[c] = 0;
-        prev = 0;
-    }
-    else if (r - p > ring_mask)
-    {
-        const int16_t* grow = spill + size_t(p) * stride + jb + kColShift;
-#pragma unroll
-        for (int q = 0; q < CPL / 8; q++)
-            unpack8(*reinterpret_cast<const uint4*>(grow + 1 + 8 * q), cur + 8 * q);
-        prev = int(grow[0]);
-    }
-}
-
-// Forward pass; returns the end row (first sink with the strictly greatest
-// last-column score, cudapoa_nw.cuh:332-349 with rows in the current
-// topological order).  Each lane owns CPL consecutive columns; one pass of
-// the wave covers 64*CPL columns (a whole 1-kb read in one pass at CPL=24).
-template <int CPL, typename SizeT>
-__device__ int nw_forward_lds(const WinGraph<SizeT>& g, const RowProg& P, int V, const uint8_t* read, int L,
-                              int16_t* ring, int ring_stride, int16_t* spill, int stride, uint8_t* codes,
-                              int code_stride, const Scores sc, int lane)
-{
-    constexpr int kPass = kWave * CPL;
-    const int gap       = sc.gap;
-    const int s_eq      = sc.match - gap; // diagonal step in the E domain
-    const int s_ne      = sc.mismatch - gap;
-    const int mask      = P.ring_mask;
-    // row 0 (E == 0 everywhere) in ring slot 0
-    for (int j = lane; j < ring_stride; j += kWave)
-        ring[j] = 0;
-    int best_row        = 0;
-    int best_val        = INT_MIN;
-    const int last_lane = ((L - 1) / CPL) % kWave; // lane owning column L in the last pass
-    const int last_c    = (L - 1) % CPL;
-    for (int r = 1; r <= V; r++)
-    {
-        const uint32_t rec = P.rec[r];
-        const int base     = int(rec & 0xff);
-        const int np       = uniform(prog_np(g, r, rec));
-        const bool spill_r = (rec >> 15) & 1;
-        int16_t* row       = ring + (r & mask) * ring_stride;
-        int16_t* srow      = spill + size_t(r) * stride;
-        uint8_t* crow      = codes + size_t(r) * code_stride;
-        // column 0: vertical from the first predecessor with the largest E[.][0]
-        int c0, c0k = 0;
-        if (np == 0)
-            c0 = gap;
-        else
-        {
-            c0 = kNeg;
-            for (int k = 0; k < np; k++)
-            {
-                const int p = uniform(prog_pred(P, g, r, rec, k));
-                int v = int(ring[(p & mask) * ring_stride + kColShift]);
-                if (p == 0)
-                    v = 0;
-                else if (r - p > mask)
-                    v = int(spill[size_t(p) * stride + kColShift]);
-                if (v > c0)
-                    c0 = v, c0k = k;
-            }
-            c0 += gap;
-        }
-        if (lane == 0)
-        {
-            row[kColShift]  = int16_t(c0);
-            crow[kColShift] = uint8_t(1 | (c0k << 2));
-            if (spill_r)
-                srow[kColShift] = int16_t(c0);
-        }
-        const int p0 = np == 0 ? 0 : uniform(prog_pred(P, g, r, rec, 0));
-        int carry    = c0;
-        int endv     = (L == 0) ? c0 : kNeg;
-        for (int cb = 0; cb < L; cb += kPass)
-        {
-            const int jb      = cb + lane * CPL;
-            const bool active = jb < L;
-            int sig[CPL], dg0[CPL], vt0[CPL], E[CPL];
-            if (active)
-            {
-#pragma unroll
-                for (int q = 0; q < CPL / 8; q++)
-                {
-                    const uint2 rc = *reinterpret_cast<const uint2*>(read + jb + 8 * q);
-#pragma unroll
-                    for (int c = 0; c < 8; c++)
-                    {
-                        const int ch    = int(((c < 4 ? rc.x : rc.y) >> (8 * (c & 3))) & 0xff);
-                        sig[8 * q + c] = (ch == base) ? s_eq : s_ne;
-                    }
-                }
-                int cur[CPL], prev;
-                load_pred<CPL>(ring, ring_stride, mask, spill, stride, r, p0, jb, cur, prev);
-#pragma unroll
-                for (int c = 0; c < CPL; c++)
-                {
-                    dg0[c] = prev + sig[c];
-                    vt0[c] = cur[c] + gap;
-                    E[c]   = max(dg0[c], vt0[c]);
-                    prev   = cur[c];
-                }
-                for (int k = 1; k < np; k++)
-                {
-                    const int p = uniform(prog_pred(P, g, r, rec, k));
-                    load_pred<CPL>(ring, ring_stride, mask, spill, stride, r, p, jb, cur, prev);
-#pragma unroll
-                    for (int c = 0; c < CPL; c++)
-                    {
-                        E[c] = max(E[c], max(prev + sig[c], cur[c] + gap));
-                        prev = cur[c];
-                    }
-                }
-            }
-            else
-            {
-#pragma unroll
-                for (int c = 0; c < CPL; c++)
-                    E[c] = dg0[c] = vt0[c] = sig[c] = kNeg;
-            }
-            // prefix maximum across the row (the horizontal gap closure)
-            int m = kNeg;
-#pragma unroll
-            for (int c = 0; c < CPL; c++)
-            {
-                m    = max(m, E[c]);
-                E[c] = m;
-            }
-            const int incl  = wave_incl_max_dpp(m);
-            const int excl  = __builtin_amdgcn_update_dpp(kNeg, incl, 0x138, 0xf, 0xf, false); // wave_shr:1
-            const int below = max(excl, carry);
-#pragma unroll
-            for (int c = 0; c < CPL; c++)
-                E[c] = max(E[c], below);
-            carry = max(carry, __builtin_amdgcn_readlane(incl, kWave - 1));
-            if (active)
-            {
-                // traceback codes: diagonal over predecessors in slot order, then
-                // vertical, then horizontal (cudapoa_nw.cuh:361-443)
-                int code[CPL];
-                if (np <= 1)
-                {
-#pragma unroll
-                    for (int c = 0; c < CPL; c++)
-                        code[c] = dg0[c] == E[c] ? 0 : (vt0[c] == E[c] ? 1 : 2);
-                }
-                else
-                {
-                    int cd[CPL], cv[CPL];
-#pragma unroll
-                    for (int c = 0; c < CPL; c++)
-                        cd[c] = cv[c] = 255;
-                    for (int k = np - 1; k >= 0; k--)
-                    {
-                        const int p = uniform(prog_pred(P, g, r, rec, k));
-                        int cur[CPL], prev;
-                        load_pred<CPL>(ring, ring_stride, mask, spill, stride, r, p, jb, cur, prev);
-#pragma unroll
-                        for (int c = 0; c < CPL; c++)
-                        {
-                            cd[c] = (prev + sig[c] == E[c]) ? (k << 2) : cd[c];
-                            cv[c] = (cur[c] + gap == E[c]) ? (1 | (k << 2)) : cv[c];
-                            prev  = cur[c];
-                        }
-                    }
-#pragma unroll
-                    for (int c = 0; c < CPL; c++)
-                        code[c] = cd[c] != 255 ? cd[c] : (cv[c] != 255 ? cv[c] : 2);
-                }
-#pragma unroll
-                for (int q = 0; q < CPL / 8; q++)
-                {
-                    const uint4 ev = pack8(E + 8 * q);
-                    *reinterpret_cast<uint4*>(row + jb + kColShift + 1 + 8 * q) = ev;
-                    if (spill_r)
-                        *reinterpret_cast<uint4*>(srow + jb + kColShift + 1 + 8 * q) = ev;
-                    uint64_t cw = 0;
-#pragma unroll
-                    for (int c = 0; c < 8; c++)
-                        cw |= uint64_t(code[8 * q + c]) << (8 * c);
-                    __builtin_nontemporal_store(cw, reinterpret_cast<uint64_t*>(crow + jb + kColShift + 1 + 8 * q));
-                }
-                if (lane == last_lane && cb + kPass >= L)
-                {
-#pragma unroll
-                    for (int c = 0; c < CPL; c++)
-                        if (c == last_c)
-                            endv = E[c];
-                }
-            }
-        }
-        if (rec & (1u << 14))
-        {
-            const int v = __builtin_amdgcn_readlane(endv, last_lane);
-            if (best_val < v)
-                best_val = v, best_row = r;
-        }
-    }
-    return best_row;
+    wave_sync();
 }
 
 // ---------------------------------------------------------------------------
@@ -707,6 +465,8 @@ __device__ int nw_forward_lds(const WinGraph<SizeT>& g, const RowProg& P, int V,
 // per 32-bit register, so the diagonal/vertical/max work runs on v_pk_*
 // instructions.  Cells beyond the read may wrap; they only feed cells further
 // right, never a cell <= L.
+#define GWAMD_LDS __attribute__((address_space(3)))
+
 typedef short pk_s16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short pk_u16x2 __attribute__((ext_vector_type(2)));
 
@@ -786,13 +546,25 @@ __device__ __forceinline__ void diag_src(const uint32_t (&P)[NR], uint32_t prev,
         Dg[i] = __builtin_amdgcn_alignbyte(P[i], P[i - 1], 2);
 }
 
-template <int CPL, typename SizeT>
+// Forward pass of one read, split over NW waves of the workgroup.  Each pass
+// covers NW * 64 * CPL columns; wave q owns the q-th 64*CPL span (CPL cells
+// per lane).  Per row every wave computes the column-0 value itself, then its
+// cells with the carry of its own span; the span totals are exchanged through
+// LDS at one barrier per pass.  The only value a wave needs from another wave's
+// span is E_p[cb] (the column left of its span) for predecessor rows p, which
+// equals the carry the wave itself computed for row p: it is kept per span
+// in `bnd` (ring rows) so no second barrier is needed per row.
+template <int CPL, int NW, typename SizeT>
 __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int V, const uint8_t* read, int L,
                                  int16_t* ring, int ring_stride, int16_t* spill, int stride, uint8_t* codes,
-                                 int code_stride, const Scores sc, int lane)
+                                 int code_stride, const Scores sc, GWAMD_LDS int* xchg, GWAMD_LDS int16_t* bnd,
+                                 int tid)
 {
     constexpr int NR    = CPL / 2;
-    constexpr int kPass = kWave * CPL;
+    constexpr int kSpan = kWave * CPL;
+    constexpr int kPass = kSpan * NW;
+    const int lane      = tid & (kWave - 1);
+    const int wave      = uniform(tid / kWave);
     const int gap       = sc.gap;
     const int s_eq      = sc.match - gap;
     const int s_ne      = sc.mismatch - gap;
@@ -801,17 +573,23 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
     const uint32_t two2 = opaque_u32(0x00020002u);
     const uint32_t four2 = opaque_u32(0x00040004u);
     const int mask      = P.ring_mask;
-    for (int j = lane; j < ring_stride; j += kWave)
-        ring[j] = 0;
+    const int rows      = mask + 1;
     int best_row        = 0;
     int best_val        = INT_MIN;
-    const int last_lane = ((L - 1) / CPL) % kWave;
-    const int last_c    = (L - 1) % CPL;
+    // owner of the last column (L-1): pass, wave, lane, cell
+    const int jl        = L > 0 ? L - 1 : 0;
+    const int own_pass  = L > 0 ? jl / kPass : -1;
+    const int own_wave  = (jl % kPass) / kSpan;
+    const int own_lane  = (jl % kSpan) / CPL;
+    const int own_c     = jl % CPL;
+    const bool owner    = wave == own_wave;
     const int npass     = (L + kPass - 1) / kPass;
+    int xt              = 0; // exchange counter (double-buffered slots)
     // per-read substitution profiles for A, C, G, T (single-pass reads)
     uint32_t sig_acgt[4][NR];
     {
-        const int jb = (lane * CPL < L) ? lane * CPL : 0; // inactive lanes read a valid address
+        const int jb0 = wave * kSpan + lane * CPL;
+        const int jb  = jb0 < L ? jb0 : 0; // inactive lanes read a valid address
 #pragma unroll
         for (int i = 0; i < NR; i++)
         {
@@ -851,7 +629,9 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
             }
             c0 += gap;
         }
-        if (lane == 0)
+        // column 0 is written before the row's exchange barrier: every wave
+        // reads it for row r+1 only after that barrier
+        if (wave == 0 && lane == 0)
         {
             row[kColShift]  = int16_t(c0);
             crow[kColShift] = uint8_t(1 | (c0k << 2));
@@ -863,145 +643,198 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
         int endv     = (L == 0) ? c0 : kNeg;
         for (int pass = 0; pass < npass; pass++)
         {
-            const int cb      = pass * kPass;
+            const int cb      = pass * kPass + wave * kSpan;
+            const int chunk   = pass * NW + wave;
+            const bool wact   = cb < L; // wave-uniform: span holds read columns
             const int jb      = cb + lane * CPL;
             const bool active = jb < L;
             const int ja      = active ? jb : 0; // address used by inactive lanes
-            uint32_t sig[NR];
-            if (npass == 1 && (base == 'A' || base == 'C' || base == 'G' || base == 'T'))
+            uint32_t dg[NR], vt[NR], kd[NR], kv[NR], E[NR];
+            int m = kNeg;
+            if (wact)
             {
-                const int bi = base == 'A' ? 0 : base == 'C' ? 1 : base == 'G' ? 2 : 3;
-                if (bi == 0)
+                uint32_t sig[NR];
+                if (npass == 1 && (base == 'A' || base == 'C' || base == 'G' || base == 'T'))
                 {
+                    const int bi = base == 'A' ? 0 : base == 'C' ? 1 : base == 'G' ? 2 : 3;
+                    if (bi == 0)
+                    {
 #pragma unroll
-                    for (int i = 0; i < NR; i++)
-                        sig[i] = sig_acgt[0][i];
-                }
-                else if (bi == 1)
-                {
+                        for (int i = 0; i < NR; i++)
+                            sig[i] = sig_acgt[0][i];
+                    }
+                    else if (bi == 1)
+                    {
 #pragma unroll
-                    for (int i = 0; i < NR; i++)
-                        sig[i] = sig_acgt[1][i];
-                }
-                else if (bi == 2)
-                {
+                        for (int i = 0; i < NR; i++)
+                            sig[i] = sig_acgt[1][i];
+                    }
+                    else if (bi == 2)
+                    {
 #pragma unroll
-                    for (int i = 0; i < NR; i++)
-                        sig[i] = sig_acgt[2][i];
+                        for (int i = 0; i < NR; i++)
+                            sig[i] = sig_acgt[2][i];
+                    }
+                    else
+                    {
+#pragma unroll
+                        for (int i = 0; i < NR; i++)
+                            sig[i] = sig_acgt[3][i];
+                    }
                 }
                 else
                 {
 #pragma unroll
                     for (int i = 0; i < NR; i++)
-                        sig[i] = sig_acgt[3][i];
+                    {
+                        const int ch0 = int(read[ja + 2 * i]), ch1 = int(read[ja + 2 * i + 1]);
+                        sig[i]        = uint32_t(uint16_t(ch0 == base ? s_eq : s_ne)) |
+                                 (uint32_t(uint16_t(ch1 == base ? s_eq : s_ne)) << 16);
+                    }
                 }
-            }
-            else
-            {
+                uint32_t Pv[NR], prev;
+                load_pred_pk<NR>(ring, ring_stride, mask, spill, stride, r, p0, ja, Pv, prev);
+                if constexpr (NW > 1)
+                {
+                    const uint32_t bv = uint32_t(uint16_t(bnd[chunk * rows + (p0 & mask)]));
+                    if (lane == 0 && cb > 0 && p0 != 0 && r - p0 <= mask)
+                        prev = bv;
+                }
+                diag_src<NR>(Pv, prev, dg);
 #pragma unroll
                 for (int i = 0; i < NR; i++)
                 {
-                    const int ch0 = int(read[ja + 2 * i]), ch1 = int(read[ja + 2 * i + 1]);
-                    sig[i]        = uint32_t(uint16_t(ch0 == base ? s_eq : s_ne)) |
-                             (uint32_t(uint16_t(ch1 == base ? s_eq : s_ne)) << 16);
+                    dg[i] = pk_add(dg[i], sig[i]);
+                    vt[i] = pk_add(Pv[i], gap2);
+                    kd[i] = kv[i] = 0;
                 }
-            }
-            uint32_t Pv[NR], prev, dg[NR], vt[NR], kd[NR], kv[NR], E[NR];
-            load_pred_pk<NR>(ring, ring_stride, mask, spill, stride, r, p0, ja, Pv, prev);
-            diag_src<NR>(Pv, prev, dg);
-#pragma unroll
-            for (int i = 0; i < NR; i++)
-            {
-                dg[i] = pk_add(dg[i], sig[i]);
-                vt[i] = pk_add(Pv[i], gap2);
-                kd[i] = kv[i] = 0;
-            }
-            for (int k = 1; k < np; k++)
-            {
-                const int p = uniform(prog_pred(P, g, r, rec, k));
-                uint32_t Q[NR], qprev, dq[NR];
-                load_pred_pk<NR>(ring, ring_stride, mask, spill, stride, r, p, ja, Q, qprev);
-                diag_src<NR>(Q, qprev, dq);
-                const uint32_t kk = pk_bcast(k);
-#pragma unroll
-                for (int i = 0; i < NR; i++)
+                for (int k = 1; k < np; k++)
                 {
-                    // running maxima with the first maximising predecessor slot
-                    const uint32_t d  = pk_add(dq[i], sig[i]);
-                    const uint32_t nd = pk_max(dg[i], d);
-                    kd[i]             = pk_mad(pk_min_u(pk_sub(nd, dg[i]), one2), pk_sub(kk, kd[i]), kd[i]);
-                    dg[i]             = nd;
-                    const uint32_t v  = pk_add(Q[i], gap2);
-                    const uint32_t nv = pk_max(vt[i], v);
-                    kv[i]             = pk_mad(pk_min_u(pk_sub(nv, vt[i]), one2), pk_sub(kk, kv[i]), kv[i]);
-                    vt[i]             = nv;
-                }
-            }
-            // in-lane prefix maximum
-            uint32_t c = 0x80008000u;
-#pragma unroll
-            for (int i = 0; i < NR; i++)
-            {
-                const uint32_t dmax = pk_max(dg[i], vt[i]);
-                uint32_t s          = pk_max(dmax, (dmax << 16) | 0x8000u);
-                s                   = pk_max(s, c);
-                E[i]                = s;
-                c                   = __builtin_amdgcn_perm(s, s, 0x07060706u);
-            }
-            const int m     = active ? int(int16_t(E[NR - 1] >> 16)) : kNeg;
-            const int incl  = wave_incl_max_dpp(m);
-            const int excl  = __builtin_amdgcn_update_dpp(kNeg, incl, 0x138, 0xf, 0xf, false);
-            const int below = max(excl, carry);
-            carry           = max(carry, __builtin_amdgcn_readlane(incl, kWave - 1));
-            const uint32_t b2 = pk_bcast(below);
-#pragma unroll
-            for (int i = 0; i < NR; i++)
-                E[i] = pk_max(E[i], b2);
-            if (active)
-            {
-                // codes: 0 diagonal, 1 vertical, 2 horizontal (+ slot << 2)
-                uint32_t code[NR];
-#pragma unroll
-                for (int i = 0; i < NR; i++)
-                {
-                    const uint32_t a   = pk_min_u(pk_sub(E[i], dg[i]), one2); // 0: diagonal match
-                    const uint32_t bb  = pk_min_u(pk_sub(E[i], vt[i]), one2); // 0: vertical match
-                    const uint32_t cv  = pk_mad(kv[i], four2, one2);          // 1 | kv << 2
-                    const uint32_t cvh = pk_mad(bb, pk_sub(two2, cv), cv);    // vertical or horizontal
-                    const uint32_t cd = kd[i] << 2;                                  // kd < 64: no cross-half carry
-                    code[i]           = pk_mad(a, pk_sub(cvh, cd), cd);
-                }
-#pragma unroll
-                for (int q = 0; q < NR / 4; q++)
-                {
-                    const uint4 ev = make_uint4(E[4 * q], E[4 * q + 1], E[4 * q + 2], E[4 * q + 3]);
-                    *reinterpret_cast<uint4*>(row + jb + kColShift + 1 + 8 * q) = ev;
-                    if (spill_r)
-                        *reinterpret_cast<uint4*>(srow + jb + kColShift + 1 + 8 * q) = ev;
-                    const uint32_t w0 = __builtin_amdgcn_perm(code[4 * q + 1], code[4 * q], 0x06040200u);
-                    const uint32_t w1 = __builtin_amdgcn_perm(code[4 * q + 3], code[4 * q + 2], 0x06040200u);
-                    __builtin_nontemporal_store(uint64_t(w0) | (uint64_t(w1) << 32),
-                                                reinterpret_cast<uint64_t*>(crow + jb + kColShift + 1 + 8 * q));
-                }
-                if (lane == last_lane && pass == npass - 1)
-                {
+                    const int p = uniform(prog_pred(P, g, r, rec, k));
+                    uint32_t Q[NR], qprev, dq[NR];
+                    load_pred_pk<NR>(ring, ring_stride, mask, spill, stride, r, p, ja, Q, qprev);
+                    if constexpr (NW > 1)
+                    {
+                        const uint32_t bv = uint32_t(uint16_t(bnd[chunk * rows + (p & mask)]));
+                        if (lane == 0 && cb > 0 && p != 0 && r - p <= mask)
+                            qprev = bv;
+                    }
+                    diag_src<NR>(Q, qprev, dq);
+                    const uint32_t kk = pk_bcast(k);
 #pragma unroll
                     for (int i = 0; i < NR; i++)
                     {
-                        if (2 * i == last_c)
-                            endv = int(int16_t(E[i] & 0xffff));
-                        if (2 * i + 1 == last_c)
-                            endv = int(int16_t(E[i] >> 16));
+                        // running maxima with the first maximising predecessor slot
+                        const uint32_t d  = pk_add(dq[i], sig[i]);
+                        const uint32_t nd = pk_max(dg[i], d);
+                        kd[i]             = pk_mad(pk_min_u(pk_sub(nd, dg[i]), one2), pk_sub(kk, kd[i]), kd[i]);
+                        dg[i]             = nd;
+                        const uint32_t v  = pk_add(Q[i], gap2);
+                        const uint32_t nv = pk_max(vt[i], v);
+                        kv[i]             = pk_mad(pk_min_u(pk_sub(nv, vt[i]), one2), pk_sub(kk, kv[i]), kv[i]);
+                        vt[i]             = nv;
+                    }
+                }
+                // in-lane prefix maximum
+                uint32_t c = 0x80008000u;
+#pragma unroll
+                for (int i = 0; i < NR; i++)
+                {
+                    const uint32_t dmax = pk_max(dg[i], vt[i]);
+                    uint32_t s          = pk_max(dmax, (dmax << 16) | 0x8000u);
+                    s                   = pk_max(s, c);
+                    E[i]                = s;
+                    c                   = __builtin_amdgcn_perm(s, s, 0x07060706u);
+                }
+                m = active ? int(int16_t(E[NR - 1] >> 16)) : kNeg;
+            }
+            const int incl = wave_incl_max_dpp(m);
+            const int excl = __builtin_amdgcn_update_dpp(kNeg, incl, 0x138, 0xf, 0xf, false);
+            const int wtot = __builtin_amdgcn_readlane(incl, kWave - 1);
+            int cin        = carry;
+            if constexpr (NW > 1)
+            {
+                GWAMD_LDS int* xs = xchg + (xt & 1) * NW;
+                xt++;
+                if (lane == 0)
+                    xs[wave] = wtot;
+                __syncthreads();
+                int all = carry;
+#pragma unroll
+                for (int q = 0; q < NW; q++)
+                {
+                    const int t = xs[q];
+                    if (q < wave)
+                        cin = max(cin, t);
+                    all = max(all, t);
+                }
+                carry = all;
+                if (lane == 0 && cb > 0)
+                    bnd[chunk * rows + (r & mask)] = int16_t(cin);
+            }
+            else
+                carry = max(carry, wtot);
+            if (wact)
+            {
+                const int below   = max(excl, cin);
+                const uint32_t b2 = pk_bcast(below);
+#pragma unroll
+                for (int i = 0; i < NR; i++)
+                    E[i] = pk_max(E[i], b2);
+                if (active)
+                {
+                    // codes: 0 diagonal, 1 vertical, 2 horizontal (+ slot << 2)
+                    uint32_t code[NR];
+#pragma unroll
+                    for (int i = 0; i < NR; i++)
+                    {
+                        const uint32_t a   = pk_min_u(pk_sub(E[i], dg[i]), one2); // 0: diagonal match
+                        const uint32_t bb  = pk_min_u(pk_sub(E[i], vt[i]), one2); // 0: vertical match
+                        const uint32_t cv  = pk_mad(kv[i], four2, one2);          // 1 | kv << 2
+                        const uint32_t cvh = pk_mad(bb, pk_sub(two2, cv), cv);    // vertical or horizontal
+                        const uint32_t cd  = kd[i] << 2; // kd < 64: no cross-half carry
+                        code[i]            = pk_mad(a, pk_sub(cvh, cd), cd);
+                    }
+#pragma unroll
+                    for (int q = 0; q < NR / 4; q++)
+                    {
+                        const uint4 ev = make_uint4(E[4 * q], E[4 * q + 1], E[4 * q + 2], E[4 * q + 3]);
+                        *reinterpret_cast<uint4*>(row + jb + kColShift + 1 + 8 * q) = ev;
+                        if (spill_r)
+                            *reinterpret_cast<uint4*>(srow + jb + kColShift + 1 + 8 * q) = ev;
+                        const uint32_t w0 = __builtin_amdgcn_perm(code[4 * q + 1], code[4 * q], 0x06040200u);
+                        const uint32_t w1 = __builtin_amdgcn_perm(code[4 * q + 3], code[4 * q + 2], 0x06040200u);
+                        __builtin_nontemporal_store(uint64_t(w0) | (uint64_t(w1) << 32),
+                                                    reinterpret_cast<uint64_t*>(crow + jb + kColShift + 1 + 8 * q));
+                    }
+                    if (lane == own_lane && pass == own_pass && owner)
+                    {
+#pragma unroll
+                        for (int i = 0; i < NR; i++)
+                        {
+                            if (2 * i == own_c)
+                                endv = int(int16_t(E[i] & 0xffff));
+                            if (2 * i + 1 == own_c)
+                                endv = int(int16_t(E[i] >> 16));
+                        }
                     }
                 }
             }
         }
-        if (rec & (1u << 14))
+        if ((rec & (1u << 14)) && owner)
         {
-            const int v = __builtin_amdgcn_readlane(endv, last_lane);
+            const int v = __builtin_amdgcn_readlane(endv, own_lane);
             if (best_val < v)
                 best_val = v, best_row = r;
         }
+    }
+    if constexpr (NW > 1)
+    {
+        // publish the end row from the wave that owns the last column
+        if (owner && lane == 0)
+            xchg[2 * NW] = best_row;
+        __syncthreads();
+        best_row = xchg[2 * NW];
     }
     return best_row;
 }
@@ -1012,7 +845,7 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
 template <typename SizeT>
 __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V, int L, int end_row,
                                const uint8_t* codes, int code_stride, uint8_t* tile, SizeT* ag, SizeT* ar,
-                               int aln_cap, int lane)
+                               int aln_cap, int tid, int nthreads)
 {
     int i = end_row, j = L;
     int ti0 = INT_MIN / 2, tj0 = INT_MIN / 2;
@@ -1035,7 +868,7 @@ __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V
                 ti0 = max(0, i - (kTileRows - 1));
                 tj0 = max(0, cj - (kTileCols - 16)) & ~15;
                 __syncthreads();
-                for (int t = lane; t < kTileRows * (kTileCols / 16); t += kWave)
+                for (int t = tid; t < kTileRows * (kTileCols / 16); t += nthreads)
                 {
                     const int tr = t / (kTileCols / 16);
                     const int tc = (t % (kTileCols / 16)) * 16;
@@ -1061,7 +894,7 @@ __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V
                 pj                 = dir == 0 ? j - 1 : j;
             }
         }
-        if (lane == 0 && n < aln_cap)
+        if (tid == 0 && n < aln_cap)
         {
             ag[n] = SizeT(i == pi ? -1 : i);
             ar[n] = SizeT(j == pj ? -1 : j - 1);
@@ -1086,7 +919,6 @@ __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V
 // prefix sum, and the first error (node or edge limit) is found by a min
 // over positions.  Otherwise nothing is written and -1 is returned so the
 // caller runs the sequential restatement.
-#define GWAMD_LDS __attribute__((address_space(3)))
 struct AddScratch
 {
     GWAMD_LDS uint16_t* gid;   // [max_seq] aligned graph node per read position (0xffff = none)
@@ -1112,7 +944,7 @@ __device__ int add_alignment_parallel(WinGraph<SizeT>& g, int& node_count, const
         if (rp >= 0 && rp < L)
             X.gid[rp] = uint16_t(int(ag[k]) < 0 ? 0xffff : int(ag[k]));
     }
-    __syncthreads();
+    wave_sync();
     // kinds and existing targets
     for (int rp = lane; rp < L; rp += kWave)
     {
@@ -1141,7 +973,7 @@ __device__ int add_alignment_parallel(WinGraph<SizeT>& g, int& node_count, const
         X.kind[rp] = uint8_t(kind);
         X.curr[rp] = uint16_t(curr);
     }
-    __syncthreads();
+    wave_sync();
     // new node ids: prefix sum over new-node elements in read order
     int nnew = 0;
     for (int r0 = 0; r0 < L; r0 += kWave)
@@ -1159,17 +991,17 @@ __device__ int add_alignment_parallel(WinGraph<SizeT>& g, int& node_count, const
         }
         nnew += total;
     }
-    __syncthreads();
+    wave_sync();
     // independence checks without atomics: every element claims its node (and,
     // for aligned hits / ring updates, its aligned group); after a barrier an
     // element that no longer owns a claimed node has a conflicting partner.
     for (int rp = lane; rp < L; rp += kWave)
         X.owner[int(X.curr[rp])] = uint16_t(rp);
-    __syncthreads();
+    wave_sync();
     bool conflict = false;
     for (int rp = lane; rp < L; rp += kWave)
         conflict |= int(X.owner[int(X.curr[rp])]) != rp;
-    __syncthreads();
+    wave_sync();
     for (int rp = lane; rp < L; rp += kWave)
     {
         const int kind = X.kind[rp];
@@ -1182,7 +1014,7 @@ __device__ int add_alignment_parallel(WinGraph<SizeT>& g, int& node_count, const
                 X.owner[int(g.aln[gid * kMaxAlignments + n])] = uint16_t(rp);
         }
     }
-    __syncthreads();
+    wave_sync();
     for (int rp = lane; rp < L; rp += kWave)
     {
         const int kind = X.kind[rp];
@@ -1197,7 +1029,7 @@ __device__ int add_alignment_parallel(WinGraph<SizeT>& g, int& node_count, const
     }
     if (conflict)
         X.sh[0] = 1;
-    __syncthreads();
+    wave_sync();
     if (X.sh[0])
         return -1;
     // edge existence and edge-limit errors
@@ -1226,7 +1058,7 @@ __device__ int add_alignment_parallel(WinGraph<SizeT>& g, int& node_count, const
     err = -wave_max(-err); // wave-wide minimum
     if (err != INT_MAX)
         return err & 0xff;
-    __syncthreads();
+    wave_sync();
     // writes 1: new nodes and aligned rings (one lane per element)
     for (int rp = lane; rp < L; rp += kWave)
     {
@@ -1259,7 +1091,7 @@ __device__ int add_alignment_parallel(WinGraph<SizeT>& g, int& node_count, const
             g.aln_cnt[curr]                    = uint16_t(cnt + 1);
         }
     }
-    __syncthreads();
+    wave_sync();
     // writes 2: the edge head -> curr and the coverage of curr
     for (int rp = lane; rp < L; rp += kWave)
     {
@@ -1310,7 +1142,7 @@ __device__ int add_alignment_parallel(WinGraph<SizeT>& g, int& node_count, const
         g.cov[curr]++;
     }
     node_count = nc0 + nnew;
-    __syncthreads();
+    wave_sync();
     return kSuccess;
 }
 
@@ -1349,7 +1181,7 @@ __device__ bool topsort_lds(WinGraph<SizeT>& g, int n, GWAMD_LDS uint8_t* scratc
         return false;
     if (lane == 0)
         off[n] = uint32_t(ebase);
-    __syncthreads();
+    wave_sync();
     for (int v = lane; v < n; v += kWave)
     {
         const int o  = int(off[v]);
@@ -1369,7 +1201,7 @@ __device__ bool topsort_lds(WinGraph<SizeT>& g, int n, GWAMD_LDS uint8_t* scratc
             queue[k + ex] = uint16_t(v);
         k += total;
     }
-    __syncthreads();
+    wave_sync();
     if (lane == 0)
     {
         int tail = k;
@@ -1388,7 +1220,7 @@ __device__ bool topsort_lds(WinGraph<SizeT>& g, int n, GWAMD_LDS uint8_t* scratc
         }
         sh[0] = tail;
     }
-    __syncthreads();
+    wave_sync();
     const int m = sh[0];
     for (int q = lane; q < m; q += kWave)
     {
@@ -1396,23 +1228,29 @@ __device__ bool topsort_lds(WinGraph<SizeT>& g, int n, GWAMD_LDS uint8_t* scratc
         g.sorted[q] = SizeT(v);
         g.pos[v]    = SizeT(q);
     }
-    __syncthreads();
+    wave_sync();
     return true;
 }
 
-template <bool MSA, int CPL>
-__global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d, Scores sc)
+// LDS-resident POA kernel: one workgroup of NW waves per window.  The forward
+// pass and the traceback tile loads use every wave; the serial phases (graph
+// update, topological sort, consensus, MSA) run on wave 0 while the other
+// waves wait at the next barrier.
+template <bool MSA, int CPL, int NW>
+__global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, Dims d, Scores sc)
 {
     using SizeT  = int16_t;
     extern __shared__ __align__(16) uint8_t lds[];
-    __shared__ int sh_alen;
     __shared__ int sh_status;
     __shared__ int sh_len;
 
     const int w = blockIdx.x;
     if (w >= b.num_windows)
         return;
-    const int lane = threadIdx.x;
+    const int tid      = threadIdx.x;
+    const int lane     = tid & (kWave - 1);
+    const int wave     = uniform(tid / kWave);
+    constexpr int kThr = kWave * NW;
 
     uint8_t* lread   = lds;
     int16_t* ring    = reinterpret_cast<int16_t*>(lds + d.lds_ring_off);
@@ -1421,6 +1259,9 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
     uint8_t* tile    = lds + d.lds_ring_off; // traceback tiles reuse the ring
     const int rstride = d.score_stride;      // ring / spill row stride (elements)
     RowProg P{rec, xl, d.lds_ring_rows - 1};
+    GWAMD_LDS uint8_t* shb = (GWAMD_LDS uint8_t*)(lds) + d.lds_sh_off;
+    GWAMD_LDS int* xchg    = (GWAMD_LDS int*)(shb + kShXchg);
+    GWAMD_LDS int16_t* bnd = (GWAMD_LDS int16_t*)(shb + kShBnd);
     AddScratch AX;
     {
         // add-alignment scratch lives in the ring region (free between reads)
@@ -1430,7 +1271,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
         AX.curr              = (GWAMD_LDS uint16_t*)(a + 2 * ms);
         AX.kind              = a + 4 * ms;
         AX.owner             = (GWAMD_LDS uint16_t*)(a + 5 * ms);
-        AX.sh                = (GWAMD_LDS int*)((GWAMD_LDS uint8_t*)(lds) + d.lds_sh_off);
+        AX.sh                = (GWAMD_LDS int*)(shb);
     }
 
     const size_t mn = size_t(d.max_nodes);
@@ -1470,7 +1311,8 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
         const int len0      = b.seq_len[wd.first_seq];
         const uint8_t* seq0 = b.seqs + b.seq_off[wd.first_seq];
         const int8_t* w0    = b.wts + b.seq_off[wd.first_seq];
-        build_backbone<SizeT, MSA>(g, seq0, w0, len0, lane, ecov, ecovc, seq_begin, d.max_seqs);
+        if (wave == 0)
+            build_backbone<SizeT, MSA>(g, seq0, w0, len0, lane, ecov, ecovc, seq_begin, d.max_seqs);
         node_count = len0;
         ph.lap<kPhBackbone>();
         for (int s = 1; s < nseq; s++)
@@ -1485,20 +1327,22 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
             const uint8_t* read_g = b.seqs + off;
             const int8_t* wts_g   = b.wts + off;
             const int padded      = (L + 32 + 15) & ~15;
-            for (int j = lane; j < padded; j += kWave)
+            for (int j = tid; j < padded; j += kThr)
                 lread[j] = j < L ? read_g[j] : 0;
             const int V = node_count;
-            build_row_program<SizeT>(g, V, rec, xl, d.lds_xl_cap, d.lds_ring_rows, lane);
+            if (wave == 0)
+                build_row_program<SizeT>(g, V, rec, xl, d.lds_xl_cap, d.lds_ring_rows, lane);
+            __syncthreads();
             cells += int64_t(V + 1) * (L + 1);
-            const int end_row = nw_forward_lds_pk<CPL, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride, codes,
-                                                      d.code_stride, sc, lane);
+            const int end_row = nw_forward_lds_pk<CPL, NW, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride,
+                                                                  codes, d.code_stride, sc, xchg, bnd, tid);
             __syncthreads();
             ph.lap<kPhForward>();
             const int alen = traceback_codes<SizeT>(g, P, V, L, end_row, codes, d.code_stride, tile, ag, ar,
-                                                    d.aln_cap, lane);
+                                                    d.aln_cap, tid, kThr);
             __syncthreads();
             // rows -> node ids
-            for (int k = lane; k < alen; k += kWave)
+            for (int k = tid; k < alen; k += kThr)
             {
                 const int rr = int(ag[k]);
                 if (rr > 0)
@@ -1511,6 +1355,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
                 status = kLoopCountExceeded;
                 break;
             }
+            if (wave == 0)
             {
                 int nc = node_count;
                 int rc = add_alignment_parallel<SizeT, MSA>(g, nc, ag, ar, alen, L, lread, wts_g, s, ecov, ecovc,
@@ -1523,35 +1368,49 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_lds(Buffers b, Dims d
                                                               seq_begin, d.max_seqs);
                         sh_len    = nc;
                     }
-                    __syncthreads();
+                    wave_sync();
                     rc = sh_status;
                     nc = sh_len;
                 }
                 ph.lap<kPhAdd>();
-                status     = rc;
-                node_count = nc;
-                if (status != kSuccess)
-                    break;
-                if (!topsort_lds<SizeT>(g, node_count, (GWAMD_LDS uint8_t*)(lds) + d.lds_ring_off,
-                                        d.lds_bytes - d.lds_ring_off, AX.sh, lane))
+                if (rc == kSuccess)
                 {
-                    if (lane == 0)
-                        topsort_kahn<SizeT>(g, node_count, cscore);
-                    __syncthreads();
+                    if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds) + d.lds_ring_off,
+                                            d.lds_sh_off - d.lds_ring_off, AX.sh, lane))
+                    {
+                        if (lane == 0)
+                            topsort_kahn<SizeT>(g, nc, cscore);
+                        wave_sync();
+                    }
                 }
                 ph.lap<kPhTopsort>();
+                wave_sync();
+                if (lane == 0)
+                {
+                    sh_status = rc;
+                    sh_len    = nc;
+                }
             }
+            __syncthreads();
+            status     = sh_status;
+            node_count = sh_len;
+            __syncthreads(); // sh_* are rewritten by the next read
+            if (status != kSuccess)
+                break;
         }
     }
-    finish_window<SizeT, MSA>(b, d, w, lane, g, status, nseq, node_count, cscore, cpred, ecov, ecovc, seq_begin,
-                              sh_len, sh_status);
-    ph.lap<kPhOutput>();
-    if (lane == 0)
+    if (wave == 0)
     {
-        if (b.phase)
-            ph.store(b.phase + size_t(w) * kPhases);
-        b.final_nodes[w] = node_count;
-        b.cells[w]       = cells;
+        finish_window<SizeT, MSA>(b, d, w, lane, g, status, nseq, node_count, cscore, cpred, ecov, ecovc, seq_begin,
+                                  sh_len, sh_status);
+        ph.lap<kPhOutput>();
+        if (lane == 0)
+        {
+            if (b.phase)
+                ph.store(b.phase + size_t(w) * kPhases);
+            b.final_nodes[w] = node_count;
+            b.cells[w]       = cells;
+        }
     }
 }
 
@@ -1571,26 +1430,26 @@ extern "C" hipError_t gwamd_internal_poa_launch(const gwamd::poa::Buffers* b, co
     if (d->lds_kernel && !banded && score_bits == 16 && size_bits == 16)
     {
         const size_t lb = size_t(d->lds_bytes);
-#define GWAMD_LDS_LAUNCH(CPL)                                                                                  \
-    if (msa)                                                                                                   \
-        hipLaunchKernelGGL((poa_window_kernel_lds<true, CPL>), grid, block, lb, stream, *b, *d, *sc);          \
-    else                                                                                                       \
-        hipLaunchKernelGGL((poa_window_kernel_lds<false, CPL>), grid, block, lb, stream, *b, *d, *sc);         \
-    return hipGetLastError();
-        // columns per lane: one wave pass covers the longest read when possible
-        if (d->max_seq_len <= 512)
-        {
-            GWAMD_LDS_LAUNCH(8)
-        }
-        if (d->max_seq_len <= 1024)
-        {
-            GWAMD_LDS_LAUNCH(16)
-        }
-        if (d->max_seq_len <= 1536)
-        {
-            GWAMD_LDS_LAUNCH(24)
-        }
-        GWAMD_LDS_LAUNCH(32)
+#define GWAMD_LDS_LAUNCH(CPL, NW)                                                                              \
+    if (d->lds_cpl == CPL && d->lds_waves == NW)                                                               \
+    {                                                                                                          \
+        const dim3 blk(kWave * NW);                                                                            \
+        if (msa)                                                                                               \
+            hipLaunchKernelGGL((poa_window_kernel_lds<true, CPL, NW>), grid, blk, lb, stream, *b, *d, *sc);    \
+        else                                                                                                   \
+            hipLaunchKernelGGL((poa_window_kernel_lds<false, CPL, NW>), grid, blk, lb, stream, *b, *d, *sc);   \
+        return hipGetLastError();                                                                              \
+    }
+        // (columns per lane, waves per window) pairs planned by poa_batch.cpp
+        GWAMD_LDS_LAUNCH(8, 1)
+        GWAMD_LDS_LAUNCH(16, 1)
+        GWAMD_LDS_LAUNCH(24, 1)
+        GWAMD_LDS_LAUNCH(32, 1)
+        GWAMD_LDS_LAUNCH(8, 2)
+        GWAMD_LDS_LAUNCH(8, 3)
+        GWAMD_LDS_LAUNCH(8, 4)
+        GWAMD_LDS_LAUNCH(16, 4)
+        return hipErrorInvalidConfiguration;
 #undef GWAMD_LDS_LAUNCH
     }
     const int lds_bytes = (d->max_seq_len > d->band_width + kBandPad ? d->max_seq_len : d->band_width + kBandPad) + 32;

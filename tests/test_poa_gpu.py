@@ -217,3 +217,29 @@ def test_lds_kernel_empty_and_tiny_reads():
     for i, w in enumerate(wins):
         r = run_oracle(w, 128, 8)
         assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), i
+
+
+@pytest.mark.parametrize("shape", ["8,1", "16,1", "24,1", "32,1", "8,2", "8,3", "8,4", "16,4"])
+def test_lds_forward_shapes(shape, monkeypatch):
+    # every (columns per lane, waves per window) forward-pass shape, including
+    # multi-pass rows (8,1 and 8,2 at ~1100 columns) and idle waves (8,4)
+    monkeypatch.setenv("GWAMD_POA_LDS_SHAPE", shape)
+    wins = synth.poa_windows(301, 6, 1000, 12, 50, 50, 50)
+    wins.append([b"ACGT" * 270, b"ACGT" * 269 + b"A", b"", b"ACGTTGCA" * 100])
+    b = run_gpu(wins, 1100, 12)
+    assert b.kernel_variant() == 2
+    cons, cov, st = b.get_consensus()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 1100, 12)
+        assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), (shape, i)
+
+
+def test_lds_msa_multiwave(monkeypatch):
+    monkeypatch.setenv("GWAMD_POA_LDS_SHAPE", "8,3")
+    wins = synth.poa_windows(411, 4, 900, 10, 40, 40, 40)
+    b = run_gpu(wins, 1000, 10, output_type="msa")
+    assert b.kernel_variant() == 2
+    msa, st = b.get_msa()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 1000, 10, msa=True)
+        assert st[i] == r.status and msa[i] == r.msa, i
