@@ -12,7 +12,8 @@ _LIB = None
 
 
 def library_path():
-    return os.path.join(_HERE, "lib", "libgwamd.so")
+    # GWAMD_LIBRARY: an alternative in-tree build (diagnostic builds)
+    return os.environ.get("GWAMD_LIBRARY") or os.path.join(_HERE, "lib", "libgwamd.so")
 
 
 def load_library():

@@ -397,7 +397,11 @@ __device__ __forceinline__ int prog_pred(const RowProg& P, const WinGraph<SizeT>
     if (np == 1)
         return r - int(rec >> 16);
     if (np == int(kRecEscape))
-        return pred_row(g, int(g.sorted[r - 1]), k);
+    {
+        uint32_t t = uint32_t(pred_row(g, int(g.sorted[r - 1]), k));
+        asm volatile("" : "+v"(t)); // wait here, not where the paths join
+        return int(t);
+    }
     return int(P.xl[(rec >> 16) + k]);
 }
 
@@ -503,6 +507,20 @@ __device__ __forceinline__ uint32_t opaque_u32(uint32_t v)
 }
 __device__ __forceinline__ uint32_t pk_bcast(int v) { return (uint32_t(uint16_t(v)) * 0x10001u); }
 
+// Global loads on the rare far-predecessor paths are waited for inside their
+// branch: a value still in flight where the paths join makes the compiler wait
+// for vmcnt(0) on the common path too, i.e. for every code/spill store the
+// wave has issued (HBM store latency on each row).
+__device__ __forceinline__ void settle_vm1(uint32_t& v) { asm volatile("" : "+v"(v)); }
+template <int NR>
+__device__ __forceinline__ void settle_vm(uint32_t (&P)[NR], uint32_t& prev)
+{
+#pragma unroll
+    for (int i = 0; i < NR; i++)
+        settle_vm1(P[i]);
+    settle_vm1(prev);
+}
+
 // loads the packed E values of predecessor row p (NR registers) and E_p[jb]
 template <int NR>
 __device__ __forceinline__ void load_pred_pk(const int16_t* ring, int ring_stride, int ring_mask, const int16_t* spill,
@@ -533,6 +551,7 @@ __device__ __forceinline__ void load_pred_pk(const int16_t* ring, int ring_strid
             P[4 * q] = v.x, P[4 * q + 1] = v.y, P[4 * q + 2] = v.z, P[4 * q + 3] = v.w;
         }
         prev = uint32_t(uint16_t(grow[0]));
+        settle_vm<NR>(P, prev);
     }
 }
 
@@ -546,19 +565,76 @@ __device__ __forceinline__ void diag_src(const uint32_t (&P)[NR], uint32_t prev,
         Dg[i] = __builtin_amdgcn_alignbyte(P[i], P[i - 1], 2);
 }
 
+// Diagnostic build only (-DGWAMD_FWD_PROFILE): shader-clock cycles of the
+// forward pass sections, stored in place of the backbone/add/topsort/output
+// phase slots.
+#ifdef GWAMD_FWD_PROFILE
+struct FwdProf
+{
+    uint64_t t[4] = {0, 0, 0, 0};
+    uint64_t m    = 0;
+    __device__ void start() { m = __builtin_amdgcn_s_memtime(); }
+    template <int I>
+    __device__ void lap()
+    {
+        const uint64_t x = __builtin_amdgcn_s_memtime();
+        t[I] += x - m;
+        m = x;
+    }
+};
+#define GWAMD_FP_START(fp) fp.start()
+#define GWAMD_FP_LAP(fp, I) fp.template lap<I>()
+#else
+struct FwdProf
+{
+};
+#define GWAMD_FP_START(fp)
+#define GWAMD_FP_LAP(fp, I)
+#endif
+
+// Lane-parallel predecessor rows of row rr: lane k < n holds the row of
+// predecessor slot k.  A source row gets the virtual row 0 as its single
+// predecessor (n = 1, row 0), which gives the same column-0 value (gap) and
+// the same scores as the reference's source-node case.
+template <typename SizeT>
+__device__ __forceinline__ int row_preds(const RowProg& P, const WinGraph<SizeT>& g, int rr, uint32_t rec, int lane,
+                                         int& n)
+{
+    n      = int((rec >> 8) & 63);
+    int pv = 0;
+    if (n == int(kRecEscape))
+    {
+        const int node = uniform(int(g.sorted[rr - 1]));
+        n              = uniform(int(g.in_cnt[node]));
+        uint32_t t     = lane < n ? uint32_t(pred_row(g, node, lane)) : 0u;
+        settle_vm1(t);
+        pv = int(t);
+    }
+    else if (n >= 2)
+        pv = lane < n ? int(P.xl[(rec >> 16) + lane]) : 0;
+    else if (n == 1)
+        pv = rr - int(rec >> 16);
+    if (n == 0)
+        n = 1;
+    return pv;
+}
+
 // Forward pass of one read, split over NW waves of the workgroup.  Each pass
 // covers NW * 64 * CPL columns; wave q owns the q-th 64*CPL span (CPL cells
-// per lane).  Per row every wave computes the column-0 value itself, then its
-// cells with the carry of its own span; the span totals are exchanged through
-// LDS at one barrier per pass.  The only value a wave needs from another wave's
-// span is E_p[cb] (the column left of its span) for predecessor rows p, which
-// equals the carry the wave itself computed for row p: it is kept per span
-// in `bnd` (ring rows) so no second barrier is needed per row.
+// per lane).  The column-0 value of a row is the maximum of its predecessors'
+// column-0 values, which lane 0 of wave 0 loads anyway as the diagonal source
+// of column 1.  Span totals are exchanged through LDS at one barrier per pass;
+// wave 0 publishes its total including column 0.  The only value a wave needs
+// from another wave's span is E_p[cb] (the column left of its span) for
+// predecessor rows p, which equals the carry the wave itself computed for row
+// p: it is kept per span in `bnd` (ring rows), so no second barrier is
+// needed per row.  Row r+1's predecessor list and row r+2's record are loaded
+// while row r is computed.
 template <int CPL, int NW, typename SizeT>
 __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int V, const uint8_t* read, int L,
                                  int16_t* ring, int ring_stride, int16_t* spill, int stride, uint8_t* codes,
                                  int code_stride, const Scores sc, GWAMD_LDS int* xchg, GWAMD_LDS int16_t* bnd,
-                                 int tid)
+                                 int tid, FwdProf& fp)
 {
     constexpr int NR    = CPL / 2;
     constexpr int kSpan = kWave * CPL;
@@ -578,12 +654,12 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
     int best_val        = INT_MIN;
     // owner of the last column (L-1): pass, wave, lane, cell
     const int jl        = L > 0 ? L - 1 : 0;
-    const int own_pass  = L > 0 ? jl / kPass : -1;
+    const int own_pass  = L > 0 ? jl / kPass : 0;
     const int own_wave  = (jl % kPass) / kSpan;
     const int own_lane  = (jl % kSpan) / CPL;
     const int own_c     = jl % CPL;
     const bool owner    = wave == own_wave;
-    const int npass     = (L + kPass - 1) / kPass;
+    const int npass     = max(1, (L + kPass - 1) / kPass);
     int xt              = 0; // exchange counter (double-buffered slots)
     // per-read substitution profiles for A, C, G, T (single-pass reads)
     uint32_t sig_acgt[4][NR];
@@ -601,51 +677,42 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
                                  (uint32_t(uint16_t(c1 == bases[b] ? s_eq : s_ne)) << 16);
         }
     }
-    for (int r = 1; r <= V; r++)
+    if (V < 1)
+        return 0;
+    // software pipeline: predecessor rows of row r (pv_c), record of row r+1
+    uint32_t rec_c = uniform(int(P.rec[1]));
+    int np_c;
+    int pv_c       = row_preds<SizeT>(P, g, 1, rec_c, lane, np_c);
+    uint32_t rec_n = uniform(int(P.rec[min(2, V)]));
+    uint8_t* crow  = codes + code_stride;
+    for (int r = 1; r <= V; r++, crow += code_stride)
     {
-        const uint32_t rec = P.rec[r];
+        GWAMD_FP_START(fp);
+        int np_n = 1, pv_n = 0;
+        if (r < V)
+            pv_n = row_preds<SizeT>(P, g, r + 1, rec_n, lane, np_n);
+        const uint32_t rec_nn = P.rec[min(r + 2, V)];
+
+        const uint32_t rec = rec_c;
+        const int np       = np_c;
+        const int pv       = pv_c;
         const int base     = int(rec & 0xff);
-        const int np       = uniform(prog_np(g, r, rec));
         const bool spill_r = (rec >> 15) & 1;
         int16_t* row       = ring + (r & mask) * ring_stride;
         int16_t* srow      = spill + size_t(r) * stride;
-        uint8_t* crow      = codes + size_t(r) * code_stride;
-        int c0, c0k = 0;
-        if (np == 0)
-            c0 = gap;
-        else
-        {
-            c0 = kNeg;
-            for (int k = 0; k < np; k++)
-            {
-                const int p = uniform(prog_pred(P, g, r, rec, k));
-                int v       = int(ring[(p & mask) * ring_stride + kColShift]);
-                if (p == 0)
-                    v = 0;
-                else if (r - p > mask)
-                    v = int(spill[size_t(p) * stride + kColShift]);
-                if (v > c0)
-                    c0 = v, c0k = k;
-            }
-            c0 += gap;
-        }
-        // column 0 is written before the row's exchange barrier: every wave
-        // reads it for row r+1 only after that barrier
-        if (wave == 0 && lane == 0)
-        {
-            row[kColShift]  = int16_t(c0);
-            crow[kColShift] = uint8_t(1 | (c0k << 2));
-            if (spill_r)
-                srow[kColShift] = int16_t(c0);
-        }
-        const int p0 = np == 0 ? 0 : uniform(prog_pred(P, g, r, rec, 0));
-        int carry    = c0;
-        int endv     = (L == 0) ? c0 : kNeg;
+        const bool anyfar  = __builtin_amdgcn_ballot_w64(lane < np && pv != 0 && r - pv > mask) != 0;
+        const bool acgt    = npass == 1 && (base == 'A' || base == 'C' || base == 'G' || base == 'T');
+        const bool b1      = base == 'C' || base == 'T';
+        const bool b2      = base == 'G' || base == 'T';
+        int carry          = kNeg;
+        int endv           = kNeg;
+        GWAMD_FP_LAP(fp, 0);
         for (int pass = 0; pass < npass; pass++)
         {
             const int cb      = pass * kPass + wave * kSpan;
             const int chunk   = pass * NW + wave;
-            const bool wact   = cb < L; // wave-uniform: span holds read columns
+            const bool first  = pass == 0 && wave == 0; // holds column 0
+            const bool wact   = cb < L || first;        // wave-uniform
             const int jb      = cb + lane * CPL;
             const bool active = jb < L;
             const int ja      = active ? jb : 0; // address used by inactive lanes
@@ -654,52 +721,72 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
             if (wact)
             {
                 uint32_t sig[NR];
-                if (npass == 1 && (base == 'A' || base == 'C' || base == 'G' || base == 'T'))
+                if (acgt)
                 {
-                    const int bi = base == 'A' ? 0 : base == 'C' ? 1 : base == 'G' ? 2 : 3;
-                    if (bi == 0)
-                    {
+                    // bitwise selects (a select between the profile arrays
+                    // would index them dynamically, i.e. through scratch)
+                    const uint32_t m1 = opaque_u32(b1 ? ~0u : 0u);
+                    const uint32_t m2 = opaque_u32(b2 ? ~0u : 0u);
 #pragma unroll
-                        for (int i = 0; i < NR; i++)
-                            sig[i] = sig_acgt[0][i];
-                    }
-                    else if (bi == 1)
+                    for (int i = 0; i < NR; i++)
                     {
-#pragma unroll
-                        for (int i = 0; i < NR; i++)
-                            sig[i] = sig_acgt[1][i];
-                    }
-                    else if (bi == 2)
-                    {
-#pragma unroll
-                        for (int i = 0; i < NR; i++)
-                            sig[i] = sig_acgt[2][i];
-                    }
-                    else
-                    {
-#pragma unroll
-                        for (int i = 0; i < NR; i++)
-                            sig[i] = sig_acgt[3][i];
+                        const uint32_t lo = (sig_acgt[1][i] & m1) | (sig_acgt[0][i] & ~m1);
+                        const uint32_t hi = (sig_acgt[3][i] & m1) | (sig_acgt[2][i] & ~m1);
+                        sig[i]            = (hi & m2) | (lo & ~m2);
                     }
                 }
                 else
                 {
+                    const uint32_t* rw = reinterpret_cast<const uint32_t*>(read + ja);
 #pragma unroll
                     for (int i = 0; i < NR; i++)
                     {
-                        const int ch0 = int(read[ja + 2 * i]), ch1 = int(read[ja + 2 * i + 1]);
+                        const uint32_t wv = rw[i / 2] >> ((i & 1) * 16);
+                        const int ch0 = int(wv & 0xff), ch1 = int((wv >> 8) & 0xff);
                         sig[i]        = uint32_t(uint16_t(ch0 == base ? s_eq : s_ne)) |
                                  (uint32_t(uint16_t(ch1 == base ? s_eq : s_ne)) << 16);
                     }
                 }
+                // predecessor slot 0
                 uint32_t Pv[NR], prev;
-                load_pred_pk<NR>(ring, ring_stride, mask, spill, stride, r, p0, ja, Pv, prev);
-                if constexpr (NW > 1)
+                const int p0 = __builtin_amdgcn_readfirstlane(pv);
                 {
-                    const uint32_t bv = uint32_t(uint16_t(bnd[chunk * rows + (p0 & mask)]));
-                    if (lane == 0 && cb > 0 && p0 != 0 && r - p0 <= mask)
-                        prev = bv;
+                    const int16_t* lrow = ring + (p0 & mask) * ring_stride + ja + kColShift;
+#pragma unroll
+                    for (int q = 0; q < NR / 4; q++)
+                    {
+                        const uint4 v = *reinterpret_cast<const uint4*>(lrow + 1 + 8 * q);
+                        Pv[4 * q] = v.x, Pv[4 * q + 1] = v.y, Pv[4 * q + 2] = v.z, Pv[4 * q + 3] = v.w;
+                    }
+                    prev = uint32_t(uint16_t(lrow[0]));
+                    if (p0 == 0)
+                    {
+#pragma unroll
+                        for (int i = 0; i < NR; i++)
+                            Pv[i] = 0;
+                        prev = 0;
+                    }
+                    else if (anyfar && r - p0 > mask)
+                    {
+                        const int16_t* grow = spill + size_t(p0) * stride + ja + kColShift;
+#pragma unroll
+                        for (int q = 0; q < NR / 4; q++)
+                        {
+                            const uint4 v = *reinterpret_cast<const uint4*>(grow + 1 + 8 * q);
+                            Pv[4 * q] = v.x, Pv[4 * q + 1] = v.y, Pv[4 * q + 2] = v.z, Pv[4 * q + 3] = v.w;
+                        }
+                        prev = uint32_t(uint16_t(grow[0]));
+                        settle_vm<NR>(Pv, prev);
+                    }
+                    else if (NW > 1)
+                    {
+                        const uint32_t bv = uint32_t(uint16_t(bnd[chunk * rows + (p0 & mask)]));
+                        if (lane == 0 && cb > 0)
+                            prev = bv;
+                    }
                 }
+                int c0v  = int(int16_t(prev)); // lane 0 of the first span: E_p[0]
+                int c0kv = 0;
                 diag_src<NR>(Pv, prev, dg);
 #pragma unroll
                 for (int i = 0; i < NR; i++)
@@ -710,14 +797,39 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
                 }
                 for (int k = 1; k < np; k++)
                 {
-                    const int p = uniform(prog_pred(P, g, r, rec, k));
+                    const int p = __builtin_amdgcn_readlane(pv, k);
                     uint32_t Q[NR], qprev, dq[NR];
-                    load_pred_pk<NR>(ring, ring_stride, mask, spill, stride, r, p, ja, Q, qprev);
-                    if constexpr (NW > 1)
+                    const int16_t* lrow = ring + (p & mask) * ring_stride + ja + kColShift;
+#pragma unroll
+                    for (int q = 0; q < NR / 4; q++)
+                    {
+                        const uint4 v = *reinterpret_cast<const uint4*>(lrow + 1 + 8 * q);
+                        Q[4 * q] = v.x, Q[4 * q + 1] = v.y, Q[4 * q + 2] = v.z, Q[4 * q + 3] = v.w;
+                    }
+                    qprev = uint32_t(uint16_t(lrow[0]));
+                    if (anyfar && r - p > mask)
+                    {
+                        const int16_t* grow = spill + size_t(p) * stride + ja + kColShift;
+#pragma unroll
+                        for (int q = 0; q < NR / 4; q++)
+                        {
+                            const uint4 v = *reinterpret_cast<const uint4*>(grow + 1 + 8 * q);
+                            Q[4 * q] = v.x, Q[4 * q + 1] = v.y, Q[4 * q + 2] = v.z, Q[4 * q + 3] = v.w;
+                        }
+                        qprev = uint32_t(uint16_t(grow[0]));
+                        settle_vm<NR>(Q, qprev);
+                    }
+                    else if (NW > 1)
                     {
                         const uint32_t bv = uint32_t(uint16_t(bnd[chunk * rows + (p & mask)]));
-                        if (lane == 0 && cb > 0 && p != 0 && r - p <= mask)
+                        if (lane == 0 && cb > 0)
                             qprev = bv;
+                    }
+                    {
+                        // column 0: first maximising predecessor slot
+                        const int pe = int(int16_t(qprev));
+                        c0kv         = pe > c0v ? k : c0kv;
+                        c0v          = max(c0v, pe);
                     }
                     diag_src<NR>(Q, qprev, dq);
                     const uint32_t kk = pk_bcast(k);
@@ -735,6 +847,21 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
                         vt[i]             = nv;
                     }
                 }
+                if (first)
+                {
+                    const int c0  = __builtin_amdgcn_readfirstlane(c0v) + gap;
+                    const int c0k = __builtin_amdgcn_readfirstlane(c0kv);
+                    carry         = c0;
+                    if (L == 0)
+                        endv = c0;
+                    if (lane == 0)
+                    {
+                        row[kColShift]  = int16_t(c0);
+                        crow[kColShift] = uint8_t(1 | (c0k << 2));
+                        if (spill_r)
+                            srow[kColShift] = int16_t(c0);
+                    }
+                }
                 // in-lane prefix maximum
                 uint32_t c = 0x80008000u;
 #pragma unroll
@@ -748,6 +875,7 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
                 }
                 m = active ? int(int16_t(E[NR - 1] >> 16)) : kNeg;
             }
+            GWAMD_FP_LAP(fp, 1);
             const int incl = wave_incl_max_dpp(m);
             const int excl = __builtin_amdgcn_update_dpp(kNeg, incl, 0x138, 0xf, 0xf, false);
             const int wtot = __builtin_amdgcn_readlane(incl, kWave - 1);
@@ -757,7 +885,7 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
                 GWAMD_LDS int* xs = xchg + (xt & 1) * NW;
                 xt++;
                 if (lane == 0)
-                    xs[wave] = wtot;
+                    xs[wave] = max(wtot, carry); // wave 0 / pass 0: includes column 0
                 __syncthreads();
                 int all = carry;
 #pragma unroll
@@ -774,13 +902,14 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
             }
             else
                 carry = max(carry, wtot);
+            GWAMD_FP_LAP(fp, 2);
             if (wact)
             {
                 const int below   = max(excl, cin);
-                const uint32_t b2 = pk_bcast(below);
+                const uint32_t b2v = pk_bcast(below);
 #pragma unroll
                 for (int i = 0; i < NR; i++)
-                    E[i] = pk_max(E[i], b2);
+                    E[i] = pk_max(E[i], b2v);
                 if (active)
                 {
                     // codes: 0 diagonal, 1 vertical, 2 horizontal (+ slot << 2)
@@ -827,6 +956,11 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
             if (best_val < v)
                 best_val = v, best_row = r;
         }
+        rec_c = rec_n;
+        np_c  = np_n;
+        pv_c  = pv_n;
+        rec_n = uniform(int(rec_nn));
+        GWAMD_FP_LAP(fp, 3);
     }
     if constexpr (NW > 1)
     {
@@ -1300,6 +1434,7 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
     SizeT* seq_begin = MSA ? static_cast<SizeT*>(b.seq_begin) + size_t(w) * d.max_seqs : nullptr;
 
     PhaseTimer ph;
+    FwdProf fp;
     const WindowDesc wd = b.windows[w];
     const int nseq      = wd.num_seqs;
     int status          = kSuccess;
@@ -1335,7 +1470,7 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
             __syncthreads();
             cells += int64_t(V + 1) * (L + 1);
             const int end_row = nw_forward_lds_pk<CPL, NW, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride,
-                                                                  codes, d.code_stride, sc, xchg, bnd, tid);
+                                                                  codes, d.code_stride, sc, xchg, bnd, tid, fp);
             __syncthreads();
             ph.lap<kPhForward>();
             const int alen = traceback_codes<SizeT>(g, P, V, L, end_row, codes, d.code_stride, tile, ag, ar,
@@ -1407,7 +1542,15 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
         if (lane == 0)
         {
             if (b.phase)
+            {
                 ph.store(b.phase + size_t(w) * kPhases);
+#ifdef GWAMD_FWD_PROFILE
+                // cycles / 1000 so the 100 MHz tick scaling reads as kcycles*1e-5
+                const int slot[4] = {kPhBackbone, kPhAdd, kPhTopsort, kPhOutput};
+                for (int i = 0; i < 4; i++)
+                    b.phase[size_t(w) * kPhases + slot[i]] = int64_t(fp.t[i]);
+#endif
+            }
             b.final_nodes[w] = node_count;
             b.cells[w]       = cells;
         }
