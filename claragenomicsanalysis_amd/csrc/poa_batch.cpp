@@ -558,8 +558,8 @@ private:
                 cpl = c, nw = n;
             }
         }
-        const int spans = ((ms + 64 * cpl * nw - 1) / (64 * cpl * nw)) * nw;
-        if (spans > gwamd::poa::kMaxSpans)
+        // the forward pass covers a read in one sweep: NW spans of 64*CPL columns
+        if (int64_t(64) * cpl * nw < ms)
             return;
         dims_.lds_kernel    = 1;
         dims_.lds_ring_off  = int32_t(read_b);

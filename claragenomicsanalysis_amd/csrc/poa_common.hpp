@@ -73,12 +73,16 @@ struct Dims
 };
 
 // Small shared region of the LDS kernel (kShBytes at Dims::lds_sh_off):
-// control ints, the forward pass span-total exchange ([2][waves] + end row)
-// and the per-span boundary column ([spans][ring rows] int16).
-constexpr int kShXchg    = 16;
+// control ints, per-wave channel progress, the end-row slot, the per-span
+// boundary column ([waves][ring rows] int16) and the span-to-span carry
+// channels ([waves-1][kChanRows] tagged words).
+constexpr int kShProg    = 16;
+constexpr int kShEnd     = 32;
 constexpr int kShBnd     = 64;
-constexpr int kShBytes   = 256;
-constexpr int kMaxSpans  = (kShBytes - kShBnd) / (2 * 8);
+constexpr int kShChan    = 256;
+constexpr int kChanRows  = 64;
+constexpr int kMaxWaves  = 4;
+constexpr int kShBytes   = kShChan + (kMaxWaves - 1) * kChanRows * 4;
 
 constexpr int kTileRows = 128; // traceback tile (codes) rows
 constexpr int kTileCols = 128; // traceback tile columns (bytes)

@@ -300,8 +300,8 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
                 sh_len    = nc;
             }
             __syncthreads();
-            status     = sh_status;
-            node_count = sh_len;
+            status     = uniform(sh_status); // LDS values: tell the compiler they are wave-uniform
+            node_count = uniform(sh_len);
             if (status != kSuccess)
                 break;
         }
@@ -619,28 +619,43 @@ __device__ __forceinline__ int row_preds(const RowProg& P, const WinGraph<SizeT>
     return pv;
 }
 
-// Forward pass of one read, split over NW waves of the workgroup.  Each pass
-// covers NW * 64 * CPL columns; wave q owns the q-th 64*CPL span (CPL cells
-// per lane).  The column-0 value of a row is the maximum of its predecessors'
-// column-0 values, which lane 0 of wave 0 loads anyway as the diagonal source
-// of column 1.  Span totals are exchanged through LDS at one barrier per pass;
-// wave 0 publishes its total including column 0.  The only value a wave needs
-// from another wave's span is E_p[cb] (the column left of its span) for
-// predecessor rows p, which equals the carry the wave itself computed for row
-// p: it is kept per span in `bnd` (ring rows), so no second barrier is
-// needed per row.  Row r+1's predecessor list and row r+2's record are loaded
-// while row r is computed.
+// Forward pass of one read, split over NW waves of the workgroup: wave q owns
+// the span of 64*CPL columns starting at cb = q*64*CPL (CPL cells per lane),
+// and one sweep covers the read.  The waves are decoupled, not in lockstep:
+// wave q needs from wave q-1 only the carry of each row (E_r[cb], the maximum
+// over every column left of its span), which wave q-1 posts into a tagged
+// LDS channel as soon as its row scan is done; wave q computes its own cells
+// of the row before it waits for that word.  The column-0 value of a row is
+// the maximum of its predecessors' column-0 values, which lane 0 of wave 0
+// loads anyway as the diagonal source of column 1.  The diagonal source of a
+// span's first column for predecessor row p is the carry the wave received
+// for row p (kept per wave in `bnd`, and in the spill row for far rows).
+// The predecessor row r-1 (the common case in Kahn order) comes from
+// registers; row r+1's predecessor list and row r+2's record are loaded while
+// row r is computed.
+template <int NR>
+__device__ __forceinline__ void load_row_pk(const int16_t* p, uint32_t (&P)[NR], uint32_t& prev)
+{
+#pragma unroll
+    for (int q = 0; q < NR / 4; q++)
+    {
+        const uint4 v = *reinterpret_cast<const uint4*>(p + 1 + 8 * q);
+        P[4 * q] = v.x, P[4 * q + 1] = v.y, P[4 * q + 2] = v.z, P[4 * q + 3] = v.w;
+    }
+    prev = uint32_t(uint16_t(p[0]));
+}
+
 template <int CPL, int NW, typename SizeT>
 __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int V, const uint8_t* read, int L,
                                  int16_t* ring, int ring_stride, int16_t* spill, int stride, uint8_t* codes,
-                                 int code_stride, const Scores sc, GWAMD_LDS int* xchg, GWAMD_LDS int16_t* bnd,
-                                 int tid, FwdProf& fp)
+                                 int code_stride, const Scores sc, GWAMD_LDS uint8_t* shb, int tid, FwdProf& fp)
 {
     constexpr int NR    = CPL / 2;
     constexpr int kSpan = kWave * CPL;
-    constexpr int kPass = kSpan * NW;
     const int lane      = tid & (kWave - 1);
     const int wave      = uniform(tid / kWave);
+    V                   = uniform(V);
+    L                   = uniform(L);
     const int gap       = sc.gap;
     const int s_eq      = sc.match - gap;
     const int s_ne      = sc.mismatch - gap;
@@ -649,144 +664,133 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
     const uint32_t two2 = opaque_u32(0x00020002u);
     const uint32_t four2 = opaque_u32(0x00040004u);
     const int mask      = P.ring_mask;
-    const int rows      = mask + 1;
-    int best_row        = 0;
-    int best_val        = INT_MIN;
-    // owner of the last column (L-1): pass, wave, lane, cell
+    GWAMD_LDS int* prog          = (GWAMD_LDS int*)(shb + kShProg);
+    GWAMD_LDS int16_t* bnd       = (GWAMD_LDS int16_t*)(shb + kShBnd) + wave * (mask + 1);
+    GWAMD_LDS uint32_t* chan     = (GWAMD_LDS uint32_t*)(shb + kShChan);
+    volatile GWAMD_LDS uint32_t* chan_in  = chan + (wave - 1) * kChanRows; // wave > 0
+    volatile GWAMD_LDS uint32_t* chan_out = chan + wave * kChanRows;       // wave < NW-1
+    volatile GWAMD_LDS int* prog_v        = prog;
+    const int cb        = wave * kSpan;
+    const bool wact     = cb < L || wave == 0;
+    const bool feed     = wave + 1 < NW && cb + kSpan < L; // the next span holds read columns
+    // owner of the last column (L-1): wave, lane, cell
     const int jl        = L > 0 ? L - 1 : 0;
-    const int own_pass  = L > 0 ? jl / kPass : 0;
-    const int own_wave  = (jl % kPass) / kSpan;
+    const int own_wave  = jl / kSpan;
     const int own_lane  = (jl % kSpan) / CPL;
     const int own_c     = jl % CPL;
     const bool owner    = wave == own_wave;
-    const int npass     = max(1, (L + kPass - 1) / kPass);
-    int xt              = 0; // exchange counter (double-buffered slots)
-    // per-read substitution profiles for A, C, G, T (single-pass reads)
-    uint32_t sig_acgt[4][NR];
+    int best_row        = 0;
+    int best_val        = INT_MIN;
+    const int jb        = cb + lane * CPL;
+    const bool active   = jb < L;
+    const int ja        = active ? jb : 0; // address used by inactive lanes
+    if (wact && V >= 1)
     {
-        const int jb0 = wave * kSpan + lane * CPL;
-        const int jb  = jb0 < L ? jb0 : 0; // inactive lanes read a valid address
+        // per-read substitution profiles for A, C, G, T
+        uint32_t sig_acgt[4][NR];
 #pragma unroll
         for (int i = 0; i < NR; i++)
         {
-            const int c0 = int(read[jb + 2 * i]), c1 = int(read[jb + 2 * i + 1]);
+            const int c0 = int(read[ja + 2 * i]), c1 = int(read[ja + 2 * i + 1]);
             const char bases[4] = {'A', 'C', 'G', 'T'};
 #pragma unroll
             for (int b = 0; b < 4; b++)
                 sig_acgt[b][i] = uint32_t(uint16_t(c0 == bases[b] ? s_eq : s_ne)) |
                                  (uint32_t(uint16_t(c1 == bases[b] ? s_eq : s_ne)) << 16);
         }
-    }
-    if (V < 1)
-        return 0;
-    // software pipeline: predecessor rows of row r (pv_c), record of row r+1
-    uint32_t rec_c = uniform(int(P.rec[1]));
-    int np_c;
-    int pv_c       = row_preds<SizeT>(P, g, 1, rec_c, lane, np_c);
-    uint32_t rec_n = uniform(int(P.rec[min(2, V)]));
-    uint8_t* crow  = codes + code_stride;
-    for (int r = 1; r <= V; r++, crow += code_stride)
-    {
-        GWAMD_FP_START(fp);
-        int np_n = 1, pv_n = 0;
-        if (r < V)
-            pv_n = row_preds<SizeT>(P, g, r + 1, rec_n, lane, np_n);
-        const uint32_t rec_nn = P.rec[min(r + 2, V)];
-
-        const uint32_t rec = rec_c;
-        const int np       = np_c;
-        const int pv       = pv_c;
-        const int base     = int(rec & 0xff);
-        const bool spill_r = (rec >> 15) & 1;
-        int16_t* row       = ring + (r & mask) * ring_stride;
-        int16_t* srow      = spill + size_t(r) * stride;
-        const bool anyfar  = __builtin_amdgcn_ballot_w64(lane < np && pv != 0 && r - pv > mask) != 0;
-        const bool acgt    = npass == 1 && (base == 'A' || base == 'C' || base == 'G' || base == 'T');
-        const bool b1      = base == 'C' || base == 'T';
-        const bool b2      = base == 'G' || base == 'T';
-        int carry          = kNeg;
-        int endv           = kNeg;
-        GWAMD_FP_LAP(fp, 0);
-        for (int pass = 0; pass < npass; pass++)
+        uint32_t Eprev[NR]; // final E of row r-1 (row 0: zeros)
+#pragma unroll
+        for (int i = 0; i < NR; i++)
+            Eprev[i] = 0;
+        int cin_prev = 0;
+        // software pipeline: predecessor rows of row r (pv_c), record of row r+1
+        uint32_t rec_c = uniform(int(P.rec[1]));
+        int np_c;
+        int pv_c       = row_preds<SizeT>(P, g, 1, rec_c, lane, np_c);
+        uint32_t rec_n = uniform(int(P.rec[min(2, V)]));
+        uint8_t* crow  = codes + code_stride;
+        int16_t* srow  = spill + stride;
+        for (int r = 1; r <= V; r++, crow += code_stride, srow += stride)
         {
-            const int cb      = pass * kPass + wave * kSpan;
-            const int chunk   = pass * NW + wave;
-            const bool first  = pass == 0 && wave == 0; // holds column 0
-            const bool wact   = cb < L || first;        // wave-uniform
-            const int jb      = cb + lane * CPL;
-            const bool active = jb < L;
-            const int ja      = active ? jb : 0; // address used by inactive lanes
-            uint32_t dg[NR], vt[NR], kd[NR], kv[NR], E[NR];
-            int m = kNeg;
-            if (wact)
+            GWAMD_FP_START(fp);
+            int np_n = 1, pv_n = 0;
+            if (r < V)
+                pv_n = row_preds<SizeT>(P, g, r + 1, rec_n, lane, np_n);
+            const uint32_t rec_nn = P.rec[min(r + 2, V)];
+
+            const uint32_t rec = rec_c;
+            const int np       = np_c;
+            const int pv       = pv_c;
+            const int base     = int(rec & 0xff);
+            const bool spill_r = (rec >> 15) & 1;
+            int16_t* row       = ring + (r & mask) * ring_stride;
+            const bool anyfar  = __builtin_amdgcn_ballot_w64(lane < np && pv != 0 && r - pv > mask) != 0;
+            uint32_t sig[NR];
+            if (base == 'A' || base == 'C' || base == 'G' || base == 'T')
             {
-                uint32_t sig[NR];
-                if (acgt)
+                // bitwise selects (a select between the profile arrays would
+                // index them dynamically, i.e. through scratch)
+                const uint32_t m1 = opaque_u32((base == 'C' || base == 'T') ? ~0u : 0u);
+                const uint32_t m2 = opaque_u32((base == 'G' || base == 'T') ? ~0u : 0u);
+#pragma unroll
+                for (int i = 0; i < NR; i++)
                 {
-                    // bitwise selects (a select between the profile arrays
-                    // would index them dynamically, i.e. through scratch)
-                    const uint32_t m1 = opaque_u32(b1 ? ~0u : 0u);
-                    const uint32_t m2 = opaque_u32(b2 ? ~0u : 0u);
+                    const uint32_t lo = (sig_acgt[1][i] & m1) | (sig_acgt[0][i] & ~m1);
+                    const uint32_t hi = (sig_acgt[3][i] & m1) | (sig_acgt[2][i] & ~m1);
+                    sig[i]            = (hi & m2) | (lo & ~m2);
+                }
+            }
+            else
+            {
+                const uint32_t* rw = reinterpret_cast<const uint32_t*>(read + ja);
+#pragma unroll
+                for (int i = 0; i < NR; i++)
+                {
+                    const uint32_t wv = rw[i / 2] >> ((i & 1) * 16);
+                    const int ch0 = int(wv & 0xff), ch1 = int((wv >> 8) & 0xff);
+                    sig[i]        = uint32_t(uint16_t(ch0 == base ? s_eq : s_ne)) |
+                             (uint32_t(uint16_t(ch1 == base ? s_eq : s_ne)) << 16);
+                }
+            }
+            // E values of predecessor row p for the lane's cells, and E_p[jb]
+            auto load_pred = [&](int p, uint32_t(&Q)[NR], uint32_t& qprev) {
+                if (p == r - 1)
+                {
 #pragma unroll
                     for (int i = 0; i < NR; i++)
-                    {
-                        const uint32_t lo = (sig_acgt[1][i] & m1) | (sig_acgt[0][i] & ~m1);
-                        const uint32_t hi = (sig_acgt[3][i] & m1) | (sig_acgt[2][i] & ~m1);
-                        sig[i]            = (hi & m2) | (lo & ~m2);
-                    }
+                        Q[i] = Eprev[i];
+                    qprev = uint32_t(__builtin_amdgcn_update_dpp(int(uint32_t(uint16_t(cin_prev))),
+                                                                 int(Eprev[NR - 1] >> 16), 0x138, 0xf, 0xf, false));
+                }
+                else if (p == 0)
+                {
+#pragma unroll
+                    for (int i = 0; i < NR; i++)
+                        Q[i] = 0;
+                    qprev = 0;
+                }
+                else if (anyfar && r - p > mask)
+                {
+                    load_row_pk<NR>(spill + size_t(p) * stride + ja + kColShift, Q, qprev);
+                    settle_vm<NR>(Q, qprev);
                 }
                 else
                 {
-                    const uint32_t* rw = reinterpret_cast<const uint32_t*>(read + ja);
-#pragma unroll
-                    for (int i = 0; i < NR; i++)
+                    load_row_pk<NR>(ring + (p & mask) * ring_stride + ja + kColShift, Q, qprev);
+                    if (NW > 1)
                     {
-                        const uint32_t wv = rw[i / 2] >> ((i & 1) * 16);
-                        const int ch0 = int(wv & 0xff), ch1 = int((wv >> 8) & 0xff);
-                        sig[i]        = uint32_t(uint16_t(ch0 == base ? s_eq : s_ne)) |
-                                 (uint32_t(uint16_t(ch1 == base ? s_eq : s_ne)) << 16);
+                        const uint32_t bv = uint32_t(uint16_t(bnd[p & mask]));
+                        if (lane == 0 && wave > 0)
+                            qprev = bv;
                     }
                 }
-                // predecessor slot 0
+            };
+            uint32_t dg[NR], vt[NR], kd[NR], kv[NR], E[NR];
+            int c0v, c0kv = 0;
+            {
                 uint32_t Pv[NR], prev;
-                const int p0 = __builtin_amdgcn_readfirstlane(pv);
-                {
-                    const int16_t* lrow = ring + (p0 & mask) * ring_stride + ja + kColShift;
-#pragma unroll
-                    for (int q = 0; q < NR / 4; q++)
-                    {
-                        const uint4 v = *reinterpret_cast<const uint4*>(lrow + 1 + 8 * q);
-                        Pv[4 * q] = v.x, Pv[4 * q + 1] = v.y, Pv[4 * q + 2] = v.z, Pv[4 * q + 3] = v.w;
-                    }
-                    prev = uint32_t(uint16_t(lrow[0]));
-                    if (p0 == 0)
-                    {
-#pragma unroll
-                        for (int i = 0; i < NR; i++)
-                            Pv[i] = 0;
-                        prev = 0;
-                    }
-                    else if (anyfar && r - p0 > mask)
-                    {
-                        const int16_t* grow = spill + size_t(p0) * stride + ja + kColShift;
-#pragma unroll
-                        for (int q = 0; q < NR / 4; q++)
-                        {
-                            const uint4 v = *reinterpret_cast<const uint4*>(grow + 1 + 8 * q);
-                            Pv[4 * q] = v.x, Pv[4 * q + 1] = v.y, Pv[4 * q + 2] = v.z, Pv[4 * q + 3] = v.w;
-                        }
-                        prev = uint32_t(uint16_t(grow[0]));
-                        settle_vm<NR>(Pv, prev);
-                    }
-                    else if (NW > 1)
-                    {
-                        const uint32_t bv = uint32_t(uint16_t(bnd[chunk * rows + (p0 & mask)]));
-                        if (lane == 0 && cb > 0)
-                            prev = bv;
-                    }
-                }
-                int c0v  = int(int16_t(prev)); // lane 0 of the first span: E_p[0]
-                int c0kv = 0;
+                load_pred(__builtin_amdgcn_readfirstlane(pv), Pv, prev);
+                c0v = int(int16_t(prev)); // wave 0, lane 0: E_p[0]
                 diag_src<NR>(Pv, prev, dg);
 #pragma unroll
                 for (int i = 0; i < NR; i++)
@@ -795,74 +799,35 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
                     vt[i] = pk_add(Pv[i], gap2);
                     kd[i] = kv[i] = 0;
                 }
-                for (int k = 1; k < np; k++)
+            }
+            for (int k = 1; k < np; k++)
+            {
+                uint32_t Q[NR], qprev, dq[NR];
+                load_pred(__builtin_amdgcn_readlane(pv, k), Q, qprev);
                 {
-                    const int p = __builtin_amdgcn_readlane(pv, k);
-                    uint32_t Q[NR], qprev, dq[NR];
-                    const int16_t* lrow = ring + (p & mask) * ring_stride + ja + kColShift;
-#pragma unroll
-                    for (int q = 0; q < NR / 4; q++)
-                    {
-                        const uint4 v = *reinterpret_cast<const uint4*>(lrow + 1 + 8 * q);
-                        Q[4 * q] = v.x, Q[4 * q + 1] = v.y, Q[4 * q + 2] = v.z, Q[4 * q + 3] = v.w;
-                    }
-                    qprev = uint32_t(uint16_t(lrow[0]));
-                    if (anyfar && r - p > mask)
-                    {
-                        const int16_t* grow = spill + size_t(p) * stride + ja + kColShift;
-#pragma unroll
-                        for (int q = 0; q < NR / 4; q++)
-                        {
-                            const uint4 v = *reinterpret_cast<const uint4*>(grow + 1 + 8 * q);
-                            Q[4 * q] = v.x, Q[4 * q + 1] = v.y, Q[4 * q + 2] = v.z, Q[4 * q + 3] = v.w;
-                        }
-                        qprev = uint32_t(uint16_t(grow[0]));
-                        settle_vm<NR>(Q, qprev);
-                    }
-                    else if (NW > 1)
-                    {
-                        const uint32_t bv = uint32_t(uint16_t(bnd[chunk * rows + (p & mask)]));
-                        if (lane == 0 && cb > 0)
-                            qprev = bv;
-                    }
-                    {
-                        // column 0: first maximising predecessor slot
-                        const int pe = int(int16_t(qprev));
-                        c0kv         = pe > c0v ? k : c0kv;
-                        c0v          = max(c0v, pe);
-                    }
-                    diag_src<NR>(Q, qprev, dq);
-                    const uint32_t kk = pk_bcast(k);
-#pragma unroll
-                    for (int i = 0; i < NR; i++)
-                    {
-                        // running maxima with the first maximising predecessor slot
-                        const uint32_t d  = pk_add(dq[i], sig[i]);
-                        const uint32_t nd = pk_max(dg[i], d);
-                        kd[i]             = pk_mad(pk_min_u(pk_sub(nd, dg[i]), one2), pk_sub(kk, kd[i]), kd[i]);
-                        dg[i]             = nd;
-                        const uint32_t v  = pk_add(Q[i], gap2);
-                        const uint32_t nv = pk_max(vt[i], v);
-                        kv[i]             = pk_mad(pk_min_u(pk_sub(nv, vt[i]), one2), pk_sub(kk, kv[i]), kv[i]);
-                        vt[i]             = nv;
-                    }
+                    // column 0: first maximising predecessor slot
+                    const int pe = int(int16_t(qprev));
+                    c0kv         = pe > c0v ? k : c0kv;
+                    c0v          = max(c0v, pe);
                 }
-                if (first)
+                diag_src<NR>(Q, qprev, dq);
+                const uint32_t kk = pk_bcast(k);
+#pragma unroll
+                for (int i = 0; i < NR; i++)
                 {
-                    const int c0  = __builtin_amdgcn_readfirstlane(c0v) + gap;
-                    const int c0k = __builtin_amdgcn_readfirstlane(c0kv);
-                    carry         = c0;
-                    if (L == 0)
-                        endv = c0;
-                    if (lane == 0)
-                    {
-                        row[kColShift]  = int16_t(c0);
-                        crow[kColShift] = uint8_t(1 | (c0k << 2));
-                        if (spill_r)
-                            srow[kColShift] = int16_t(c0);
-                    }
+                    // running maxima with the first maximising predecessor slot
+                    const uint32_t d  = pk_add(dq[i], sig[i]);
+                    const uint32_t nd = pk_max(dg[i], d);
+                    kd[i]             = pk_mad(pk_min_u(pk_sub(nd, dg[i]), one2), pk_sub(kk, kd[i]), kd[i]);
+                    dg[i]             = nd;
+                    const uint32_t v  = pk_add(Q[i], gap2);
+                    const uint32_t nv = pk_max(vt[i], v);
+                    kv[i]             = pk_mad(pk_min_u(pk_sub(nv, vt[i]), one2), pk_sub(kk, kv[i]), kv[i]);
+                    vt[i]             = nv;
                 }
-                // in-lane prefix maximum
+            }
+            // in-lane prefix maximum
+            {
                 uint32_t c = 0x80008000u;
 #pragma unroll
                 for (int i = 0; i < NR; i++)
@@ -873,102 +838,123 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
                     E[i]                = s;
                     c                   = __builtin_amdgcn_perm(s, s, 0x07060706u);
                 }
-                m = active ? int(int16_t(E[NR - 1] >> 16)) : kNeg;
             }
-            GWAMD_FP_LAP(fp, 1);
+            const int m    = active ? int(int16_t(E[NR - 1] >> 16)) : kNeg;
+            GWAMD_FP_LAP(fp, 0);
             const int incl = wave_incl_max_dpp(m);
             const int excl = __builtin_amdgcn_update_dpp(kNeg, incl, 0x138, 0xf, 0xf, false);
             const int wtot = __builtin_amdgcn_readlane(incl, kWave - 1);
-            int cin        = carry;
-            if constexpr (NW > 1)
+            int cin;
+            if (wave == 0)
             {
-                GWAMD_LDS int* xs = xchg + (xt & 1) * NW;
-                xt++;
+                cin           = __builtin_amdgcn_readfirstlane(c0v) + gap; // column 0
+                const int c0k = __builtin_amdgcn_readfirstlane(c0kv);
                 if (lane == 0)
-                    xs[wave] = max(wtot, carry); // wave 0 / pass 0: includes column 0
-                __syncthreads();
-                int all = carry;
-#pragma unroll
-                for (int q = 0; q < NW; q++)
                 {
-                    const int t = xs[q];
-                    if (q < wave)
-                        cin = max(cin, t);
-                    all = max(all, t);
+                    row[kColShift]  = int16_t(cin);
+                    crow[kColShift] = uint8_t(1 | (c0k << 2));
+                    if (spill_r)
+                        srow[kColShift] = int16_t(cin);
                 }
-                carry = all;
-                if (lane == 0 && cb > 0)
-                    bnd[chunk * rows + (r & mask)] = int16_t(cin);
             }
             else
-                carry = max(carry, wtot);
-            GWAMD_FP_LAP(fp, 2);
-            if (wact)
             {
-                const int below   = max(excl, cin);
-                const uint32_t b2v = pk_bcast(below);
-#pragma unroll
-                for (int i = 0; i < NR; i++)
-                    E[i] = pk_max(E[i], b2v);
-                if (active)
+                // carry of this row from the previous span
+                uint32_t w = uint32_t(uniform(int(chan_in[r & (kChanRows - 1)])));
+                while ((w >> 16) != (uint32_t(r) & 0xffffu))
                 {
-                    // codes: 0 diagonal, 1 vertical, 2 horizontal (+ slot << 2)
-                    uint32_t code[NR];
-#pragma unroll
-                    for (int i = 0; i < NR; i++)
-                    {
-                        const uint32_t a   = pk_min_u(pk_sub(E[i], dg[i]), one2); // 0: diagonal match
-                        const uint32_t bb  = pk_min_u(pk_sub(E[i], vt[i]), one2); // 0: vertical match
-                        const uint32_t cv  = pk_mad(kv[i], four2, one2);          // 1 | kv << 2
-                        const uint32_t cvh = pk_mad(bb, pk_sub(two2, cv), cv);    // vertical or horizontal
-                        const uint32_t cd  = kd[i] << 2; // kd < 64: no cross-half carry
-                        code[i]            = pk_mad(a, pk_sub(cvh, cd), cd);
-                    }
-#pragma unroll
-                    for (int q = 0; q < NR / 4; q++)
-                    {
-                        const uint4 ev = make_uint4(E[4 * q], E[4 * q + 1], E[4 * q + 2], E[4 * q + 3]);
-                        *reinterpret_cast<uint4*>(row + jb + kColShift + 1 + 8 * q) = ev;
-                        if (spill_r)
-                            *reinterpret_cast<uint4*>(srow + jb + kColShift + 1 + 8 * q) = ev;
-                        const uint32_t w0 = __builtin_amdgcn_perm(code[4 * q + 1], code[4 * q], 0x06040200u);
-                        const uint32_t w1 = __builtin_amdgcn_perm(code[4 * q + 3], code[4 * q + 2], 0x06040200u);
-                        __builtin_nontemporal_store(uint64_t(w0) | (uint64_t(w1) << 32),
-                                                    reinterpret_cast<uint64_t*>(crow + jb + kColShift + 1 + 8 * q));
-                    }
-                    if (lane == own_lane && pass == own_pass && owner)
-                    {
-#pragma unroll
-                        for (int i = 0; i < NR; i++)
-                        {
-                            if (2 * i == own_c)
-                                endv = int(int16_t(E[i] & 0xffff));
-                            if (2 * i + 1 == own_c)
-                                endv = int(int16_t(E[i] >> 16));
-                        }
-                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    w = uint32_t(uniform(int(chan_in[r & (kChanRows - 1)])));
+                }
+                cin = int(int16_t(w & 0xffffu));
+                if ((r & 7) == 0 && lane == 0)
+                    prog_v[wave] = r;
+                if (lane == 0)
+                {
+                    bnd[r & mask] = int16_t(cin);
+                    if (spill_r)
+                        srow[cb + kColShift] = int16_t(cin); // same value as the previous span's last cell
                 }
             }
+            GWAMD_FP_LAP(fp, 1);
+            if (feed)
+            {
+                // flow control: the consumer must have taken row r-kChanRows+32
+                if ((r & 31) == 0 && r >= kChanRows)
+                {
+                    while (uniform(prog_v[wave + 1]) < r - 32)
+                        __builtin_amdgcn_s_sleep(1);
+                }
+                if (lane == 0)
+                    chan_out[r & (kChanRows - 1)] = (uint32_t(r) << 16) | uint32_t(uint16_t(max(cin, wtot)));
+            }
+            GWAMD_FP_LAP(fp, 2);
+            const uint32_t b2v = pk_bcast(max(excl, cin));
+#pragma unroll
+            for (int i = 0; i < NR; i++)
+                E[i] = pk_max(E[i], b2v);
+            if (active)
+            {
+                // codes: 0 diagonal, 1 vertical, 2 horizontal (+ slot << 2)
+                uint32_t code[NR];
+#pragma unroll
+                for (int i = 0; i < NR; i++)
+                {
+                    const uint32_t a   = pk_min_u(pk_sub(E[i], dg[i]), one2); // 0: diagonal match
+                    const uint32_t bb  = pk_min_u(pk_sub(E[i], vt[i]), one2); // 0: vertical match
+                    const uint32_t cv  = pk_mad(kv[i], four2, one2);          // 1 | kv << 2
+                    const uint32_t cvh = pk_mad(bb, pk_sub(two2, cv), cv);    // vertical or horizontal
+                    const uint32_t cd  = kd[i] << 2; // kd < 64: no cross-half carry
+                    code[i]            = pk_mad(a, pk_sub(cvh, cd), cd);
+                }
+#pragma unroll
+                for (int q = 0; q < NR / 4; q++)
+                {
+                    const uint4 ev = make_uint4(E[4 * q], E[4 * q + 1], E[4 * q + 2], E[4 * q + 3]);
+                    *reinterpret_cast<uint4*>(row + jb + kColShift + 1 + 8 * q) = ev;
+                    if (spill_r)
+                        *reinterpret_cast<uint4*>(srow + jb + kColShift + 1 + 8 * q) = ev;
+                    const uint32_t w0 = __builtin_amdgcn_perm(code[4 * q + 1], code[4 * q], 0x06040200u);
+                    const uint32_t w1 = __builtin_amdgcn_perm(code[4 * q + 3], code[4 * q + 2], 0x06040200u);
+                    __builtin_nontemporal_store(uint64_t(w0) | (uint64_t(w1) << 32),
+                                                reinterpret_cast<uint64_t*>(crow + jb + kColShift + 1 + 8 * q));
+                }
+            }
+            if ((rec & (1u << 14)) && owner)
+            {
+                // sink row: E at the last column (column 0 for an empty read)
+                int endv = cin;
+#pragma unroll
+                for (int i = 0; i < NR; i++)
+                {
+                    if (2 * i == own_c)
+                        endv = int(int16_t(E[i] & 0xffff));
+                    if (2 * i + 1 == own_c)
+                        endv = int(int16_t(E[i] >> 16));
+                }
+                const int v = L == 0 ? cin : __builtin_amdgcn_readlane(endv, own_lane);
+                if (best_val < v)
+                    best_val = v, best_row = r;
+            }
+#pragma unroll
+            for (int i = 0; i < NR; i++)
+                Eprev[i] = E[i];
+            cin_prev = cin;
+            rec_c    = rec_n;
+            np_c     = np_n;
+            pv_c     = pv_n;
+            rec_n    = uniform(int(rec_nn));
+            GWAMD_FP_LAP(fp, 3);
         }
-        if ((rec & (1u << 14)) && owner)
-        {
-            const int v = __builtin_amdgcn_readlane(endv, own_lane);
-            if (best_val < v)
-                best_val = v, best_row = r;
-        }
-        rec_c = rec_n;
-        np_c  = np_n;
-        pv_c  = pv_n;
-        rec_n = uniform(int(rec_nn));
-        GWAMD_FP_LAP(fp, 3);
     }
     if constexpr (NW > 1)
     {
         // publish the end row from the wave that owns the last column
+        GWAMD_LDS int* endp = (GWAMD_LDS int*)(shb + kShEnd);
         if (owner && lane == 0)
-            xchg[2 * NW] = best_row;
+            *endp = best_row;
         __syncthreads();
-        best_row = xchg[2 * NW];
+        best_row = uniform(*endp);
     }
     return best_row;
 }
@@ -981,7 +967,9 @@ __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V
                                const uint8_t* codes, int code_stride, uint8_t* tile, SizeT* ag, SizeT* ar,
                                int aln_cap, int tid, int nthreads)
 {
-    int i = end_row, j = L;
+    V       = uniform(V);
+    L       = uniform(L);
+    int i   = uniform(end_row), j = L;
     int ti0 = INT_MIN / 2, tj0 = INT_MIN / 2;
     int n = 0, loops = 0;
     const int bound = L + V + 2;
@@ -1014,7 +1002,7 @@ __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V
                 }
                 __syncthreads();
             }
-            const int code = int(tile[(i - ti0) * kTileCols + (cj - tj0)]);
+            const int code = uniform(int(tile[(i - ti0) * kTileCols + (cj - tj0)]));
             const int dir  = code & 3;
             if (dir == 2)
             {
@@ -1023,8 +1011,8 @@ __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V
             }
             else
             {
-                const uint32_t rec = P.rec[i];
-                pi                 = prog_pred(P, g, i, rec, code >> 2);
+                const uint32_t rec = uint32_t(uniform(int(P.rec[i])));
+                pi                 = uniform(prog_pred(P, g, i, rec, code >> 2));
                 pj                 = dir == 0 ? j - 1 : j;
             }
         }
@@ -1394,8 +1382,6 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
     const int rstride = d.score_stride;      // ring / spill row stride (elements)
     RowProg P{rec, xl, d.lds_ring_rows - 1};
     GWAMD_LDS uint8_t* shb = (GWAMD_LDS uint8_t*)(lds) + d.lds_sh_off;
-    GWAMD_LDS int* xchg    = (GWAMD_LDS int*)(shb + kShXchg);
-    GWAMD_LDS int16_t* bnd = (GWAMD_LDS int16_t*)(shb + kShBnd);
     AddScratch AX;
     {
         // add-alignment scratch lives in the ring region (free between reads)
@@ -1467,10 +1453,16 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
             const int V = node_count;
             if (wave == 0)
                 build_row_program<SizeT>(g, V, rec, xl, d.lds_xl_cap, d.lds_ring_rows, lane);
+            if (NW > 1)
+            {
+                // forward-pass channels and progress words start empty
+                for (int t = tid; t < (kShBytes - kShProg) / 4; t += kThr)
+                    reinterpret_cast<GWAMD_LDS int*>(shb + kShProg)[t] = 0;
+            }
             __syncthreads();
             cells += int64_t(V + 1) * (L + 1);
             const int end_row = nw_forward_lds_pk<CPL, NW, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride,
-                                                                  codes, d.code_stride, sc, xchg, bnd, tid, fp);
+                                                                  codes, d.code_stride, sc, shb, tid, fp);
             __syncthreads();
             ph.lap<kPhForward>();
             const int alen = traceback_codes<SizeT>(g, P, V, L, end_row, codes, d.code_stride, tile, ag, ar,
@@ -1527,8 +1519,8 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
                 }
             }
             __syncthreads();
-            status     = sh_status;
-            node_count = sh_len;
+            status     = uniform(sh_status); // LDS values: tell the compiler they are wave-uniform
+            node_count = uniform(sh_len);
             __syncthreads(); // sh_* are rewritten by the next read
             if (status != kSuccess)
                 break;

@@ -221,16 +221,20 @@ def test_lds_kernel_empty_and_tiny_reads():
 
 @pytest.mark.parametrize("shape", ["8,1", "16,1", "24,1", "32,1", "8,2", "8,3", "8,4", "16,4"])
 def test_lds_forward_shapes(shape, monkeypatch):
-    # every (columns per lane, waves per window) forward-pass shape, including
-    # multi-pass rows (8,1 and 8,2 at ~1100 columns) and idle waves (8,4)
+    # every (columns per lane, waves per window) forward-pass shape; one sweep
+    # covers max_seq, so reads fill the spans up to the last one (idle lanes
+    # and idle waves included)
     monkeypatch.setenv("GWAMD_POA_LDS_SHAPE", shape)
-    wins = synth.poa_windows(301, 6, 1000, 12, 50, 50, 50)
-    wins.append([b"ACGT" * 270, b"ACGT" * 269 + b"A", b"", b"ACGTTGCA" * 100])
-    b = run_gpu(wins, 1100, 12)
+    c, n = map(int, shape.split(","))
+    max_seq = min(64 * c * n, 1100)
+    bb = max_seq - 60
+    wins = synth.poa_windows(301, 5, bb, 12, 25, 25, 25)
+    wins.append([b"ACGT" * (max_seq // 4), b"ACGT" * (max_seq // 4 - 1) + b"A", b"", b"ACGTTGCA" * (max_seq // 9)])
+    b = run_gpu(wins, max_seq, 12)
     assert b.kernel_variant() == 2
     cons, cov, st = b.get_consensus()
     for i, w in enumerate(wins):
-        r = run_oracle(w, 1100, 12)
+        r = run_oracle(w, max_seq, 12)
         assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), (shape, i)
 
 
