@@ -55,6 +55,16 @@ def cpu_threads():
     return os.cpu_count() or 1
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def main():
     args = parse()
     cfg = dict(CONFIGS[args.config])
@@ -71,8 +81,8 @@ def main():
     from claragenomicsanalysis_amd import synth
     from claragenomicsanalysis_amd.cudapoa import CudaPoaBatch
 
-    nwin = cfg["windows"]
-    first_seed = 1 + rank * nwin
+    from claragenomicsanalysis_amd.shard import window_range
+    first_seed, nwin = window_range(rank, cfg["windows"])
     t0 = time.time()
     bases, lens = synth.poa_windows_packed(first_seed, nwin, cfg["backbone"], cfg["reads"], cfg["err"], cfg["err"],
                                            cfg["err"])
@@ -138,19 +148,14 @@ def main():
     # final consensus gather to rank 0 over RCCL
     gather_ms = None
     if world > 1:
-        cmax = 2 * cfg["max_seq"]
-        buf = np.zeros((nwin, cmax + 4), np.uint8)
-        for i, c in enumerate(cons):
-            b = c.encode()
-            buf[i, :4] = np.frombuffer(np.int32(len(b)).tobytes(), np.uint8)
-            buf[i, 4:4 + len(b)] = np.frombuffer(b, np.uint8)
-        t = torch.from_numpy(buf).cuda()
-        parts = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+        from claragenomicsanalysis_amd.shard import gather_consensus
         torch.cuda.synchronize()
         tg = time.perf_counter()
-        dist.gather(t, parts, dst=0)
+        allc = gather_consensus(cons, 2 * cfg["max_seq"], device="cuda")
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
+        if rank == 0 and len(allc) != nwin * world:
+            raise RuntimeError("gather returned %d strings" % len(allc))
 
     # parity spot-check and CPU baseline (rank 0, test infrastructure)
     parity = None
@@ -174,6 +179,7 @@ def main():
                                                    max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"])
             cpu_s = time.perf_counter() - tc
             cpu = {"value": round(ns / cpu_s, 3), "unit": "windows/s", "cores": int(used), "kind": "port",
+                   "nproc": os.cpu_count(), "cpu_model": cpu_model(),
                    "sample": "first %d windows of the same workload, oracle/poa_oracle.cpp (reference-algorithm "
                              "C++ restatement, not SPOA), OpenMP one window per thread, %.1f s wall" % (ns, cpu_s),
                    "matches_gpu": bool(all(ccons[i] == cons[i] for i in range(ns)))}

@@ -1,0 +1,46 @@
+"""Copy a rocprofv3 run (scripts/profile.sh output) into profiles/<name>/.
+
+Writes kernel_stats.csv (the --kernel-trace --stats summary), pmc_summary.json
+(FETCH_SIZE / WRITE_SIZE per dispatch of the POA kernel) and, for the bench
+config, profiles/traffic_poa_<config>.json which bench.py reports as
+roofline.traffic.  HBM bytes per launch = 2 x FETCH_SIZE (gfx950 tallies a
+128 B read request as 64 B; MI355X_MICROARCH.md, HBM/rocprofv3 section)
++ WRITE_SIZE, both in KB.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(src, name, config="B", windows=1024):
+    dst = os.path.join(ROOT, "profiles", name)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "trace_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    stats = list(csv.DictReader(open(os.path.join(dst, "kernel_stats.csv"))))
+    poa = [r for r in stats if "poa_window_kernel" in r["Name"]]
+    vals = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        rows = csv.DictReader(open(os.path.join(src, "pmc_" + c, "pmc_counter_collection.csv")))
+        vals[c] = [float(r["Counter_Value"]) for r in rows
+                   if "poa_window_kernel" in r["Kernel_Name"] and r["Counter_Name"] == c]
+    fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
+    write = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
+    hbm = int((2 * fetch + write) * 1024)
+    summ = {"kernel": poa[0]["Name"] if poa else None,
+            "avg_duration_ns": float(poa[0]["AverageNs"]) if poa else None,
+            "counters_kb_per_launch": vals,
+            "hbm_bytes_per_launch": hbm,
+            "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, KB per dispatch; "
+                    "hbm bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024"}
+    json.dump(summ, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+    json.dump({"config": config, "windows": windows, "hbm_bytes_per_launch": hbm, "source": "profiles/" + name},
+              open(os.path.join(ROOT, "profiles", "traffic_poa_%s.json" % config), "w"), indent=1)
+    print(json.dumps(summ, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], *(sys.argv[3:4] or []))
