@@ -50,10 +50,14 @@ def _declare(L):
     L.oracle_add_alignment.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp]
     L.oracle_consensus_raw.restype = C.c_int
     L.oracle_consensus_raw.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp]
-    if hasattr(L, "oracle_align"):
-        L.oracle_align.restype = C.c_int
-        L.oracle_align.argtypes = [C.c_char_p, i32, C.c_char_p, i32, i32, vp]
-    del i64
+    L.oracle_align.restype = C.c_int
+    L.oracle_align.argtypes = [i32, C.c_char_p, i32, C.c_char_p, i32, i32, vp, i32]
+    L.oracle_align_batch.restype = C.c_int
+    L.oracle_align_batch.argtypes = [i32, i32, vp, vp, vp, i32, vp, vp, i32, i32]
+    L.oracle_edit_distance.restype = C.c_int
+    L.oracle_edit_distance.argtypes = [C.c_char_p, i32, C.c_char_p, i32]
+    L.oracle_query_pattern.restype = C.c_uint32
+    L.oracle_query_pattern.argtypes = [C.c_char_p, i32, C.c_char, i32, i32]
 
 
 class WindowResult:
@@ -267,3 +271,87 @@ def consensus_raw(nodes, sorted_graph, aligned, outgoing, coverage, weights, max
     st = lib().oracle_consensus_raw(n, _p(bases), _p(srt), _p(pos), _p(in_cnt), _p(in_e), _p(in_w), _p(out_cnt),
                                     _p(out_e), _p(aln_cnt), _p(aln), _p(cov), max_cons, _p(cons), _p(ccov))
     return st, bytes(cons).split(b"\0", 1)[0].decode()
+
+
+# ---------------------------------------------------------------------------
+# cudaaligner restatement (oracle/aligner_oracle.cpp)
+ALIGN_HM, ALIGN_MYERS = 0, 1
+_CIGAR = {0: "M", 1: "M", 2: "I", 3: "D"}
+
+
+def _b(s):
+    return s.encode() if isinstance(s, str) else bytes(s)
+
+
+def align(query, target, algo=ALIGN_HM, max_query_length=None):
+    """Alignment states (AlignmentState values, start -> end) of query vs target."""
+    q, t = _b(query), _b(target)
+    mq = len(q) if max_query_length is None else max_query_length
+    cap = len(q) + len(t) + 8
+    buf = np.zeros(cap, np.int8)
+    n = lib().oracle_align(algo, q, len(q), t, len(t), mq, _p(buf), cap)
+    if n < 0:
+        raise RuntimeError("oracle path buffer too small")
+    return buf[:n][::-1].tolist()
+
+
+def cigar(states):
+    """AlignmentImpl::convert_to_cigar (alignment_impl.cpp:47-73)."""
+    if not states:
+        return ""
+    out, last, cnt = [], _CIGAR[states[0]], 0
+    for s in states:
+        c = _CIGAR[s]
+        if c == last:
+            cnt += 1
+        else:
+            out.append("%d%s" % (cnt, last))
+            last, cnt = c, 1
+    out.append("%d%s" % (cnt, last))
+    return "".join(out)
+
+
+def format_alignment(query, target, states):
+    """AlignmentImpl::format_alignment (alignment_impl.cpp:75-112): (query, pairing, target)."""
+    q, t = (query.decode() if isinstance(query, bytes) else query), (target.decode() if isinstance(target, bytes)
+                                                                    else target)
+    qs, ps, ts, qi, ti = [], [], [], 0, 0
+    for s in states:
+        if s in (0, 1):
+            ts.append(t[ti]); qs.append(q[qi]); ps.append("|" if s == 0 else "x"); ti += 1; qi += 1
+        elif s == 3:
+            ts.append("-"); qs.append(q[qi]); ps.append(" "); qi += 1
+        else:
+            ts.append(t[ti]); qs.append("-"); ps.append(" "); ti += 1
+    return "".join(qs), "".join(ps), "".join(ts)
+
+
+def edit_distance(query, target):
+    q, t = _b(query), _b(target)
+    return lib().oracle_edit_distance(q, len(q), t, len(t))
+
+
+def query_pattern(query, x, word, reverse=False):
+    q = _b(query)
+    return lib().oracle_query_pattern(q, len(q), _b(x), word, int(reverse))
+
+
+def align_batch(pairs, algo=ALIGN_HM, max_query_length=None, nthreads=0):
+    """All pairs (query, target) with OpenMP; returns (list of state lists, threads used)."""
+    n = len(pairs)
+    blobs, off, lens = [], np.zeros(2 * n, np.int64), np.zeros(2 * n, np.int32)
+    pos = 0
+    for i, (q, t) in enumerate(pairs):
+        for k, s in enumerate((_b(q), _b(t))):
+            off[2 * i + k] = pos
+            lens[2 * i + k] = len(s)
+            blobs.append(s)
+            pos += len(s)
+    seqs = np.frombuffer(b"".join(blobs) + b"\0", np.uint8).copy()
+    mq = int(max(lens[0::2])) if max_query_length is None and n else (max_query_length or 0)
+    stride = int(lens.max()) * 2 + 8 if n else 8
+    paths = np.zeros(n * stride, np.int8)
+    plen = np.zeros(n, np.int32)
+    used = lib().oracle_align_batch(algo, n, _p(seqs), _p(off), _p(lens), mq, _p(paths), _p(plen), stride, nthreads)
+    out = [paths[i * stride:i * stride + plen[i]][::-1].tolist() for i in range(n)]
+    return out, used
