@@ -1,0 +1,597 @@
+// Host side of the MI355X global aligner: the reference's C++ API
+// (create_aligner / Aligner / Alignment, cudaaligner/src/aligner.cpp,
+// aligner_global.cpp, alignment_impl.cpp) and the C ABI of
+// include/gwamd_cudaaligner.h.  Device work is in aligner_kernels.hip.
+#include <claraparabricks/genomeworks/cudaaligner/aligner.hpp>
+#include <claraparabricks/genomeworks/cudaaligner/alignment.hpp>
+#include <claraparabricks/genomeworks/cudaaligner/cudaaligner.hpp>
+
+#include "aligner_common.hpp"
+#include "gwamd_cudaaligner.h"
+#include "host_common.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+extern "C" hipError_t gwamd_internal_align_launch(const gwamd::aln::Args* a, int algo, int grid, hipStream_t stream);
+extern "C" hipError_t gwamd_internal_align_occupancy(int algo, int lds_bytes, int* blocks_per_cu);
+
+namespace claraparabricks
+{
+namespace genomeworks
+{
+namespace cudaaligner
+{
+
+using gwamd::host::PinnedBuf;
+using gwamd::host::ScopedDevice;
+
+StatusType Init() { return StatusType::success; }
+
+std::ostream& operator<<(std::ostream& os, const FormattedAlignment& f)
+{
+    // alignment.cpp:24-35
+    const std::size_t line = (f.linebreak_after == 0) ? f.query.size() : f.linebreak_after;
+    for (std::size_t i = 0; i < f.query.size(); i += line)
+        os << f.query.substr(i, line) << '\n' << f.pairing.substr(i, line) << '\n' << f.target.substr(i, line) << '\n';
+    os << std::endl;
+    return os;
+}
+
+namespace
+{
+
+int32_t throw_on_negative(int32_t v, const char* msg)
+{
+    if (v < 0)
+        throw std::invalid_argument(msg);
+    return v;
+}
+
+// genomeutils::reverse_complement (genomeutils.hpp:137-150)
+void reverse_complement(const char* src, int32_t n, char* dst)
+{
+    for (int32_t p = 0; p < n; p++)
+    {
+        const char c = src[n - 1 - p];
+        dst[p]       = c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'C' ? 'G' : c == 'G' ? 'C' : c;
+    }
+}
+
+char cigar_state(AlignmentState s)
+{
+    switch (s)
+    {
+    case AlignmentState::match:
+    case AlignmentState::mismatch: return 'M';
+    case AlignmentState::insertion: return 'I';
+    case AlignmentState::deletion: return 'D';
+    default: throw std::runtime_error("Unrecognized alignment state.");
+    }
+}
+
+} // namespace
+
+// AlignmentImpl (alignment_impl.cpp:24-112)
+class AlignmentImpl : public Alignment
+{
+public:
+    AlignmentImpl(const char* query, int32_t query_length, const char* target, int32_t target_length)
+        : query_(query, query + throw_on_negative(query_length, "query_length has to be non-negative."))
+        , target_(target, target + throw_on_negative(target_length, "target_length has to be non-negative."))
+    {
+    }
+    const std::string& get_query_sequence() const override { return query_; }
+    const std::string& get_target_sequence() const override { return target_; }
+    AlignmentType get_alignment_type() const override { return type_; }
+    StatusType get_status() const override { return status_; }
+    const std::vector<AlignmentState>& get_alignment() const override { return alignment_; }
+    void set_alignment_type(AlignmentType t) { type_ = t; }
+    void set_status(StatusType s) { status_ = s; }
+    void set_alignment(std::vector<AlignmentState>&& a) { alignment_ = std::move(a); }
+
+    std::string convert_to_cigar() const override
+    {
+        if (alignment_.empty())
+            return std::string();
+        std::string cigar;
+        char last   = cigar_state(alignment_[0]);
+        int32_t cnt = 0;
+        for (AlignmentState x : alignment_)
+        {
+            const char c = cigar_state(x);
+            if (c == last)
+                cnt++;
+            else
+            {
+                cigar += std::to_string(cnt) + last;
+                cnt  = 1;
+                last = c;
+            }
+        }
+        cigar += std::to_string(cnt) + last;
+        return cigar;
+    }
+
+    FormattedAlignment format_alignment(int32_t maximal_line_length) const override
+    {
+        int64_t t = 0, q = 0;
+        FormattedAlignment r;
+        r.linebreak_after = (maximal_line_length < 0) ? 0 : maximal_line_length;
+        for (AlignmentState x : alignment_)
+        {
+            switch (x)
+            {
+            case AlignmentState::match:
+                r.target += target_[t++];
+                r.query += query_[q++];
+                r.pairing += '|';
+                break;
+            case AlignmentState::mismatch:
+                r.target += target_[t++];
+                r.query += query_[q++];
+                r.pairing += 'x';
+                break;
+            case AlignmentState::deletion:
+                r.target += '-';
+                r.query += query_[q++];
+                r.pairing += ' ';
+                break;
+            case AlignmentState::insertion:
+                r.target += target_[t++];
+                r.query += '-';
+                r.pairing += ' ';
+                break;
+            default: throw std::runtime_error("Unknown alignment state");
+            }
+        }
+        return r;
+    }
+
+private:
+    std::string query_, target_;
+    StatusType status_ = StatusType::uninitialized;
+    AlignmentType type_ = AlignmentType::unset;
+    std::vector<AlignmentState> alignment_;
+};
+
+// AlignerGlobal (aligner_global.cpp) with the HIP kernels of aligner_kernels.hip.
+class AlignerGlobalHip : public Aligner
+{
+public:
+    AlignerGlobalHip(int32_t max_query_length, int32_t max_target_length, int32_t max_alignments, int algorithm,
+                     hipStream_t stream, int32_t device_id)
+        : max_q_(throw_on_negative(max_query_length, "max_query_length must be non-negative."))
+        , max_t_(throw_on_negative(max_target_length, "max_target_length must be non-negative."))
+        , max_n_(throw_on_negative(max_alignments, "max_alignments must be non-negative."))
+        , algo_(algorithm)
+        , stream_(stream)
+        , device_id_(device_id)
+    {
+        if (max_alignments < 1)
+            throw std::runtime_error("Max alignments must be at least 1.");
+        // limits of this implementation: the Myers state of a query segment
+        // is held in 4 blocks of 64x32 bits; split scores are 16-bit in LDS
+        if (algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS && max_q_ > 16384)
+            throw std::invalid_argument("max_query_length above 16384 is not supported by this aligner.");
+        if (algo_ == GWAMD_ALIGNER_MYERS && max_q_ > 8192)
+            throw std::invalid_argument("max_query_length above 8192 is not supported by the full Myers aligner.");
+        if (max_t_ > 65535)
+            throw std::invalid_argument("max_target_length above 65535 is not supported by this aligner.");
+        stride_     = std::max(max_q_, max_t_);
+        max_result_ = (max_q_ + max_t_ + 3) / 4 * 4; // calc_max_result_length (aligner_global.cpp:26-31)
+        ScopedDevice dev(device_id_);
+        plan();
+        auto dalloc = [&](void** p, size_t bytes) {
+            GWAMD_HIP_CHECK(hipMalloc(p, std::max<size_t>(bytes, 16)));
+            GWAMD_HIP_CHECK(hipMemsetAsync(*p, 0, std::max<size_t>(bytes, 16), stream_));
+            device_bytes_ += int64_t(bytes);
+        };
+        dalloc(reinterpret_cast<void**>(&d_seqs_), size_t(2) * stride_ * max_n_ + 16);
+        dalloc(reinterpret_cast<void**>(&d_lens_), size_t(2) * max_n_ * 4);
+        dalloc(reinterpret_cast<void**>(&d_paths_), size_t(max_result_) * max_n_ + 16);
+        dalloc(reinterpret_cast<void**>(&d_plen_), size_t(max_n_) * 4);
+        dalloc(reinterpret_cast<void**>(&d_ws_), size_t(slots_) * size_t(slot_bytes_));
+        h_seqs_.reserve(size_t(2) * stride_ * max_n_ + 16, stream_);
+        h_lens_.reserve(size_t(2) * max_n_ * 4, stream_);
+        h_paths_.reserve(size_t(max_result_) * max_n_ + 16, stream_);
+        h_plen_.reserve(size_t(max_n_) * 4, stream_);
+        GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+
+    ~AlignerGlobalHip() override
+    {
+        (void)hipSetDevice(device_id_);
+        for (void* p : {static_cast<void*>(d_seqs_), static_cast<void*>(d_lens_), static_cast<void*>(d_paths_),
+                        static_cast<void*>(d_plen_), static_cast<void*>(d_ws_)})
+            if (p)
+                (void)hipFree(p);
+    }
+
+    StatusType add_alignment(const char* query, int32_t query_length, const char* target, int32_t target_length,
+                             bool rc_query, bool rc_target) override
+    {
+        // aligner_global.cpp:60-118
+        if (query_length < 0 || target_length < 0)
+            return StatusType::generic_error;
+        const int32_t n = int32_t(alignments_.size());
+        if (n >= max_n_)
+            return StatusType::exceeded_max_alignments;
+        if (query_length > max_q_)
+            return StatusType::exceeded_max_length;
+        if (target_length > max_t_)
+            return StatusType::exceeded_max_length;
+        char* qd = h_seqs_.as<char>() + size_t(2 * n) * stride_;
+        char* td = h_seqs_.as<char>() + size_t(2 * n + 1) * stride_;
+        if (rc_query)
+            reverse_complement(query, query_length, qd);
+        else if (query_length > 0)
+            std::memcpy(qd, query, size_t(query_length));
+        if (rc_target)
+            reverse_complement(target, target_length, td);
+        else if (target_length > 0)
+            std::memcpy(td, target, size_t(target_length));
+        h_lens_.as<int32_t>()[2 * n]     = query_length;
+        h_lens_.as<int32_t>()[2 * n + 1] = target_length;
+        auto a = std::make_shared<AlignmentImpl>(qd, query_length, td, target_length);
+        a->set_alignment_type(AlignmentType::global_alignment);
+        alignments_.push_back(a);
+        return StatusType::success;
+    }
+
+    StatusType align_all() override
+    {
+        if (alignments_.empty())
+            return StatusType::success;
+        upload();
+        launch();
+        download();
+        return StatusType::success;
+    }
+
+    StatusType sync_alignments() override
+    {
+        // aligner_global.cpp:161-189: paths come out end -> start
+        ScopedDevice dev(device_id_);
+        GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
+        const int32_t n = int32_t(alignments_.size());
+        for (int32_t i = 0; i < n; i++)
+        {
+            const int32_t len = h_plen_.as<int32_t>()[i];
+            const int8_t* p   = h_paths_.as<int8_t>() + size_t(i) * max_result_;
+            std::vector<AlignmentState> st(size_t(std::max(len, 0)));
+            for (int32_t k = 0; k < len; k++)
+                st[size_t(len - 1 - k)] = static_cast<AlignmentState>(p[k]);
+            auto* a = static_cast<AlignmentImpl*>(alignments_[size_t(i)].get());
+            a->set_alignment(std::move(st));
+            a->set_status(StatusType::success);
+        }
+        return StatusType::success;
+    }
+
+    const std::vector<std::shared_ptr<Alignment>>& get_alignments() const override { return alignments_; }
+    void reset() override { alignments_.clear(); }
+
+    // bench / C ABI helpers
+    void upload()
+    {
+        ScopedDevice dev(device_id_);
+        const size_t n = alignments_.size();
+        GWAMD_HIP_CHECK(hipMemcpyAsync(d_lens_, h_lens_.as<int32_t>(), 2 * n * 4, hipMemcpyHostToDevice, stream_));
+        GWAMD_HIP_CHECK(hipMemcpyAsync(d_seqs_, h_seqs_.as<char>(), 2 * n * size_t(stride_), hipMemcpyHostToDevice,
+                                       stream_));
+    }
+    void launch()
+    {
+        ScopedDevice dev(device_id_);
+        gwamd::aln::Args a = args();
+        const int grid     = std::min<int>(int(alignments_.size()), slots_);
+        GWAMD_HIP_CHECK(gwamd_internal_align_launch(&a, algo_, grid, stream_));
+    }
+    void download()
+    {
+        ScopedDevice dev(device_id_);
+        const size_t n = alignments_.size();
+        GWAMD_HIP_CHECK(hipMemcpyAsync(h_paths_.as<int8_t>(), d_paths_, n * size_t(max_result_),
+                                       hipMemcpyDeviceToHost, stream_));
+        GWAMD_HIP_CHECK(hipMemcpyAsync(h_plen_.as<int32_t>(), d_plen_, n * 4, hipMemcpyDeviceToHost, stream_));
+    }
+    void synchronize()
+    {
+        ScopedDevice dev(device_id_);
+        GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+    const int8_t* host_paths() const { return h_paths_.as<int8_t>(); }
+    const int32_t* host_path_lengths() const { return h_plen_.as<int32_t>(); }
+    int32_t max_result_length() const { return max_result_; }
+    int32_t grid() const { return slots_; }
+    int64_t device_bytes() const { return device_bytes_; }
+
+private:
+    static int64_t a16(int64_t v) { return (v + 15) & ~int64_t(15); }
+
+    void plan()
+    {
+        using namespace gwamd::aln;
+        const int pat_words = (max_q_ + kWordBits - 1) / kWordBits;
+        lds_target_off_     = 0;
+        lds_pat_off_        = int32_t(a16(max_t_ + 16));
+        lds_scratch_off_    = int32_t(lds_pat_off_ + a16(int64_t(pat_words) * 32 + 16));
+        scratch_bytes_      = 0;
+        if (algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS)
+            scratch_bytes_ = int32_t(a16(std::max<int64_t>(int64_t(max_t_ + 1) * 2, int64_t(kLeafCols) * kLeafColBytes)));
+        lds_stack_off_ = lds_scratch_off_ + scratch_bytes_;
+        lds_bytes_     = lds_stack_off_ + (algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS ? kStackSize * 16 : 0);
+        if (lds_bytes_ > 65536)
+            throw std::invalid_argument("aligner problem size does not fit in LDS");
+        pat_words_ = pat_words;
+        int per_cu = 1, cus = 1;
+        GWAMD_HIP_CHECK(gwamd_internal_align_occupancy(algo_, lds_bytes_, &per_cu));
+        GWAMD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
+        slots_ = std::max(1, per_cu * cus);
+        if (algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS)
+            slot_bytes_ = a16(int64_t(max_t_ + 1) * 20 + 64); // base cases too wide for LDS
+        else
+        {
+            // full matrix: pv, mv, score per (word, column)
+            slot_bytes_ = a16(int64_t(pat_words) * (max_t_ + 1) * 12 + 64);
+            const int64_t cap = int64_t(4) << 30; // keep the resident slots within 4 GiB
+            slots_            = int32_t(std::max<int64_t>(1, std::min<int64_t>(slots_, cap / slot_bytes_)));
+        }
+        slots_ = std::min(slots_, max_n_);
+    }
+
+    gwamd::aln::Args args() const
+    {
+        gwamd::aln::Args a{};
+        a.seqs             = d_seqs_;
+        a.lens             = d_lens_;
+        a.stride           = stride_;
+        a.paths            = d_paths_;
+        a.path_len         = d_plen_;
+        a.max_path_length  = max_result_;
+        a.n                = int32_t(alignments_.size());
+        a.max_query_length = max_q_;
+        a.max_matrix_elems = int64_t((max_q_ + 3) / 4) * (gwamd::aln::kFullMyers + 1);
+        a.ws               = d_ws_;
+        a.ws_slot_bytes    = slot_bytes_;
+        a.lds_target_off   = lds_target_off_;
+        a.lds_pat_off      = lds_pat_off_;
+        a.lds_scratch_off  = lds_scratch_off_;
+        a.lds_stack_off    = lds_stack_off_;
+        a.lds_bytes        = lds_bytes_;
+        a.pat_words        = pat_words_;
+        a.scratch_bytes    = scratch_bytes_;
+        return a;
+    }
+
+    int32_t max_q_, max_t_, max_n_;
+    int algo_;
+    hipStream_t stream_;
+    int32_t device_id_;
+    int32_t stride_ = 0, max_result_ = 0;
+    int32_t lds_target_off_ = 0, lds_pat_off_ = 0, lds_scratch_off_ = 0, lds_stack_off_ = 0, lds_bytes_ = 0;
+    int32_t pat_words_ = 0, scratch_bytes_ = 0;
+    int32_t slots_ = 1;
+    int64_t slot_bytes_ = 0, device_bytes_ = 0;
+    char* d_seqs_     = nullptr;
+    int32_t* d_lens_  = nullptr;
+    int8_t* d_paths_  = nullptr;
+    int32_t* d_plen_  = nullptr;
+    uint8_t* d_ws_    = nullptr;
+    PinnedBuf h_seqs_, h_lens_, h_paths_, h_plen_;
+    std::vector<std::shared_ptr<Alignment>> alignments_;
+};
+
+std::unique_ptr<Aligner> create_aligner(int32_t max_query_length, int32_t max_target_length, int32_t max_alignments,
+                                        AlignmentType type, DefaultDeviceAllocator allocator, hipStream_t stream,
+                                        int32_t device_id)
+{
+    (void)allocator;
+    // aligner.cpp:30-38
+    if (type == AlignmentType::global_alignment)
+        return std::make_unique<AlignerGlobalHip>(max_query_length, max_target_length, max_alignments,
+                                                  GWAMD_ALIGNER_HIRSCHBERG_MYERS, stream, device_id);
+    throw std::runtime_error("Aligner for specified type not implemented yet.");
+}
+
+std::unique_ptr<Aligner> create_aligner(int32_t max_query_length, int32_t max_target_length, int32_t max_alignments,
+                                        AlignmentType type, hipStream_t stream, int32_t device_id,
+                                        int64_t max_device_memory_allocator_caching_size)
+{
+    // aligner.cpp:40-63
+    if (max_device_memory_allocator_caching_size < -1)
+        throw std::invalid_argument("max_device_memory_allocator_caching_size has to be either -1 (=all available "
+                                    "GPU memory) or greater or equal than 0.");
+    return create_aligner(max_query_length, max_target_length, max_alignments, type,
+                          DefaultDeviceAllocator(max_device_memory_allocator_caching_size), stream, device_id);
+}
+
+} // namespace cudaaligner
+} // namespace genomeworks
+} // namespace claraparabricks
+
+// ===========================================================================
+// C ABI (include/gwamd_cudaaligner.h)
+// ===========================================================================
+namespace ca = claraparabricks::genomeworks::cudaaligner;
+
+namespace
+{
+template <typename F>
+int32_t guarded_aln(F&& f)
+{
+    try
+    {
+        gwamd::host::last_error().clear();
+        return f();
+    }
+    catch (const std::invalid_argument& e)
+    {
+        gwamd::host::last_error() = e.what();
+        return GWAMD_E_INVALID_ARGUMENT;
+    }
+    catch (const std::runtime_error& e)
+    {
+        gwamd::host::last_error() = e.what();
+        return std::string(e.what()).rfind("HIP error", 0) == 0 ? GWAMD_E_HIP : GWAMD_E_RUNTIME;
+    }
+    catch (const std::exception& e)
+    {
+        gwamd::host::last_error() = e.what();
+        return GWAMD_E_RUNTIME;
+    }
+}
+} // namespace
+
+struct gwamd_aligner
+{
+    std::unique_ptr<ca::AlignerGlobalHip> impl;
+};
+
+extern "C" {
+
+int32_t gwamd_aligner_create(gwamd_aligner** out, int32_t max_query_length, int32_t max_target_length,
+                             int32_t max_alignments, int32_t alignment_type, int32_t algorithm, void* stream,
+                             int32_t device_id, int64_t max_caching)
+{
+    return guarded_aln([&] {
+        if (!out)
+            throw std::invalid_argument("out is NULL");
+        if (max_caching < -1)
+            throw std::invalid_argument("max_device_memory_allocator_caching_size has to be either -1 (=all "
+                                        "available GPU memory) or greater or equal than 0.");
+        if (alignment_type != ca::AlignmentType::global_alignment)
+            throw std::runtime_error("Aligner for specified type not implemented yet.");
+        if (algorithm != GWAMD_ALIGNER_HIRSCHBERG_MYERS && algorithm != GWAMD_ALIGNER_MYERS)
+            throw std::invalid_argument("unknown aligner algorithm");
+        auto h  = std::make_unique<gwamd_aligner>();
+        h->impl = std::make_unique<ca::AlignerGlobalHip>(max_query_length, max_target_length, max_alignments,
+                                                         algorithm, static_cast<hipStream_t>(stream), device_id);
+        *out    = h.release();
+        return int32_t(0);
+    });
+}
+
+void gwamd_aligner_destroy(gwamd_aligner* a) { delete a; }
+
+int32_t gwamd_aligner_add_alignment(gwamd_aligner* a, const char* q, int32_t qlen, const char* t, int32_t tlen,
+                                    int32_t rc_q, int32_t rc_t)
+{
+    return guarded_aln([&] { return int32_t(a->impl->add_alignment(q, qlen, t, tlen, rc_q != 0, rc_t != 0)); });
+}
+
+int32_t gwamd_aligner_align_all(gwamd_aligner* a)
+{
+    return guarded_aln([&] { return int32_t(a->impl->align_all()); });
+}
+
+int32_t gwamd_aligner_sync_alignments(gwamd_aligner* a)
+{
+    return guarded_aln([&] { return int32_t(a->impl->sync_alignments()); });
+}
+
+int32_t gwamd_aligner_num_alignments(const gwamd_aligner* a) { return int32_t(a->impl->get_alignments().size()); }
+
+int32_t gwamd_aligner_get_alignment(gwamd_aligner* a, int32_t i, int8_t* states, int32_t cap, int32_t* status)
+{
+    return guarded_aln([&] {
+        const auto& al = a->impl->get_alignments();
+        if (i < 0 || i >= int32_t(al.size()))
+            throw std::invalid_argument("alignment index out of range");
+        const auto& st = al[size_t(i)]->get_alignment();
+        if (status)
+            *status = int32_t(al[size_t(i)]->get_status());
+        if (states && int32_t(st.size()) <= cap)
+            for (size_t k = 0; k < st.size(); k++)
+                states[k] = int8_t(st[k]);
+        return int32_t(st.size());
+    });
+}
+
+int32_t gwamd_aligner_get_sequences(gwamd_aligner* a, int32_t i, const char** q, int32_t* qlen, const char** t,
+                                    int32_t* tlen)
+{
+    return guarded_aln([&] {
+        const auto& al = a->impl->get_alignments();
+        if (i < 0 || i >= int32_t(al.size()))
+            throw std::invalid_argument("alignment index out of range");
+        const std::string& qs = al[size_t(i)]->get_query_sequence();
+        const std::string& ts = al[size_t(i)]->get_target_sequence();
+        *q                    = qs.data();
+        *qlen                 = int32_t(qs.size());
+        *t                    = ts.data();
+        *tlen                 = int32_t(ts.size());
+        return int32_t(0);
+    });
+}
+
+int32_t gwamd_aligner_get_cigar(gwamd_aligner* a, int32_t i, char* buf, int32_t cap)
+{
+    return guarded_aln([&] {
+        const auto& al = a->impl->get_alignments();
+        if (i < 0 || i >= int32_t(al.size()))
+            throw std::invalid_argument("alignment index out of range");
+        const std::string c = al[size_t(i)]->convert_to_cigar();
+        if (buf && int32_t(c.size()) < cap)
+            std::memcpy(buf, c.c_str(), c.size() + 1);
+        return int32_t(c.size());
+    });
+}
+
+void gwamd_aligner_reset(gwamd_aligner* a) { a->impl->reset(); }
+
+int32_t gwamd_aligner_upload(gwamd_aligner* a)
+{
+    return guarded_aln([&] {
+        a->impl->upload();
+        return int32_t(0);
+    });
+}
+
+int32_t gwamd_aligner_launch(gwamd_aligner* a)
+{
+    return guarded_aln([&] {
+        a->impl->launch();
+        return int32_t(0);
+    });
+}
+
+int32_t gwamd_aligner_download(gwamd_aligner* a)
+{
+    return guarded_aln([&] {
+        a->impl->download();
+        return int32_t(0);
+    });
+}
+
+int32_t gwamd_aligner_synchronize(gwamd_aligner* a)
+{
+    return guarded_aln([&] {
+        a->impl->synchronize();
+        return int32_t(0);
+    });
+}
+
+int32_t gwamd_aligner_get_paths(gwamd_aligner* a, const int8_t** paths, const int32_t** lengths, int32_t* stride)
+{
+    *paths   = a->impl->host_paths();
+    *lengths = a->impl->host_path_lengths();
+    *stride  = a->impl->max_result_length();
+    return 0;
+}
+
+int32_t gwamd_aligner_get_config(const gwamd_aligner* a, int32_t* grid, int64_t* device_bytes)
+{
+    *grid         = a->impl->grid();
+    *device_bytes = a->impl->device_bytes();
+    return 0;
+}
+
+} // extern "C"

@@ -1,0 +1,59 @@
+// Shared host/device definitions for the MI355X global aligner
+// (cudaaligner: AlignerGlobalHirschbergMyers, AlignerGlobalMyers).
+//
+// Batch layout (same packing as the reference, aligner_global.cpp:33-116):
+// pair i's query at seqs + 2*i*stride, its target at seqs + (2*i+1)*stride;
+// lengths[2i], lengths[2i+1]; path i (int8 AlignmentState, emitted end ->
+// start, reversed on the host) at paths + i*max_path_length; path_len[i].
+#pragma once
+
+#include <cstdint>
+
+namespace gwamd
+{
+namespace aln
+{
+
+constexpr int kWave       = 64;
+constexpr int kWordBits   = 32;  // Myers word (hirschbergmyers::WordType, uint32_t)
+constexpr int kStackSize  = 64;  // hirschberg_myers_stackbuffer_size (aligner_global_hirschberg_myers.cpp:29)
+constexpr int kFullMyers  = 63;  // hirschberg_myers_switch_to_myers_size (:30)
+constexpr int kMaxChunks  = 4;   // Myers block = 64 lanes x 32 bits; up to 4 blocks per sweep
+constexpr int kLeafCols   = 512; // base-case columns kept in LDS (larger leaves use HBM)
+constexpr int kLeafColBytes = 20; // per column: pv u64, mv u64, score i32
+
+// AlignmentState (cudaaligner.hpp:46-52)
+enum State : int8_t
+{
+    kMatch     = 0,
+    kMismatch  = 1,
+    kInsertion = 2,
+    kDeletion  = 3,
+};
+
+struct Args
+{
+    const char* seqs;
+    const int32_t* lens;
+    int32_t stride;          // max(max_query_length, max_target_length)
+    int8_t* paths;
+    int32_t* path_len;
+    int32_t max_path_length; // ceil4(maxQ + maxT) (aligner_global.cpp:32-37)
+    int32_t n;
+    int32_t max_query_length;
+    int64_t max_matrix_elems; // ceil(maxQ/4) * 64: the reference's pv/mv matrix capacity
+    // global workspace, one slot per resident workgroup
+    uint8_t* ws;
+    int64_t ws_slot_bytes;
+    // LDS layout (bytes)
+    int32_t lds_target_off;
+    int32_t lds_pat_off;     // [pat_words][8] u32: forward A C T G, reverse A C T G
+    int32_t lds_scratch_off;
+    int32_t lds_stack_off;
+    int32_t lds_bytes;
+    int32_t pat_words;       // ceil(max_query_length / 32)
+    int32_t scratch_bytes;
+};
+
+} // namespace aln
+} // namespace gwamd

@@ -1,0 +1,673 @@
+// MI355X global aligners: Hirschberg + Myers (the default of create_aligner,
+// cudaaligner/src/hirschberg_myers_gpu.cu) and full Myers with backtrace
+// (AlignerGlobalMyers, cudaaligner/src/myers_gpu.cu:95-375).
+//
+// One wave per pair; a persistent grid walks the pairs with a static stride.
+// The Myers bit-vector state of a query segment lives in registers: lane l of
+// block c holds query word 64c + l (32 rows), a block is 2048 rows, and the
+// multi-word addition and the one-bit shift of the recurrence cross lanes with
+// ballot masks (carry lookahead on the 64-bit generate/propagate masks) and
+// the lane-bit extraction below.  Any exact Myers implementation gives the
+// edit-distance matrix bit for bit, so the results depend only on the tie
+// rules, which follow the reference:
+//   * target split: minimum of fwd(t) + rev(T-t), ties to the 32-lane /
+//     shfl_down order (hirschberg_myers_gpu.cu:450-474),
+//   * backtrace: insertion, then deletion, then diagonal (:118-160),
+//   * base cases and their order, the 64-entry stack and its overflow
+//     behaviour, the full-Myers switch condition with the reference's
+//     workspace capacity (:569-638, aligner_global_hirschberg_myers.cpp:51-54).
+#include <hip/hip_runtime.h>
+
+#include "aligner_common.hpp"
+
+#include <climits>
+
+#define GWAMD_LDS __attribute__((address_space(3)))
+
+namespace gwamd
+{
+namespace aln
+{
+
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint32_t uniu(uint32_t x) { return uint32_t(__builtin_amdgcn_readfirstlane(int(x))); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x)
+{
+    return uint64_t(uniu(uint32_t(x))) | (uint64_t(uniu(uint32_t(x >> 32))) << 32);
+}
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// bit `lane` of a 64-bit wave mask
+__device__ __forceinline__ uint32_t mask_bit(uint64_t m, uint32_t lo_or_hi_sel, int lane)
+{
+    const uint32_t half = lo_or_hi_sel ? uint32_t(m >> 32) : uint32_t(m);
+    return __builtin_amdgcn_ubfe(half, uint32_t(lane & 31), 1u);
+}
+
+// Myers letter index of a target character: "ACTG"[(c >> 1) & 3]
+// (hirschberg_myers_gpu.cu:241-244)
+__device__ __forceinline__ int letter(int c) { return (c >> 1) & 3; }
+
+// Query pattern words of the whole query: pat[k*8 + L] (L = A C T G forward,
+// 4 + L reversed), bit i of word k set where query[32k+i] (resp.
+// query[Q-1-(32k+i)]) equals the letter (myers_preprocess, :210-225).
+__device__ void build_patterns(GWAMD_LDS uint32_t* pat, const char* q, int Q, int lane)
+{
+    const int nw = (Q + kWordBits - 1) / kWordBits;
+    const char letters[4] = {'A', 'C', 'T', 'G'};
+    for (int k = lane; k < nw; k += kWave)
+    {
+        uint32_t f[4] = {0, 0, 0, 0}, r[4] = {0, 0, 0, 0};
+        const int lim = min(Q - k * kWordBits, kWordBits);
+        for (int i = 0; i < lim; i++)
+        {
+            const char cf = q[k * kWordBits + i];
+            const char cr = q[Q - 1 - (k * kWordBits + i)];
+#pragma unroll
+            for (int L = 0; L < 4; L++)
+            {
+                f[L] |= (cf == letters[L] ? 1u : 0u) << i;
+                r[L] |= (cr == letters[L] ? 1u : 0u) << i;
+            }
+        }
+#pragma unroll
+        for (int L = 0; L < 4; L++)
+        {
+            pat[k * 8 + L]     = f[L];
+            pat[k * 8 + 4 + L] = r[L];
+        }
+    }
+}
+
+// Segment pattern word w for letter L: rows start at query offset `off` of the
+// (forward or reversed) query (get_query_pattern, :246-268).
+__device__ __forceinline__ uint32_t seg_pattern(const GWAMD_LDS uint32_t* pat, int pat_words, int off, int w, int L)
+{
+    const int k  = (off >> 5) + w;
+    const int sh = off & 31;
+    uint32_t r   = k < pat_words ? pat[k * 8 + L] : 0u;
+    if (sh != 0)
+    {
+        r >>= sh;
+        if (k + 1 < pat_words)
+            r |= pat[(k + 1) * 8 + L] << (32 - sh);
+    }
+    return r;
+}
+
+// One column of the block-wise Myers recurrence for block c.  hin is the
+// horizontal delta entering the block's first row; returns the delta leaving
+// its last row (row `hb` of lane `ll` for the segment's last block).
+struct MyersBlock
+{
+    uint32_t pv, mv;
+    uint32_t e[4];
+    uint64_t act; // lanes holding segment words
+};
+
+// own (optional): each lane's delta at its own word's last row (bit own_hb),
+// i.e. the per-word score update of the full-matrix variant (myers_gpu.cu:356).
+template <bool OWN = false>
+__device__ __forceinline__ int myers_block_step(MyersBlock& B, int code, int hin, bool last, int ll, int hb, int lane,
+                                                uint32_t hisel, uint32_t lane0bit, int own_hb = 31,
+                                                int* own = nullptr)
+{
+    // select the pattern of this column's letter (code is wave-uniform)
+    const uint32_t lo = (code & 1) ? B.e[1] : B.e[0];
+    const uint32_t hi = (code & 1) ? B.e[3] : B.e[2];
+    uint32_t eq       = (code & 2) ? hi : lo;
+    const uint32_t xv = eq | B.mv;
+    if (hin < 0)
+        eq |= lane0bit;
+    // (eq & pv) + pv over the whole block: carry lookahead on ballot masks
+    const uint32_t a = eq & B.pv;
+    uint32_t s;
+    const bool ov     = __builtin_add_overflow(a, B.pv, &s);
+    const uint64_t G  = __builtin_amdgcn_ballot_w64(ov) & B.act;
+    const uint64_t P  = __builtin_amdgcn_ballot_w64(s == 0xffffffffu) & B.act;
+    const uint64_t GP = G | P;
+    const uint64_t C  = ((GP + G) ^ GP ^ G);
+    s += mask_bit(C, hisel, lane);
+    const uint32_t xh = (s ^ B.pv) | eq;
+    uint32_t ph       = B.mv | ~(xh | B.pv);
+    uint32_t mh       = B.pv & xh;
+    if constexpr (OWN)
+        *own = int((ph >> own_hb) & 1u) - int((mh >> own_hb) & 1u);
+    int hout;
+    const uint64_t PH = __builtin_amdgcn_ballot_w64((ph >> 31) != 0u);
+    const uint64_t MH = __builtin_amdgcn_ballot_w64((mh >> 31) != 0u);
+    if (last)
+    {
+        const uint32_t phl = uniu(__builtin_amdgcn_readlane(int(ph), ll));
+        const uint32_t mhl = uniu(__builtin_amdgcn_readlane(int(mh), ll));
+        hout               = int((phl >> hb) & 1u) - int((mhl >> hb) & 1u);
+    }
+    else
+        hout = int((PH >> 63) & 1u) - int((MH >> 63) & 1u);
+    ph = (ph << 1) | mask_bit(PH << 1, hisel, lane);
+    mh = (mh << 1) | mask_bit(MH << 1, hisel, lane);
+    if (hin > 0)
+        ph |= lane0bit;
+    if (hin < 0)
+        mh |= lane0bit;
+    B.pv = mh | ~(xv | ph);
+    B.mv = ph & xv;
+    return hout;
+}
+
+// Myers sweep of query rows [qb, qe) (reversed: rows qe-1 down to qb) over the
+// target columns [tb, te) (reversed: te-1 down to tb); on_col(t, D(m, t)) for
+// t = 0..T (myers_compute_scores with full_score_matrix = false, :272-370).
+template <typename OnCol>
+__device__ void myers_sweep(const GWAMD_LDS uint32_t* pat, int pat_words, int Q, int qb, int qe, bool rev,
+                            const GWAMD_LDS uint8_t* tgt, int tb, int te, int lane, OnCol&& on_col)
+{
+    const int m      = qe - qb;
+    const int nwords = (m + kWordBits - 1) / kWordBits;
+    const int nch    = uni((nwords + kWave - 1) / kWave);
+    const int off    = rev ? Q - qe : qb;
+    const int pbase  = rev ? 4 : 0;
+    const int lw     = nwords - 1;
+    const int lc     = lw / kWave;
+    const int ll     = lw % kWave;
+    const int hb     = (m - 1) % kWordBits;
+    const uint32_t hisel    = lane >= 32 ? 1u : 0u;
+    const uint32_t lane0bit = lane == 0 ? 1u : 0u;
+    MyersBlock B[kMaxChunks];
+#pragma unroll
+    for (int c = 0; c < kMaxChunks; c++)
+    {
+        const int w      = c * kWave + lane;
+        const bool valid = c < nch && w < nwords;
+#pragma unroll
+        for (int L = 0; L < 4; L++)
+            B[c].e[L] = valid ? seg_pattern(pat, pat_words, off, w, pbase + L) : 0u;
+        B[c].pv  = ~0u;
+        B[c].mv  = 0u;
+        B[c].act = __builtin_amdgcn_ballot_w64(valid);
+    }
+    const int T = te - tb;
+    int score   = m;
+    on_col(0, score);
+    int tv = 0;
+    for (int t = 1; t <= T; t++)
+    {
+        const int tl = (t - 1) & (kWave - 1);
+        if (tl == 0)
+        {
+            // next 64 target characters, one per lane
+            const int idx = t - 1 + lane;
+            tv            = idx < T ? int(tgt[rev ? te - 1 - idx : tb + idx]) : 0;
+        }
+        const int code = letter(uni(__builtin_amdgcn_readlane(tv, tl)));
+        int h          = 1; // top row 0, 1, 2, ...: +1 into the first block
+#pragma unroll
+        for (int c = 0; c < kMaxChunks; c++)
+        {
+            if (c < nch)
+                h = myers_block_step(B[c], code, h, c == lc, ll, hb, lane, hisel, lane0bit);
+        }
+        score += h;
+        on_col(t, score);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Full-Myers base case of a segment shorter than 63 rows (one 64-bit word,
+// wave-uniform): column state into `leaf` (LDS or HBM), then the backtrace
+// (hirschberg_myers_compute_path / append_myers_backtrace, :372-392, :100-160).
+template <typename LeafPtr64, typename LeafPtr32>
+__device__ int leaf_full_myers(const GWAMD_LDS uint32_t* pat, int pat_words, int qb, int qe,
+                               const GWAMD_LDS uint8_t* tgt, int tb, int te, LeafPtr64 lpv, LeafPtr64 lmv,
+                               LeafPtr32 lsc, int8_t* path, int lane)
+{
+    const int m          = qe - qb;
+    const int T          = te - tb;
+    const uint64_t full  = (uint64_t(1) << m) - 1;
+    // segment patterns as one 64-bit word per letter
+    uint64_t e[4];
+    {
+        const int k  = qb >> 5;
+        const int sh = qb & 31;
+#pragma unroll
+        for (int L = 0; L < 4; L++)
+        {
+            const uint64_t w0 = k < pat_words ? pat[k * 8 + L] : 0u;
+            const uint64_t w1 = k + 1 < pat_words ? pat[(k + 1) * 8 + L] : 0u;
+            const uint64_t w2 = k + 2 < pat_words ? pat[(k + 2) * 8 + L] : 0u;
+            uint64_t r        = (w0 | (w1 << 32)) >> sh;
+            if (sh != 0)
+                r |= w2 << (64 - sh);
+            e[L] = uni64(r & full);
+        }
+    }
+    uint64_t pv = full, mv = 0;
+    int score   = m;
+    if (lane == 0)
+    {
+        lpv[0] = pv;
+        lmv[0] = mv;
+        lsc[0] = score;
+    }
+    for (int t = 1; t <= T; t++)
+    {
+        const int code    = letter(uni(int(tgt[tb + t - 1])));
+        const uint64_t lo = (code & 1) ? e[1] : e[0];
+        const uint64_t hi = (code & 1) ? e[3] : e[2];
+        const uint64_t eq = (code & 2) ? hi : lo;
+        const uint64_t xv = eq | mv;
+        const uint64_t xh = (((eq & pv) + pv) ^ pv) | eq;
+        uint64_t ph       = mv | ~(xh | pv);
+        uint64_t mh       = pv & xh;
+        score += int((ph >> (m - 1)) & 1u) - int((mh >> (m - 1)) & 1u);
+        ph = (ph << 1) | 1u;
+        mh = mh << 1;
+        pv = (mh | ~(xv | ph)) & full;
+        mv = (ph & xv) & full;
+        if (lane == 0)
+        {
+            lpv[t] = pv;
+            lmv[t] = mv;
+            lsc[t] = score;
+        }
+    }
+    __threadfence_block(); // the HBM variant: lane 0's stores before the wave's loads
+    wave_sync();
+    // D(i, j) = D(m, j) - sum of vertical deltas of rows i+1..m
+    auto D = [&](int i, int j) -> int {
+        if (i == 0)
+            return j;
+        const uint64_t hm = full & ~((uint64_t(1) << i) - 1);
+        const uint64_t p  = uni64(lpv[j]);
+        const uint64_t n  = uni64(lmv[j]);
+        return uni(lsc[j]) - __builtin_popcountll(p & hm) + __builtin_popcountll(n & hm);
+    };
+    int i = m, j = T, pos = 0;
+    int s = D(i, j);
+    while (i > 0 && j > 0)
+    {
+        const int above = D(i - 1, j);
+        const int diag  = D(i - 1, j - 1);
+        const int left  = D(i, j - 1);
+        int8_t r;
+        if (left + 1 == s)
+        {
+            r = kInsertion;
+            s = left;
+            --j;
+        }
+        else if (above + 1 == s)
+        {
+            r = kDeletion;
+            s = above;
+            --i;
+        }
+        else
+        {
+            r = diag == s ? kMatch : kMismatch;
+            s = diag;
+            --i;
+            --j;
+        }
+        if (lane == 0)
+            path[pos] = r;
+        ++pos;
+    }
+    for (int k = lane; k < i; k += kWave)
+        path[pos + k] = kDeletion;
+    pos += i;
+    for (int k = lane; k < j; k += kWave)
+        path[pos + k] = kInsertion;
+    pos += j;
+    return pos;
+}
+
+struct Range
+{
+    int32_t qb, qe, tb, te;
+};
+
+__device__ __forceinline__ void put_range(GWAMD_LDS Range* p, int qb, int qe, int tb, int te)
+{
+    p->qb = qb;
+    p->qe = qe;
+    p->tb = tb;
+    p->te = te;
+}
+
+// ---------------------------------------------------------------------------
+// Hirschberg + Myers (hirschberg_myers, :569-638), one wave per pair.
+__global__ void __launch_bounds__(kWave) hm_kernel(Args a)
+{
+    extern __shared__ __align__(16) uint8_t lds[];
+    const int lane                  = threadIdx.x;
+    GWAMD_LDS uint8_t* base         = (GWAMD_LDS uint8_t*)(lds);
+    GWAMD_LDS uint8_t* tgt          = base + a.lds_target_off;
+    GWAMD_LDS uint32_t* pat         = (GWAMD_LDS uint32_t*)(base + a.lds_pat_off);
+    GWAMD_LDS uint8_t* scratch      = base + a.lds_scratch_off;
+    GWAMD_LDS uint16_t* revs        = (GWAMD_LDS uint16_t*)(scratch);
+    GWAMD_LDS Range* stack          = (GWAMD_LDS Range*)(base + a.lds_stack_off);
+    uint8_t* ws                     = a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes);
+
+    for (int idx = blockIdx.x; idx < a.n; idx += gridDim.x)
+    {
+        const char* q  = a.seqs + size_t(2 * idx) * a.stride;
+        const char* tg = a.seqs + size_t(2 * idx + 1) * a.stride;
+        const int Q    = uni(a.lens[2 * idx]);
+        const int T    = uni(a.lens[2 * idx + 1]);
+        int8_t* path   = a.paths + size_t(idx) * a.max_path_length;
+        for (int k = lane; k < T; k += kWave)
+            tgt[k] = uint8_t(tg[k]);
+        build_patterns(pat, q, Q, lane);
+        const int pat_words = (Q + kWordBits - 1) / kWordBits;
+        wave_sync();
+
+        int sp = 0;
+        if (lane == 0)
+            put_range(stack, 0, Q, 0, T);
+        sp           = 1;
+        bool success = true;
+        int len      = 0;
+        while (success && sp > 0)
+        {
+            wave_sync();
+            --sp;
+            const Range e = Range{uni(stack[sp].qb), uni(stack[sp].qe), uni(stack[sp].tb), uni(stack[sp].te)};
+            wave_sync();
+            const int m  = e.qe - e.qb;
+            const int Ts = e.te - e.tb;
+            if (Ts == 0)
+            {
+                for (int k = lane; k < m; k += kWave)
+                    path[len + k] = kDeletion;
+                len += m;
+            }
+            else if (m == 0)
+            {
+                for (int k = lane; k < Ts; k += kWave)
+                    path[len + k] = kInsertion;
+                len += Ts;
+            }
+            else if (m == 1)
+            {
+                // last target position equal to the query character (:477-508)
+                const char c = q[e.qb];
+                int found    = -1;
+                for (int k0 = 0; k0 < Ts && found < 0; k0 += kWave)
+                {
+                    const int k       = k0 + lane;
+                    const bool hit    = k < Ts && char(tgt[e.te - 1 - k]) == c;
+                    const uint64_t hm = __builtin_amdgcn_ballot_w64(hit);
+                    if (hm != 0)
+                        found = k0 + __builtin_ctzll(hm);
+                }
+                for (int k = lane; k < Ts; k += kWave)
+                {
+                    int8_t st = k == found ? kMatch : kInsertion;
+                    if (found < 0 && k == Ts - 1)
+                        st = kMismatch;
+                    path[len + k] = st;
+                }
+                len += Ts;
+            }
+            else
+            {
+                const int nw = (m + kWordBits - 1) / kWordBits;
+                if (m < kFullMyers && int64_t(Ts + 1) * nw <= a.max_matrix_elems)
+                {
+                    if (Ts + 1 <= kLeafCols)
+                    {
+                        GWAMD_LDS uint64_t* lpv = (GWAMD_LDS uint64_t*)(scratch);
+                        GWAMD_LDS uint64_t* lmv = lpv + kLeafCols;
+                        GWAMD_LDS int32_t* lsc  = (GWAMD_LDS int32_t*)(lmv + kLeafCols);
+                        len += leaf_full_myers(pat, pat_words, e.qb, e.qe, tgt, e.tb, e.te, lpv, lmv, lsc, path + len,
+                                               lane);
+                    }
+                    else
+                    {
+                        uint64_t* lpv = reinterpret_cast<uint64_t*>(ws);
+                        uint64_t* lmv = lpv + (a.stride + 1);
+                        int32_t* lsc  = reinterpret_cast<int32_t*>(lmv + (a.stride + 1));
+                        len += leaf_full_myers(pat, pat_words, e.qb, e.qe, tgt, e.tb, e.te, lpv, lmv, lsc, path + len,
+                                               lane);
+                    }
+                    wave_sync();
+                    continue;
+                }
+                // split the query at its middle, the target at the best column
+                const int qm = e.qb + m / 2;
+                // reverse half: rev[t] = D(q[qm, qe), target suffix of length t)
+                uint32_t acc = 0;
+                myers_sweep(pat, pat_words, Q, qm, e.qe, true, tgt, e.tb, e.te, lane, [&](int t, int sc) {
+                    const int tl = t & (kWave - 1);
+                    if (lane == tl)
+                        acc = uint32_t(sc);
+                    if (tl == kWave - 1 || t == Ts)
+                    {
+                        const int t0 = t - tl;
+                        if (lane <= tl)
+                            revs[t0 + lane] = uint16_t(acc);
+                    }
+                });
+                wave_sync();
+                int best = INT_MAX, bkey = INT_MAX, bt = 0;
+                int rv   = 0;
+                myers_sweep(pat, pat_words, Q, e.qb, qm, false, tgt, e.tb, e.te, lane, [&](int t, int sc) {
+                    const int tl = t & (kWave - 1);
+                    if (tl == 0)
+                    {
+                        const int x = t + lane;
+                        rv          = x <= Ts ? int(revs[Ts - x]) : 0;
+                    }
+                    const int sum = sc + uni(__builtin_amdgcn_readlane(rv, tl));
+                    const int key = int(__builtin_bitreverse32(uint32_t(t) & 31u) >> 27);
+                    if (sum < best || (sum == best && key < bkey))
+                    {
+                        best = sum;
+                        bkey = key;
+                        bt   = t;
+                    }
+                });
+                const int tm = e.tb + bt;
+                wave_sync();
+                if (sp < kStackSize)
+                {
+                    if (lane == 0)
+                        put_range(stack + sp, e.qb, qm, e.tb, tm);
+                    ++sp;
+                }
+                else
+                    success = false;
+                if (success)
+                {
+                    if (sp < kStackSize)
+                    {
+                        if (lane == 0)
+                            put_range(stack + sp, qm, e.qe, tm, e.te);
+                        ++sp;
+                    }
+                    else
+                        success = false;
+                }
+            }
+        }
+        if (lane == 0)
+            a.path_len[idx] = success ? len : 0;
+        wave_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Full Myers (myers_compute_score_matrix_kernel + myers_backtrace,
+// myers_gpu.cu:95-375): per (word, column) pv, mv and the score of the word's
+// last row in the workgroup's HBM slot, then the backtrace on the wave.
+__global__ void __launch_bounds__(kWave) myers_kernel(Args a)
+{
+    extern __shared__ __align__(16) uint8_t lds[];
+    const int lane          = threadIdx.x;
+    GWAMD_LDS uint8_t* base = (GWAMD_LDS uint8_t*)(lds);
+    GWAMD_LDS uint8_t* tgt  = base + a.lds_target_off;
+    GWAMD_LDS uint32_t* pat = (GWAMD_LDS uint32_t*)(base + a.lds_pat_off);
+    uint8_t* ws             = a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes);
+
+    for (int idx = blockIdx.x; idx < a.n; idx += gridDim.x)
+    {
+        const char* q  = a.seqs + size_t(2 * idx) * a.stride;
+        const char* tg = a.seqs + size_t(2 * idx + 1) * a.stride;
+        const int Q    = uni(a.lens[2 * idx]);
+        const int T    = uni(a.lens[2 * idx + 1]);
+        int8_t* path   = a.paths + size_t(idx) * a.max_path_length;
+        for (int k = lane; k < T; k += kWave)
+            tgt[k] = uint8_t(tg[k]);
+        build_patterns(pat, q, Q, lane);
+        const int nw = (Q + kWordBits - 1) / kWordBits;
+        wave_sync();
+        uint32_t* wpv = reinterpret_cast<uint32_t*>(ws);
+        uint32_t* wmv = wpv + size_t(nw) * (T + 1);
+        int32_t* wsc  = reinterpret_cast<int32_t*>(wmv + size_t(nw) * (T + 1));
+        if (Q > 0)
+        {
+            const int nch           = uni((nw + kWave - 1) / kWave);
+            const int lw            = nw - 1;
+            const int lc            = lw / kWave;
+            const int ll            = lw % kWave;
+            const int hb            = (Q - 1) % kWordBits;
+            const uint32_t hisel    = lane >= 32 ? 1u : 0u;
+            const uint32_t lane0bit = lane == 0 ? 1u : 0u;
+            MyersBlock B[kMaxChunks];
+            int score[kMaxChunks];
+#pragma unroll
+            for (int c = 0; c < kMaxChunks; c++)
+            {
+                const int w      = c * kWave + lane;
+                const bool valid = c < nch && w < nw;
+#pragma unroll
+                for (int L = 0; L < 4; L++)
+                    B[c].e[L] = valid ? seg_pattern(pat, nw, 0, w, L) : 0u;
+                B[c].pv  = ~0u;
+                B[c].mv  = 0u;
+                B[c].act = __builtin_amdgcn_ballot_w64(valid);
+                score[c] = min((w + 1) * kWordBits, Q); // myers_gpu.cu:341
+                if (valid)
+                {
+                    wpv[w] = ~0u;
+                    wmv[w] = 0u;
+                    wsc[w] = score[c];
+                }
+            }
+            int tv = 0;
+            for (int t = 1; t <= T; t++)
+            {
+                const int tl = (t - 1) & (kWave - 1);
+                if (tl == 0)
+                {
+                    const int x = t - 1 + lane;
+                    tv          = x < T ? int(tgt[x]) : 0;
+                }
+                const int code = letter(uni(__builtin_amdgcn_readlane(tv, tl)));
+                int h          = 1;
+#pragma unroll
+                for (int c = 0; c < kMaxChunks; c++)
+                {
+                    if (c < nch)
+                    {
+                        const int w = c * kWave + lane;
+                        int own     = 0;
+                        h = myers_block_step<true>(B[c], code, h, c == lc, ll, hb, lane, hisel, lane0bit,
+                                                   w == lw ? hb : 31, &own);
+                        score[c] += own;
+                        if (w < nw)
+                        {
+                            wpv[size_t(t) * nw + w] = B[c].pv;
+                            wmv[size_t(t) * nw + w] = B[c].mv;
+                            wsc[size_t(t) * nw + w] = score[c];
+                        }
+                    }
+                }
+            }
+        }
+        __threadfence_block();
+        wave_sync();
+        // backtrace (myers_backtrace, myers_gpu.cu:181-245)
+        const uint32_t last_mask = (Q % kWordBits) != 0 ? (1u << (Q % kWordBits)) - 1u : ~0u;
+        auto gms                 = [&](int i, int j) -> int {
+            const int wi     = (i - 1) / kWordBits;
+            const int bi     = (i - 1) % kWordBits;
+            uint32_t mask    = (~1u) << bi;
+            if (wi == nw - 1)
+                mask &= last_mask;
+            const size_t o   = size_t(j) * nw + wi;
+            const uint32_t p = uniu(wpv[o]);
+            const uint32_t n = uniu(wmv[o]);
+            return uni(wsc[o]) - __builtin_popcount(mask & p) + __builtin_popcount(mask & n);
+        };
+        int i = Q, j = T, pos = 0;
+        int s = Q > 0 ? uni(wsc[size_t(T) * nw + (nw - 1)]) : 0;
+        while (i > 0 && j > 0)
+        {
+            const int above = i == 1 ? j : gms(i - 1, j);
+            const int diag  = i == 1 ? j - 1 : gms(i - 1, j - 1);
+            const int left  = gms(i, j - 1);
+            int8_t r;
+            if (left + 1 == s)
+            {
+                r = kInsertion;
+                s = left;
+                --j;
+            }
+            else if (above + 1 == s)
+            {
+                r = kDeletion;
+                s = above;
+                --i;
+            }
+            else
+            {
+                r = diag == s ? kMatch : kMismatch;
+                s = diag;
+                --i;
+                --j;
+            }
+            if (lane == 0)
+                path[pos] = r;
+            ++pos;
+        }
+        for (int k = lane; k < i; k += kWave)
+            path[pos + k] = kDeletion;
+        pos += i;
+        for (int k = lane; k < j; k += kWave)
+            path[pos + k] = kInsertion;
+        pos += j;
+        if (lane == 0)
+            a.path_len[idx] = pos;
+        wave_sync();
+    }
+}
+
+} // namespace aln
+} // namespace gwamd
+
+extern "C" hipError_t gwamd_internal_align_launch(const gwamd::aln::Args* a, int algo, int grid, hipStream_t stream)
+{
+    using namespace gwamd::aln;
+    if (a->n <= 0)
+        return hipSuccess;
+    if (algo == 0)
+        hipLaunchKernelGGL(hm_kernel, dim3(grid), dim3(kWave), size_t(a->lds_bytes), stream, *a);
+    else
+        hipLaunchKernelGGL(myers_kernel, dim3(grid), dim3(kWave), size_t(a->lds_bytes), stream, *a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t gwamd_internal_align_occupancy(int algo, int lds_bytes, int* blocks_per_cu)
+{
+    using namespace gwamd::aln;
+    if (algo == 0)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, hm_kernel, kWave, size_t(lds_bytes));
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, myers_kernel, kWave, size_t(lds_bytes));
+}

@@ -11,6 +11,7 @@
 #include <claraparabricks/genomeworks/cudapoa/batch.hpp>
 
 #include "gwamd_cudapoa.h"
+#include "host_common.hpp"
 #include "poa_common.hpp"
 
 #include <hip/hip_runtime.h>
@@ -34,33 +35,11 @@ namespace genomeworks
 namespace cudapoa
 {
 
+using gwamd::host::PinnedBuf;
+using gwamd::host::ScopedDevice;
+
 namespace
 {
-
-#define GWAMD_HIP_CHECK(expr)                                                                                  \
-    do                                                                                                         \
-    {                                                                                                          \
-        hipError_t e__ = (expr);                                                                               \
-        if (e__ != hipSuccess)                                                                                 \
-            throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e__) + " at " #expr);       \
-    } while (0)
-
-struct ScopedDevice
-{
-    int prev = -1;
-    explicit ScopedDevice(int dev)
-    {
-        GWAMD_HIP_CHECK(hipGetDevice(&prev));
-        if (prev != dev)
-            GWAMD_HIP_CHECK(hipSetDevice(dev));
-    }
-    ~ScopedDevice()
-    {
-        int cur = -1;
-        if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0)
-            (void)hipSetDevice(prev);
-    }
-};
 
 // use32bitScore / use32bitSize (cudapoa_limits.hpp:28-53)
 bool use32bit_score(const BatchSize& bs, int16_t gap, int16_t mismatch, int16_t match)
@@ -114,42 +93,6 @@ struct DevBuf
 {
     void* p = nullptr;
     size_t n = 0;
-};
-
-class PinnedBuf
-{
-public:
-    ~PinnedBuf() { release(); }
-    void reserve(size_t bytes, hipStream_t stream)
-    {
-        if (bytes <= cap_)
-            return;
-        size_t ncap = std::max(bytes, cap_ * 2);
-        void* np    = nullptr;
-        GWAMD_HIP_CHECK(hipHostMalloc(&np, ncap, hipHostMallocDefault));
-        if (p_)
-        {
-            // an async H2D copy may still read the old buffer
-            GWAMD_HIP_CHECK(hipStreamSynchronize(stream));
-            std::memcpy(np, p_, used_);
-            (void)hipHostFree(p_);
-        }
-        p_   = np;
-        cap_ = ncap;
-    }
-    template <typename T>
-    T* as() const { return static_cast<T*>(p_); }
-    size_t used_ = 0;
-
-private:
-    void release()
-    {
-        if (p_)
-            (void)hipHostFree(p_);
-        p_ = nullptr;
-    }
-    void* p_    = nullptr;
-    size_t cap_ = 0;
 };
 
 } // namespace
@@ -811,29 +754,28 @@ namespace cp = claraparabricks::genomeworks::cudapoa;
 
 namespace
 {
-thread_local std::string g_last_error;
 
 template <typename F>
 int32_t guarded(F&& f)
 {
     try
     {
-        g_last_error.clear();
+        gwamd::host::last_error().clear();
         return f();
     }
     catch (const std::invalid_argument& e)
     {
-        g_last_error = e.what();
+        gwamd::host::last_error() = e.what();
         return GWAMD_E_INVALID_ARGUMENT;
     }
     catch (const std::runtime_error& e)
     {
-        g_last_error = e.what();
+        gwamd::host::last_error() = e.what();
         return std::string(e.what()).rfind("HIP error", 0) == 0 ? GWAMD_E_HIP : GWAMD_E_RUNTIME;
     }
     catch (const std::exception& e)
     {
-        g_last_error = e.what();
+        gwamd::host::last_error() = e.what();
         return GWAMD_E_RUNTIME;
     }
 }
@@ -874,7 +816,7 @@ struct gwamd_poa_batch
 
 extern "C" {
 
-const char* gwamd_last_error(void) { return g_last_error.c_str(); }
+const char* gwamd_last_error(void) { return gwamd::host::last_error().c_str(); }
 
 int32_t gwamd_poa_batch_size_init(gwamd_poa_batch_size* out, int32_t max_seq_sz, int32_t max_seq_per_poa,
                                   int32_t band_width)

@@ -62,3 +62,12 @@ def pairs(first_seed, n, target_len, query_cap, max_mut, max_ins, max_del):
     qs = [q[i * stride:i * stride + ql[i]].tobytes() for i in range(n)]
     ts = [t[i * stride:i * stride + tl[i]].tobytes() for i in range(n)]
     return qs, ts
+
+
+def aligner_pairs(first_seed, n, length=5000, errors=166):
+    """per pair i, minstd_rand(first_seed + i); target =
+    generate_random_genome(length); query = generate_random_sequence(target,
+    errors, errors, errors) truncated to length (cudaaligner/benchmarks/main.cpp:109-115).
+    Returns a list of (query, target) str pairs."""
+    qs, ts = pairs(first_seed, n, length, length, errors, errors, errors)
+    return [(q.decode(), t.decode()) for q, t in zip(qs, ts)]

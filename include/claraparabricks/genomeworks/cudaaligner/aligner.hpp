@@ -1,0 +1,51 @@
+// MI355X drop-in for cudaaligner/include/claraparabricks/genomeworks/cudaaligner/aligner.hpp.
+// The only signature change: hipStream_t instead of cudaStream_t.
+#pragma once
+
+#include <claraparabricks/genomeworks/cudaaligner/alignment.hpp>
+#include <claraparabricks/genomeworks/cudaaligner/cudaaligner.hpp>
+#include <claraparabricks/genomeworks/utils/allocator.hpp>
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+namespace claraparabricks
+{
+namespace genomeworks
+{
+namespace cudaaligner
+{
+
+/// Batched aligner (aligner.hpp:42-77).
+class Aligner
+{
+public:
+    virtual ~Aligner() = default;
+    /// Launch alignment of every pair added so far (asynchronous).
+    virtual StatusType align_all() = 0;
+    /// Wait for align_all() and fill the Alignment objects.
+    virtual StatusType sync_alignments() = 0;
+    /// Copy a pair into the batch (optionally reverse-complemented).
+    virtual StatusType add_alignment(const char* query, int32_t query_length, const char* target,
+                                     int32_t target_length, bool reverse_complement_query = false,
+                                     bool reverse_complement_target = false) = 0;
+    virtual const std::vector<std::shared_ptr<Alignment>>& get_alignments() const = 0;
+    virtual void reset() = 0;
+};
+
+/// Global aligner (Hirschberg + Myers) on device_id / stream (aligner.hpp:90).
+std::unique_ptr<Aligner> create_aligner(int32_t max_query_length, int32_t max_target_length,
+                                        int32_t max_alignments, AlignmentType type,
+                                        DefaultDeviceAllocator allocator, hipStream_t stream, int32_t device_id);
+
+/// Same, with the caching budget of the reference's allocator (aligner.hpp:103).
+std::unique_ptr<Aligner> create_aligner(int32_t max_query_length, int32_t max_target_length,
+                                        int32_t max_alignments, AlignmentType type, hipStream_t stream,
+                                        int32_t device_id, int64_t max_device_memory_allocator_caching_size = -1);
+
+} // namespace cudaaligner
+} // namespace genomeworks
+} // namespace claraparabricks

@@ -1,0 +1,93 @@
+/*
+ * gwamd_cudaaligner.h -- C ABI of the MI355X global aligner (libgwamd.so).
+ *
+ * Plain C: opaque handle, plain pointers and sizes.  Each entry point replaces
+ * one method of the reference's C++ aligner API, which is what the reference's
+ * own FFI (pygenomeworks/genomeworks/cudaaligner/cudaaligner.pxd) binds:
+ *
+ *   gwamd_aligner_create          create_aligner(...)                      aligner.hpp:90,103
+ *                                 (algorithm 1: AlignerGlobalMyers,        aligner_global_myers.hpp:28)
+ *   gwamd_aligner_destroy         ~Aligner                                 aligner.hpp:45
+ *   gwamd_aligner_add_alignment   Aligner::add_alignment                   aligner.hpp:70-71
+ *   gwamd_aligner_align_all       Aligner::align_all                       aligner.hpp:55
+ *   gwamd_aligner_sync_alignments Aligner::sync_alignments                 aligner.hpp:61
+ *   gwamd_aligner_num_alignments  get_alignments().size()                  aligner.hpp:76
+ *   gwamd_aligner_get_alignment   Alignment::get_alignment / get_status    alignment.hpp:72-80
+ *   gwamd_aligner_get_sequences   Alignment::get_query/target_sequence     alignment.hpp:53-56
+ *   gwamd_aligner_get_cigar       Alignment::convert_to_cigar              alignment.hpp:62
+ *   gwamd_aligner_reset           Aligner::reset                           aligner.hpp:79
+ *
+ * Extra entry points (bench.py): split align_all into upload / launch /
+ * download and read the raw device paths.
+ *
+ * Error convention: StatusType values (cudaaligner.hpp:27-35) >= 0, or a
+ * negative GWAMD_E_* code where the reference throws (gwamd_last_error()).
+ */
+#ifndef GWAMD_CUDAALIGNER_H
+#define GWAMD_CUDAALIGNER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef GWAMD_E_INVALID_ARGUMENT
+#define GWAMD_E_INVALID_ARGUMENT (-1)
+#define GWAMD_E_RUNTIME (-2)
+#define GWAMD_E_HIP (-3)
+#endif
+
+#define GWAMD_ALIGNER_HIRSCHBERG_MYERS 0 /* create_aligner(global_alignment) */
+#define GWAMD_ALIGNER_MYERS 1            /* AlignerGlobalMyers (full matrix) */
+
+typedef struct gwamd_aligner gwamd_aligner;
+
+const char* gwamd_last_error(void);
+
+/* alignment_type: 0 = global_alignment (the only type the reference
+ * implements); stream: a hipStream_t (NULL = default stream). */
+int32_t gwamd_aligner_create(gwamd_aligner** out, int32_t max_query_length, int32_t max_target_length,
+                             int32_t max_alignments, int32_t alignment_type, int32_t algorithm, void* stream,
+                             int32_t device_id, int64_t max_device_memory_allocator_caching_size);
+void gwamd_aligner_destroy(gwamd_aligner* aligner);
+
+int32_t gwamd_aligner_add_alignment(gwamd_aligner* aligner, const char* query, int32_t query_length,
+                                    const char* target, int32_t target_length, int32_t reverse_complement_query,
+                                    int32_t reverse_complement_target);
+int32_t gwamd_aligner_align_all(gwamd_aligner* aligner);
+int32_t gwamd_aligner_sync_alignments(gwamd_aligner* aligner);
+int32_t gwamd_aligner_num_alignments(const gwamd_aligner* aligner);
+
+/* Alignment i after sync: states (AlignmentState, start -> end) into
+ * states[0..cap); returns the alignment length (states untouched if cap is
+ * too small); *status receives the alignment's StatusType. */
+int32_t gwamd_aligner_get_alignment(gwamd_aligner* aligner, int32_t i, int8_t* states, int32_t cap,
+                                    int32_t* status);
+/* Query and target of alignment i as stored by add_alignment (reverse-
+ * complemented when requested): Alignment::get_query_sequence /
+ * get_target_sequence (alignment.hpp:53-56).  Pointers stay valid until reset. */
+int32_t gwamd_aligner_get_sequences(gwamd_aligner* aligner, int32_t i, const char** query, int32_t* query_length,
+                                    const char** target, int32_t* target_length);
+/* CIGAR of alignment i, NUL-terminated if it fits; returns its length. */
+int32_t gwamd_aligner_get_cigar(gwamd_aligner* aligner, int32_t i, char* buf, int32_t cap);
+void gwamd_aligner_reset(gwamd_aligner* aligner);
+
+/* bench.py helpers: align_all == upload + launch + download. */
+int32_t gwamd_aligner_upload(gwamd_aligner* aligner);
+int32_t gwamd_aligner_launch(gwamd_aligner* aligner);
+int32_t gwamd_aligner_download(gwamd_aligner* aligner);
+int32_t gwamd_aligner_synchronize(gwamd_aligner* aligner);
+/* Raw device results (copied to host by download): path i (emitted end ->
+ * start) at paths + i * stride, length lengths[i]. */
+int32_t gwamd_aligner_get_paths(gwamd_aligner* aligner, const int8_t** paths, const int32_t** lengths,
+                                int32_t* stride);
+/* Resident workgroups of the kernel (persistent grid) and device bytes. */
+int32_t gwamd_aligner_get_config(const gwamd_aligner* aligner, int32_t* grid, int64_t* device_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GWAMD_CUDAALIGNER_H */

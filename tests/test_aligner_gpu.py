@@ -1,0 +1,159 @@
+"""GPU parity of the HIP global aligners (through the C ABI via
+CudaAlignerBatch) against the aligner oracle and the reference's own KATs."""
+import json
+import os
+import random
+
+import pytest
+
+from claragenomicsanalysis_amd import synth
+from claragenomicsanalysis_amd.cudaaligner import CudaAlignerBatch
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "aligner_kat.json")))
+ALGOS = [("hirschberg_myers", oracle.ALIGN_HM), ("myers", oracle.ALIGN_MYERS)]
+
+
+def run(pairs, max_q=None, max_t=None, algorithm="hirschberg_myers", rc=None):
+    mq = max_q if max_q is not None else max(1, max(len(q) for q, _ in pairs))
+    mt = max_t if max_t is not None else max(1, max(len(t) for _, t in pairs))
+    b = CudaAlignerBatch(mq, mt, len(pairs), algorithm=algorithm)
+    for k, (q, t) in enumerate(pairs):
+        flags = rc[k] if rc else (False, False)
+        assert b.add_alignment(q, t, *flags) == 0
+    b.align_all()
+    return b, b.get_alignments()
+
+
+def states(al):
+    inv = {"m": 0, "mm": 1, "i": 2, "d": 3}
+    return [inv[s] for s in al.alignment]
+
+
+@pytest.mark.parametrize("case", GOLD["cigar"], ids=lambda c: c["source"])
+@pytest.mark.parametrize("algo", ["hirschberg_myers", "myers"])
+def test_cigar_kats(case, algo):
+    if algo == "myers" and "myers" not in case["algorithms"]:
+        pytest.skip("KAT not stated for full Myers")
+    pairs = [(p["query"], p["target"]) for p in case["pairs"]]
+    _, al = run(pairs, case["max_query_length"], case["max_target_length"], algo)
+    assert [a.cigar for a in al] == [p["cigar"] for p in case["pairs"]]
+    assert all(a.status == 0 and a.alignment_type == "global" for a in al)
+
+
+def _rand_pairs(seed, n, lo, hi, err):
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        t = "".join(rng.choice("ACGT") for _ in range(rng.randrange(lo, hi + 1)))
+        q = list(t)
+        for _ in range(int(len(t) * err)):
+            k, p = rng.randrange(3), rng.randrange(len(q) + 1)
+            if k == 0 and p < len(q):
+                q[p] = rng.choice("ACGT")
+            elif k == 1:
+                q.insert(p, rng.choice("ACGT"))
+            elif p < len(q):
+                del q[p]
+        out.append(("".join(q), t))
+    return out
+
+
+@pytest.mark.parametrize("algo,oalgo", ALGOS)
+@pytest.mark.parametrize("lo,hi,err", [(1, 40, 0.2), (50, 200, 0.1), (300, 1200, 0.08), (2000, 4000, 0.05)])
+def test_random_pairs_match_oracle(algo, oalgo, lo, hi, err):
+    pairs = _rand_pairs(lo * 7 + hi, 24 if hi < 2000 else 6, lo, hi, err)
+    mq = max(len(q) for q, _ in pairs)
+    _, al = run(pairs, mq, max(len(t) for _, t in pairs), algo)
+    for (q, t), a in zip(pairs, al):
+        assert states(a) == oracle.align(q, t, oalgo, mq), (len(q), len(t))
+
+
+def test_config_d_pairs_match_oracle():
+    # SURVEY 8(d) config D shape: 5 kb target, ~10% difference (synthetic generator)
+    pairs = synth.aligner_pairs(1, 4, 5000)
+    _, al = run(pairs, 5000, 5000)
+    for (q, t), a in zip(pairs, al):
+        assert states(a) == oracle.align(q, t, oracle.ALIGN_HM, 5000)
+
+
+def test_unrelated_long_pairs_optimal():
+    # Test_AlignerGlobal.cpp:130-134 shape (random 4800 vs 5000, no CIGAR stated)
+    rng = random.Random(11)
+    pairs = [("".join(rng.choice("ACGT") for _ in range(4800)), "".join(rng.choice("ACGT") for _ in range(5000)))]
+    _, al = run(pairs, 5001, 5001)
+    q, t = pairs[0]
+    st = states(al[0])
+    assert st == oracle.align(q, t, oracle.ALIGN_HM, 5001)
+    assert sum(1 for s in st if s != 0) == oracle.edit_distance(q, t)
+
+
+@pytest.mark.parametrize("algo,oalgo", ALGOS)
+def test_edge_cases(algo, oalgo):
+    pairs = [("", "ACGT"), ("ACGT", ""), ("A", "T"), ("A", "TTTA"), ("G", "ACGTGT"), ("C", "C"),
+             ("ACGNNT", "ACGGGT"), ("acgt", "ACGT"), ("NNNN", "ACGT"), ("ACGT" * 20, "TTTT"),
+             ("T" * 70, "T" * 69 + "A"), ("", "")]
+    _, al = run(pairs, 80, 80, algo)
+    for (q, t), a in zip(pairs, al):
+        assert states(a) == oracle.align(q, t, oalgo, 80), (q, t)
+        assert a.query == q and a.target == t
+
+
+def test_wide_leaf_in_hbm():
+    # a base case (query < 63) over a target segment wider than the LDS leaf
+    # (512 columns): query 40 bases vs target 1500
+    rng = random.Random(5)
+    t = "".join(rng.choice("ACGT") for _ in range(1500))
+    q = t[700:740]
+    _, al = run([(q, t)], 5000, 5000)
+    assert states(al[0]) == oracle.align(q, t, oracle.ALIGN_HM, 5000)
+
+
+def test_reverse_complement_flags():
+    def rc(s):
+        return "".join({"A": "T", "T": "A", "C": "G", "G": "C"}.get(c, c) for c in reversed(s))
+    pairs = _rand_pairs(3, 4, 100, 300, 0.1)
+    flags = [(True, False), (False, True), (True, True), (False, False)]
+    _, al = run(pairs, 400, 400, rc=flags)
+    for (q, t), (fq, ft), a in zip(pairs, flags, al):
+        qq, tt = (rc(q) if fq else q), (rc(t) if ft else t)
+        assert a.query == qq and a.target == tt
+        assert states(a) == oracle.align(qq, tt, oracle.ALIGN_HM, 400)
+
+
+def test_add_alignment_status_codes():
+    # Test_AlignerGlobal.cpp:58-83
+    case = GOLD["add_alignment"]
+    b = CudaAlignerBatch(case["max_query_length"], case["max_target_length"], case["max_alignments"])
+    for q, t, want in case["calls"]:
+        assert b.add_alignment(q, t) == want
+    assert b.num_alignments() == case["final_count"]
+    b.align_all()
+    assert [a.cigar for a in b.get_alignments()] == [oracle.cigar(oracle.align("ATCG", "TACG", 0, 10))] * 5
+    b.reset()
+    assert b.get_alignments() == []
+
+
+@pytest.mark.parametrize("max_len,max_n,seq_len,n,ok", [(1000, 100, 10000, 10, False), (1000, 100, 100, 10, True),
+                                                        (100, 10, 100, 1000, False)])
+def test_various_arguments(max_len, max_n, seq_len, n, ok):
+    # test_cudaaligner_bindings.py:84-112
+    rng = random.Random(seq_len)
+    b = CudaAlignerBatch(max_len, max_len, max_n)
+    good = True
+    for _ in range(n):
+        s = "".join(rng.choice("ACGT") for _ in range(seq_len))
+        good &= b.add_alignment(s, s) == 0
+    b.align_all()
+    assert good is ok
+
+
+def test_invalid_construction():
+    with pytest.raises(RuntimeError):
+        CudaAlignerBatch(10, 10, 0)
+    with pytest.raises(RuntimeError):
+        CudaAlignerBatch(10, 10, 1, alignment_type="local")
+    with pytest.raises(ValueError):
+        CudaAlignerBatch(10, 10, 1, max_device_memory_allocator_caching_size=-2)
