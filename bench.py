@@ -28,6 +28,13 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
+ALIGNER_CONFIGS = {
+    # 100k pairs x 5 kb, ~10% difference; Hirschberg-Myers
+    # (create_aligner default) and, separately, full Myers
+    "D": dict(pairs=100000, length=5000, algorithm="hirschberg_myers"),
+    "D_myers": dict(pairs=100000, length=5000, algorithm="myers"),
+}
+
 CONFIGS = {
     # name: (backbone, reads, mut, ins, del, max_seq, banded, band_width, windows per GPU)
     "B": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=False, bw=256, windows=1024),
@@ -40,7 +47,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--config", default="B", choices=sorted(CONFIGS))
+    p.add_argument("--config", default="B", choices=sorted(CONFIGS) + sorted(ALIGNER_CONFIGS))
+    p.add_argument("--pairs", type=int, default=None, help="override aligner pairs per GPU")
     p.add_argument("--windows", type=int, default=None, help="override windows per GPU")
     p.add_argument("--cpu-sample", type=int, default=None, help="windows in the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true")
@@ -65,8 +73,115 @@ def cpu_model():
     return None
 
 
+def bench_aligner(args):
+    """Global alignments/s on this rank's pairs."""
+    cfg = dict(ALIGNER_CONFIGS[args.config])
+    if args.pairs:
+        cfg["pairs"] = args.pairs
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    torch.cuda.set_device(local_rank)
+    from claragenomicsanalysis_amd import synth
+    from claragenomicsanalysis_amd.cudaaligner import CudaAlignerBatch
+
+    n, L = cfg["pairs"], cfg["length"]
+    t0 = time.time()
+    qs, ts = synth.pairs(1 + rank * n, n, L, L, 166, 166, 166)
+    gen_s = time.time() - t0
+    stream = torch.cuda.Stream()
+    b = CudaAlignerBatch(L, L, n, stream=stream, algorithm=cfg["algorithm"])
+    for q, t in zip(qs, ts):
+        if b.add_alignment(q, t) != 0:
+            raise RuntimeError("add_alignment failed")
+    b.upload()
+    b.synchronize()
+    for _ in range(args.warmup):
+        b.launch()
+    b.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_start = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        b.launch()
+    ev1.record(stream)
+    b.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t_start
+    kernel_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
+    t_max = torch.tensor([wall], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    wall_max = float(t_max.item())
+    b.download()
+    b.synchronize()
+    paths, plen = b.raw_paths()
+    cells = sum(len(q) * len(t) for q, t in zip(qs, ts))
+    alg_bytes = sum(((len(q) + 31) // 32) * (len(t) + 1) * 12 for q, t in zip(qs, ts))
+    out = None
+    if rank == 0:
+        from oracle import oracle
+        k = min(8, n)
+        ok = True
+        algo = oracle.ALIGN_HM if cfg["algorithm"] == "hirschberg_myers" else oracle.ALIGN_MYERS
+        for i in range(k):
+            want = oracle.align(qs[i], ts[i], algo, L)
+            got = paths[i, :plen[i]][::-1].tolist()
+            ok = ok and got == want
+        parity = {"pairs_checked": k, "bit_exact_vs_oracle": bool(ok)}
+        cpu = None
+        if not args.no_cpu and world == 1:
+            th = cpu_threads()
+            ns = args.cpu_sample or min(n, max(th * 4, 16))
+            tc = time.perf_counter()
+            cres, used = oracle.align_batch(list(zip(qs[:ns], ts[:ns])), algo, L, th)
+            cpu_s = time.perf_counter() - tc
+            match = all(cres[i] == paths[i, :plen[i]][::-1].tolist() for i in range(ns))
+            cpu = {"value": round(ns / cpu_s, 3), "unit": "alignments/s", "cores": int(used), "kind": "port",
+                   "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+                   "sample": "first %d pairs of the same workload, oracle/aligner_oracle.cpp (reference-algorithm "
+                             "C++ restatement, scalar DP), OpenMP one pair per thread, %.1f s wall" % (ns, cpu_s),
+                   "matches_gpu": bool(match)}
+        kernel_s = kernel_ms / 1e3
+        achieved = alg_bytes / kernel_s / 1e9
+        grid, dev_bytes = b.config()
+        out = {
+            "metric": "global alignments/sec",
+            "value": round(n * world * args.steps / wall_max, 3),
+            "unit": "alignments/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(wall_max / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 bit-vectors",
+            "data": "synthetic (reference genomeutils generators, seeds 1..N)",
+            "config": {"workload": "cudaaligner global, %d pairs/GPU x %d bp, ~10%% difference, %s"
+                                   % (n, L, cfg["algorithm"]),
+                       "config_key": args.config, "pairs_per_gpu": n, "length": L,
+                       "algorithm": cfg["algorithm"], "grid": grid, "device_bytes": dev_bytes,
+                       "gcups": round(cells / kernel_s / 1e9, 3), "input_gen_s": round(gen_s, 2),
+                       "parallelism": "dp%d (pairs sharded)" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "hm_kernel" if cfg["algorithm"] == "hirschberg_myers" else "myers_kernel",
+                         "kernel_ms": round(kernel_ms, 3), "algorithmic_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.config in ALIGNER_CONFIGS:
+        return bench_aligner(args)
     cfg = dict(CONFIGS[args.config])
     if args.windows:
         cfg["windows"] = args.windows
