@@ -16,17 +16,17 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(src, name, config="B", windows=1024):
+def main(src, name, config="B", windows=1024, kernel="poa_window_kernel"):
     dst = os.path.join(ROOT, "profiles", name)
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "trace_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     stats = list(csv.DictReader(open(os.path.join(dst, "kernel_stats.csv"))))
-    poa = [r for r in stats if "poa_window_kernel" in r["Name"]]
+    poa = [r for r in stats if kernel in r["Name"]]
     vals = {}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         rows = csv.DictReader(open(os.path.join(src, "pmc_" + c, "pmc_counter_collection.csv")))
         vals[c] = [float(r["Counter_Value"]) for r in rows
-                   if "poa_window_kernel" in r["Kernel_Name"] and r["Counter_Name"] == c]
+                   if kernel in r["Kernel_Name"] and r["Counter_Name"] == c]
     fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
     write = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
     hbm = int((2 * fetch + write) * 1024)
@@ -37,10 +37,16 @@ def main(src, name, config="B", windows=1024):
             "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, KB per dispatch; "
                     "hbm bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024"}
     json.dump(summ, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
-    json.dump({"config": config, "windows": windows, "hbm_bytes_per_launch": hbm, "source": "profiles/" + name},
-              open(os.path.join(ROOT, "profiles", "traffic_poa_%s.json" % config), "w"), indent=1)
+    if kernel == "poa_window_kernel":
+        json.dump({"config": config, "windows": windows, "hbm_bytes_per_launch": hbm, "source": "profiles/" + name},
+                  open(os.path.join(ROOT, "profiles", "traffic_poa_%s.json" % config), "w"), indent=1)
+    else:
+        json.dump({"config": config, "pairs": windows, "hbm_bytes_per_launch": hbm, "source": "profiles/" + name},
+                  open(os.path.join(ROOT, "profiles", "traffic_aligner_%s.json" % config), "w"), indent=1)
     print(json.dumps(summ, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], *(sys.argv[3:4] or []))
+    a = sys.argv[1:]
+    main(a[0], a[1], a[2] if len(a) > 2 else "B", int(a[3]) if len(a) > 3 else 1024,
+         a[4] if len(a) > 4 else "poa_window_kernel")
