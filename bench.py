@@ -152,6 +152,15 @@ def bench_aligner(args):
         kernel_s = kernel_ms / 1e3
         achieved = alg_bytes / kernel_s / 1e9
         grid, dev_bytes = b.config()
+        traffic = None
+        tfile = os.path.join(ROOT, "profiles", "traffic_aligner_%s.json" % args.config)
+        if os.path.exists(tfile):
+            try:
+                tf = json.load(open(tfile))
+                if tf.get("pairs") == n:
+                    traffic = tf.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
         out = {
             "metric": "global alignments/sec",
             "value": round(n * world * args.steps / wall_max, 3),
@@ -167,7 +176,7 @@ def bench_aligner(args):
                        "gcups": round(cells / kernel_s / 1e9, 3), "input_gen_s": round(gen_s, 2),
                        "parallelism": "dp%d (pairs sharded)" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "hm_kernel" if cfg["algorithm"] == "hirschberg_myers" else "myers_kernel",
                          "kernel_ms": round(kernel_ms, 3), "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
