@@ -443,7 +443,7 @@ private:
         b += 2 * align8(int64_t(dims_.aln_cap) * sz);                 // ag, ar
         b += int64_t(dims_.score_rows) * dims_.score_stride * sbytes; // scores (LDS kernel: spill rows)
         if (dims_.lds_kernel)
-            b += int64_t(dims_.score_rows) * dims_.code_stride;           // traceback codes
+            b += dims_.aux_stride; // traceback codes, row program, predecessor lists, carries
         b += align8(mn * 4) + align8(mn * 4 * sz);                    // cscore, cpred
         b += align8(dims_.max_consensus) + align8(int64_t(dims_.max_consensus) * 2) + 32; // outputs
         b += int64_t(S) * dims_.max_seq_len * 2 + S * 12;             // inputs
@@ -454,9 +454,12 @@ private:
     }
 
     // LDS-resident kernel (poa_window_kernel_lds): full alignment with 16-bit
-    // scores and node ids.  LDS image: read | ring (>= one traceback tile) |
-    // row program | extra predecessor list, sized to keep 4 workgroups per CU
-    // (40 KiB) when the window limits allow it.
+    // scores and node ids.  LDS image per window: read | ring of E rows (also
+    // the traceback tile + staged row program, the add-alignment scratch and,
+    // together with the read, the topological-sort scratch) | shared words.
+    // The row program, predecessor lists and span carries live in HBM next to
+    // the traceback codes.  About 20 KiB per window for 1 kb reads: 8 windows
+    // per CU.
     void plan_lds_kernel()
     {
         dims_.lds_kernel = 0;
@@ -468,27 +471,13 @@ private:
         auto a16             = [](int64_t v) { return (v + 15) & ~int64_t(15); };
         const int ring_rows  = 8;
         const int64_t read_b = a16(int64_t(dims_.max_seq_len) + 48);
-        // the ring region also holds one traceback tile and the add-alignment scratch
-        const int64_t add_b  = 5 * a16(dims_.max_seq_len + 16) + 2 * (int64_t(dims_.max_nodes) + dims_.max_seq_len);
-        const int64_t ring_b = std::max<int64_t>({int64_t(ring_rows) * dims_.score_stride * 2,
-                                                  int64_t(gwamd::poa::kTileRows) * gwamd::poa::kTileCols, add_b});
-        const int64_t rec_b  = a16(int64_t(dims_.max_nodes + 1) * 4);
-        const int64_t fixed  = read_b + ring_b + rec_b;
-        const int64_t sh_b   = gwamd::poa::kShBytes;
-        const int64_t target = 40960 - 16; // keep 4 workgroups per CU incl. static LDS
-        int64_t xl_cap       = std::max<int64_t>(1024, (target - fixed - sh_b) / 2);
-        xl_cap               = std::min<int64_t>(xl_cap, 65535);
-        const int64_t total  = fixed + a16(xl_cap * 2) + sh_b;
-        if (total > 65536)
-            return;
-        // forward pass shape: CPL columns per lane on NW waves; one pass
-        // covers NW*64*CPL read columns (GWAMD_POA_LDS_SHAPE="cpl,waves")
+        // forward pass shape: CPL columns per lane on NW waves; a sweep covers
+        // NW*64*CPL read columns, longer reads take several sweeps
+        // (GWAMD_POA_LDS_SHAPE="cpl,waves")
         int cpl = 8, nw = 1;
         const int ms = dims_.max_seq_len;
-        if (ms <= 4 * 512)
-            nw = (ms + 511) / 512;
-        else
-            nw = 4, cpl = 16;
+        if (ms > 512)
+            nw = 2;
         if (const char* sh = std::getenv("GWAMD_POA_LDS_SHAPE"))
         {
             int c = 0, n = 0;
@@ -501,20 +490,35 @@ private:
                 cpl = c, nw = n;
             }
         }
-        // the forward pass covers a read in one sweep: NW spans of 64*CPL columns
-        if (int64_t(64) * cpl * nw < ms)
+        const int64_t add_b  = 5 * a16(dims_.max_seq_len + 16) + 2 * (int64_t(dims_.max_nodes) + dims_.max_seq_len);
+        const int64_t tile_b = int64_t(gwamd::poa::kTileRows) * gwamd::poa::kTileCols + gwamd::poa::kTileRows * 4 +
+                               gwamd::poa::kTileXlMin * 2;
+        const int64_t ring_b = a16(std::max<int64_t>({int64_t(ring_rows) * dims_.score_stride * 2, tile_b, add_b}));
+        const int64_t sh_b   = a16(gwamd::poa::kShBytes(nw));
+        int64_t total        = read_b + ring_b + sh_b;
+        if (const char* pad = std::getenv("GWAMD_POA_LDS_PAD")) // diagnostic: fewer windows per CU
+            total += a16(std::atoi(pad));
+        if (total > 65536)
             return;
         dims_.lds_kernel    = 1;
         dims_.lds_ring_off  = int32_t(read_b);
         dims_.lds_ring_rows = ring_rows;
-        dims_.lds_rec_off   = int32_t(read_b + ring_b);
-        dims_.lds_xl_off    = int32_t(read_b + ring_b + rec_b);
-        dims_.lds_xl_cap    = int32_t(xl_cap);
         dims_.lds_bytes     = int32_t(total);
-        dims_.lds_sh_off    = int32_t(total - sh_b);
+        dims_.lds_sh_off    = int32_t(read_b + ring_b);
         dims_.lds_cpl       = cpl;
         dims_.lds_waves     = nw;
         dims_.code_stride   = int32_t(a16(int64_t(dims_.max_seq_len) + 48));
+        // HBM side buffer per window
+        const int64_t code_b = int64_t(dims_.score_rows) * dims_.code_stride;
+        const int64_t rec_b  = a16(int64_t(dims_.max_nodes + 2) * 4);
+        const int64_t xl_cap = std::min<int64_t>(int64_t(dims_.max_nodes) * 8, 1 << 20);
+        const int64_t xl_b   = a16(xl_cap * 2);
+        const int64_t cr_b   = a16(int64_t(dims_.max_nodes + 2) * 2);
+        dims_.aux_rec_off    = int32_t(code_b);
+        dims_.aux_xl_off     = int32_t(code_b + rec_b);
+        dims_.aux_xl_cap     = int32_t(xl_cap);
+        dims_.aux_carry_off  = int32_t(code_b + rec_b + xl_b);
+        dims_.aux_stride     = code_b + rec_b + xl_b + cr_b;
     }
 
     // Non-score bytes of the reference slab for max_poas windows
@@ -603,7 +607,7 @@ private:
         bufs_.scores = base + sc_off;
         if (dims_.lds_kernel)
         {
-            const size_t code_bytes = size_t(P) * size_t(dims_.score_rows) * size_t(dims_.code_stride);
+            const size_t code_bytes = size_t(P) * size_t(dims_.aux_stride);
             GWAMD_HIP_CHECK(hipMalloc(&d_codes_.p, code_bytes));
             d_codes_.n   = code_bytes;
             bufs_.codes = static_cast<uint8_t*>(d_codes_.p);

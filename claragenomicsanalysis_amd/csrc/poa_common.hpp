@@ -58,34 +58,37 @@ struct Dims
     int32_t band_width;    // banded mode only
     int32_t want_consensus; // MSA kernels also emit the consensus when set
     // LDS-resident kernel (full alignment, 16-bit scores): layout of the
-    // per-workgroup LDS image and the traceback-code matrix
+    // per-workgroup LDS image and of the per-window HBM side buffers
     int32_t lds_kernel;     // 1: launch the LDS-resident kernel
     int32_t lds_bytes;      // dynamic LDS per workgroup
     int32_t lds_ring_off;   // E-domain score rows ring (int16)
     int32_t lds_ring_rows;  // power of two
-    int32_t lds_rec_off;    // per-row program (u32 per row)
-    int32_t lds_xl_off;     // extra predecessor rows (u16)
-    int32_t lds_xl_cap;
-    int32_t code_stride;    // bytes per traceback-code row
     int32_t lds_sh_off;     // small shared region (layout: kSh* below)
     int32_t lds_cpl;        // forward pass: columns per lane
     int32_t lds_waves;      // forward pass: waves per window
+    int32_t code_stride;    // bytes per traceback-code row
+    int64_t aux_stride;     // bytes per window of the HBM side buffer:
+    int32_t aux_rec_off;    //   codes [score_rows x code_stride] | row program (u32 per row)
+    int32_t aux_xl_off;     //   | predecessor lists (u16) | per-row span carries (int16)
+    int32_t aux_xl_cap;
+    int32_t aux_carry_off;
 };
 
-// Small shared region of the LDS kernel (kShBytes at Dims::lds_sh_off):
+// Small shared region of the LDS kernel (kShBytes(waves) at Dims::lds_sh_off):
 // control ints, per-wave channel progress, the end-row slot, the per-span
 // boundary column ([waves][ring rows] int16) and the span-to-span carry
 // channels ([waves-1][kChanRows] tagged words).
 constexpr int kShProg    = 16;
 constexpr int kShEnd     = 32;
 constexpr int kShBnd     = 64;
-constexpr int kShChan    = 256;
+constexpr int kShChan    = 128;
 constexpr int kChanRows  = 64;
 constexpr int kMaxWaves  = 4;
-constexpr int kShBytes   = kShChan + (kMaxWaves - 1) * kChanRows * 4;
+constexpr int kShBytes(int waves) { return kShChan + (waves - 1) * kChanRows * 4; }
 
 constexpr int kTileRows = 128; // traceback tile (codes) rows
 constexpr int kTileCols = 128; // traceback tile columns (bytes)
+constexpr int kTileXlMin = 512; // predecessor-list entries staged with a tile (at least)
 
 // Device pointers of one batch (all batch-wide; per-window slots are derived
 // in-kernel).  SizeT-typed arrays are passed as void* and cast in the kernel.

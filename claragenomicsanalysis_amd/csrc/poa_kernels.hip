@@ -648,7 +648,8 @@ __device__ __forceinline__ void load_row_pk(const int16_t* p, uint32_t (&P)[NR],
 template <int CPL, int NW, typename SizeT>
 __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int V, const uint8_t* read, int L,
                                  int16_t* ring, int ring_stride, int16_t* spill, int stride, uint8_t* codes,
-                                 int code_stride, const Scores sc, GWAMD_LDS uint8_t* shb, int tid, FwdProf& fp)
+                                 int code_stride, const Scores sc, GWAMD_LDS uint8_t* shb, int16_t* carry_hbm,
+                                 int tid, FwdProf& fp)
 {
     constexpr int NR    = CPL / 2;
     constexpr int kSpan = kWave * CPL;
@@ -670,17 +671,33 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
     volatile GWAMD_LDS uint32_t* chan_in  = chan + (wave - 1) * kChanRows; // wave > 0
     volatile GWAMD_LDS uint32_t* chan_out = chan + wave * kChanRows;       // wave < NW-1
     volatile GWAMD_LDS int* prog_v        = prog;
-    const int cb        = wave * kSpan;
-    const bool wact     = cb < L || wave == 0;
-    const bool feed     = wave + 1 < NW && cb + kSpan < L; // the next span holds read columns
-    // owner of the last column (L-1): wave, lane, cell
+    // owner of the last column (L-1): span, lane, cell
     const int jl        = L > 0 ? L - 1 : 0;
-    const int own_wave  = jl / kSpan;
+    const int own_span  = jl / kSpan;
     const int own_lane  = (jl % kSpan) / CPL;
     const int own_c     = jl % CPL;
-    const bool owner    = wave == own_wave;
+    const int nspan     = max(1, (L + kSpan - 1) / kSpan);
+    const int nsweep    = (nspan + NW - 1) / NW;
     int best_row        = 0;
     int best_val        = INT_MIN;
+    for (int sweep = 0; sweep < nsweep; sweep++)
+    {
+    if (sweep > 0)
+    {
+        // channels restart empty; the previous sweep's carries are in HBM
+        __syncthreads();
+        for (int t = tid; t < (kShChan - kShProg) / 4 + (NW - 1) * kChanRows; t += kWave * NW)
+            reinterpret_cast<GWAMD_LDS int*>(shb + kShProg)[t] = 0;
+        __syncthreads();
+    }
+    const int span      = sweep * NW + wave;
+    const int cb        = span * kSpan;
+    const bool first    = span == 0;                // holds column 0
+    const bool wact     = cb < L || first;
+    const bool feed     = wave + 1 < NW && cb + kSpan < L;  // next span, same sweep
+    const bool to_hbm   = wave == NW - 1 && cb + kSpan < L; // next span, next sweep
+    const bool from_hbm = wave == 0 && sweep > 0;
+    const bool owner    = span == own_span;
     const int jb        = cb + lane * CPL;
     const bool active   = jb < L;
     const int ja        = active ? jb : 0; // address used by inactive lanes
@@ -703,6 +720,7 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
         for (int i = 0; i < NR; i++)
             Eprev[i] = 0;
         int cin_prev = 0;
+        int hbm_c    = 0; // carries of 64 rows from the previous sweep, one per lane
         // software pipeline: predecessor rows of row r (pv_c), record of row r+1
         uint32_t rec_c = uniform(int(P.rec[1]));
         int np_c;
@@ -777,10 +795,9 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
                 else
                 {
                     load_row_pk<NR>(ring + (p & mask) * ring_stride + ja + kColShift, Q, qprev);
-                    if (NW > 1)
                     {
                         const uint32_t bv = uint32_t(uint16_t(bnd[p & mask]));
-                        if (lane == 0 && wave > 0)
+                        if (lane == 0 && cb > 0)
                             qprev = bv;
                     }
                 }
@@ -845,7 +862,7 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
             const int excl = __builtin_amdgcn_update_dpp(kNeg, incl, 0x138, 0xf, 0xf, false);
             const int wtot = __builtin_amdgcn_readlane(incl, kWave - 1);
             int cin;
-            if (wave == 0)
+            if (first)
             {
                 cin           = __builtin_amdgcn_readfirstlane(c0v) + gap; // column 0
                 const int c0k = __builtin_amdgcn_readfirstlane(c0kv);
@@ -859,16 +876,29 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
             }
             else
             {
-                // carry of this row from the previous span
-                uint32_t w = uint32_t(uniform(int(chan_in[r & (kChanRows - 1)])));
-                while ((w >> 16) != (uint32_t(r) & 0xffffu))
+                if (from_hbm)
                 {
-                    __builtin_amdgcn_s_sleep(1);
-                    w = uint32_t(uniform(int(chan_in[r & (kChanRows - 1)])));
+                    // carry of this row from the previous sweep's last span
+                    if (((r - 1) & (kWave - 1)) == 0)
+                    {
+                        const int x = r + lane;
+                        hbm_c       = x <= V ? int(carry_hbm[x]) : 0;
+                    }
+                    cin = int(int16_t(__builtin_amdgcn_readlane(hbm_c, (r - 1) & (kWave - 1))));
                 }
-                cin = int(int16_t(w & 0xffffu));
-                if ((r & 7) == 0 && lane == 0)
-                    prog_v[wave] = r;
+                else
+                {
+                    // carry of this row from the previous span
+                    uint32_t w = uint32_t(uniform(int(chan_in[r & (kChanRows - 1)])));
+                    while ((w >> 16) != (uint32_t(r) & 0xffffu))
+                    {
+                        __builtin_amdgcn_s_sleep(1);
+                        w = uint32_t(uniform(int(chan_in[r & (kChanRows - 1)])));
+                    }
+                    cin = int(int16_t(w & 0xffffu));
+                    if ((r & 7) == 0 && lane == 0)
+                        prog_v[wave] = r;
+                }
                 if (lane == 0)
                 {
                     bnd[r & mask] = int16_t(cin);
@@ -888,6 +918,8 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
                 if (lane == 0)
                     chan_out[r & (kChanRows - 1)] = (uint32_t(r) << 16) | uint32_t(uint16_t(max(cin, wtot)));
             }
+            if (to_hbm && lane == 0)
+                carry_hbm[r] = int16_t(max(cin, wtot));
             GWAMD_FP_LAP(fp, 2);
             const uint32_t b2v = pk_bcast(max(excl, cin));
 #pragma unroll
@@ -947,11 +979,12 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
             GWAMD_FP_LAP(fp, 3);
         }
     }
-    if constexpr (NW > 1)
+    } // sweeps
+    if (nsweep > 1 || NW > 1)
     {
         // publish the end row from the wave that owns the last column
         GWAMD_LDS int* endp = (GWAMD_LDS int*)(shb + kShEnd);
-        if (owner && lane == 0)
+        if (wave == own_span % NW && lane == 0)
             *endp = best_row;
         __syncthreads();
         best_row = uniform(*endp);
@@ -959,20 +992,41 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
     return best_row;
 }
 
-// Traceback over the code matrix (lane-uniform walk, tiles staged in LDS by
-// the whole wave).  Emits reversed (row or -1, read position or -1) pairs;
-// rows are converted to node ids afterwards.
+// Traceback over the code matrix, run by one wave (lane-uniform walk; code
+// tiles of 128 rows x 128 columns staged in LDS).  The tile code and the row
+// record are loaded together, so a step waits for at most two LDS round trips
+// (code/record, then a predecessor list).  Emitted pairs (node id or -1, read
+// position or -1; reversed, as the reference's traceback,
+// cudapoa_nw.cuh:361-452) are collected one per lane and stored 64 at a time;
+// rows become node ids at the store.
 template <typename SizeT>
 __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V, int L, int end_row,
-                               const uint8_t* codes, int code_stride, uint8_t* tile, SizeT* ag, SizeT* ar,
-                               int aln_cap, int tid, int nthreads)
+                               const uint8_t* codes, int code_stride, uint8_t* tile, int tile_bytes, SizeT* ag,
+                               SizeT* ar, int aln_cap, int lane)
 {
+    // staged with each code tile: the row records of its rows and the
+    // predecessor-list entries they index (the row program lives in HBM)
+    uint32_t* trec    = reinterpret_cast<uint32_t*>(tile + kTileRows * kTileCols);
+    uint16_t* txl     = reinterpret_cast<uint16_t*>(trec + kTileRows);
+    const int txl_cap = (tile_bytes - kTileRows * kTileCols - kTileRows * 4) / 2;
+    int xlo = 0, xcnt = 0;
     V       = uniform(V);
     L       = uniform(L);
     int i   = uniform(end_row), j = L;
     int ti0 = INT_MIN / 2, tj0 = INT_MIN / 2;
     int n = 0, loops = 0;
     const int bound = L + V + 2;
+    int eg = 0, er = 0; // lane (n & 63) holds pair n until it is stored
+    auto flush = [&](int upto) {
+        // pairs [upto & ~63, upto) are held by lanes 0 .. (upto-1) & 63
+        const int base = (upto - 1) & ~(kWave - 1);
+        const int k    = base + lane;
+        if (k < upto && k < aln_cap)
+        {
+            ag[k] = SizeT(eg > 0 ? int(g.sorted[eg - 1]) : -1);
+            ar[k] = SizeT(er);
+        }
+    };
     while (!(i == 0 && j == 0) && loops < bound)
     {
         loops++;
@@ -989,8 +1043,8 @@ __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V
             {
                 ti0 = max(0, i - (kTileRows - 1));
                 tj0 = max(0, cj - (kTileCols - 16)) & ~15;
-                __syncthreads();
-                for (int t = tid; t < kTileRows * (kTileCols / 16); t += nthreads)
+                wave_sync();
+                for (int t = lane; t < kTileRows * (kTileCols / 16); t += kWave)
                 {
                     const int tr = t / (kTileCols / 16);
                     const int tc = (t % (kTileCols / 16)) * 16;
@@ -1000,10 +1054,32 @@ __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V
                         v = *reinterpret_cast<const uint4*>(codes + size_t(rr) * code_stride + tj0 + tc);
                     *reinterpret_cast<uint4*>(tile + tr * kTileCols + tc) = v;
                 }
-                __syncthreads();
+                int lo = INT_MAX, hi = 0;
+                for (int t = lane; t < kTileRows; t += kWave)
+                {
+                    const int rr     = ti0 + t;
+                    const uint32_t v = (rr >= 1 && rr <= V) ? P.rec[rr] : 0u;
+                    trec[t]          = v;
+                    const int np     = int((v >> 8) & 63);
+                    if (np >= 2 && np != int(kRecEscape))
+                    {
+                        lo = min(lo, int(v >> 16));
+                        hi = max(hi, int(v >> 16) + np);
+                    }
+                }
+                lo   = -wave_max(-lo);
+                hi   = wave_max(hi);
+                xlo  = uniform(lo);
+                xcnt = (hi > xlo && hi - xlo <= txl_cap) ? uniform(hi - xlo) : 0;
+                for (int t = lane; t < xcnt; t += kWave)
+                    txl[t] = P.xl[xlo + t];
+                wave_sync();
             }
-            const int code = uniform(int(tile[(i - ti0) * kTileCols + (cj - tj0)]));
-            const int dir  = code & 3;
+            const int code_v   = int(tile[(i - ti0) * kTileCols + (cj - tj0)]);
+            const int rec_v    = int(trec[i - ti0]);
+            const int code     = uniform(code_v);
+            const uint32_t rec = uint32_t(uniform(rec_v));
+            const int dir      = code & 3;
             if (dir == 2)
             {
                 pi = i;
@@ -1011,20 +1087,32 @@ __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V
             }
             else
             {
-                const uint32_t rec = uint32_t(uniform(int(P.rec[i])));
-                pi                 = uniform(prog_pred(P, g, i, rec, code >> 2));
-                pj                 = dir == 0 ? j - 1 : j;
+                const int np   = int((rec >> 8) & 63);
+                const int slot = code >> 2;
+                if (np >= 2 && np != int(kRecEscape))
+                {
+                    const int x = int(rec >> 16) + slot - xlo;
+                    pi          = uniform(x >= 0 && x < xcnt ? int(txl[x]) : int(P.xl[int(rec >> 16) + slot]));
+                }
+                else
+                    pi = uniform(prog_pred(P, g, i, rec, slot));
+                pj = dir == 0 ? j - 1 : j;
             }
         }
-        if (tid == 0 && n < aln_cap)
+        if (lane == (n & (kWave - 1)))
         {
-            ag[n] = SizeT(i == pi ? -1 : i);
-            ar[n] = SizeT(j == pj ? -1 : j - 1);
+            eg = i == pi ? -1 : i;
+            er = j == pj ? -1 : j - 1;
         }
         n++;
+        if ((n & (kWave - 1)) == 0)
+            flush(n);
         i = pi;
         j = pj;
     }
+    if ((n & (kWave - 1)) != 0)
+        flush(n);
+    wave_sync();
     if (loops >= bound || n > aln_cap)
         return -1;
     return n;
@@ -1277,10 +1365,10 @@ template <typename SizeT>
 __device__ bool topsort_lds(WinGraph<SizeT>& g, int n, GWAMD_LDS uint8_t* scratch, int scratch_bytes,
                             GWAMD_LDS int* sh, int lane)
 {
-    GWAMD_LDS uint32_t* off   = (GWAMD_LDS uint32_t*)(scratch);
-    GWAMD_LDS uint16_t* queue = (GWAMD_LDS uint16_t*)(scratch + (n + 1) * 4);
-    GWAMD_LDS uint8_t* cnt    = scratch + (n + 1) * 4 + n * 2;
-    const int head_bytes      = ((n + 1) * 4 + n * 2 + n + 15) & ~15;
+    GWAMD_LDS uint16_t* off   = (GWAMD_LDS uint16_t*)(scratch);
+    GWAMD_LDS uint16_t* queue = (GWAMD_LDS uint16_t*)(scratch + (n + 1) * 2);
+    GWAMD_LDS uint8_t* cnt    = scratch + (n + 1) * 2 + n * 2;
+    const int head_bytes      = ((n + 1) * 2 + n * 2 + n + 15) & ~15;
     GWAMD_LDS uint16_t* edges = (GWAMD_LDS uint16_t*)(scratch + head_bytes);
     if (head_bytes > scratch_bytes)
         return false;
@@ -1294,15 +1382,15 @@ __device__ bool topsort_lds(WinGraph<SizeT>& g, int n, GWAMD_LDS uint8_t* scratc
         const int ex = wave_excl_sum(oc, lane, total);
         if (v < n)
         {
-            off[v] = uint32_t(ebase + ex);
+            off[v] = uint16_t(ebase + ex);
             cnt[v] = uint8_t(g.in_cnt[v]);
         }
         ebase += total;
     }
-    if (ebase > edge_cap)
+    if (ebase > edge_cap || ebase > 65535)
         return false;
     if (lane == 0)
-        off[n] = uint32_t(ebase);
+        off[n] = uint16_t(ebase);
     wave_sync();
     for (int v = lane; v < n; v += kWave)
     {
@@ -1376,11 +1464,9 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
 
     uint8_t* lread   = lds;
     int16_t* ring    = reinterpret_cast<int16_t*>(lds + d.lds_ring_off);
-    uint32_t* rec    = reinterpret_cast<uint32_t*>(lds + d.lds_rec_off);
-    uint16_t* xl     = reinterpret_cast<uint16_t*>(lds + d.lds_xl_off);
     uint8_t* tile    = lds + d.lds_ring_off; // traceback tiles reuse the ring
+    const int tile_bytes = d.lds_sh_off - d.lds_ring_off;
     const int rstride = d.score_stride;      // ring / spill row stride (elements)
-    RowProg P{rec, xl, d.lds_ring_rows - 1};
     GWAMD_LDS uint8_t* shb = (GWAMD_LDS uint8_t*)(lds) + d.lds_sh_off;
     AddScratch AX;
     {
@@ -1412,7 +1498,11 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
     SizeT* ag        = static_cast<SizeT*>(b.ag) + size_t(w) * d.aln_cap;
     SizeT* ar        = static_cast<SizeT*>(b.ar) + size_t(w) * d.aln_cap;
     int16_t* spill   = static_cast<int16_t*>(b.scores) + size_t(w) * d.score_rows * size_t(rstride);
-    uint8_t* codes   = b.codes + size_t(w) * d.score_rows * size_t(d.code_stride);
+    uint8_t* codes   = b.codes + size_t(w) * size_t(d.aux_stride);
+    uint32_t* rec    = reinterpret_cast<uint32_t*>(codes + d.aux_rec_off);
+    uint16_t* xl     = reinterpret_cast<uint16_t*>(codes + d.aux_xl_off);
+    int16_t* carry   = reinterpret_cast<int16_t*>(codes + d.aux_carry_off);
+    RowProg P{rec, xl, d.lds_ring_rows - 1};
     int32_t* cscore  = b.cscore + w * mn;
     SizeT* cpred     = static_cast<SizeT*>(b.cpred) + w * mn * 4;
     uint16_t* ecov   = MSA ? b.edge_cov + w * mn * kMaxEdges * d.max_seqs : nullptr;
@@ -1452,29 +1542,28 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
                 lread[j] = j < L ? read_g[j] : 0;
             const int V = node_count;
             if (wave == 0)
-                build_row_program<SizeT>(g, V, rec, xl, d.lds_xl_cap, d.lds_ring_rows, lane);
+                build_row_program<SizeT>(g, V, rec, xl, d.aux_xl_cap, d.lds_ring_rows, lane);
             if (NW > 1)
             {
                 // forward-pass channels and progress words start empty
-                for (int t = tid; t < (kShBytes - kShProg) / 4; t += kThr)
+                for (int t = tid; t < (kShBytes(NW) - kShProg) / 4; t += kThr)
                     reinterpret_cast<GWAMD_LDS int*>(shb + kShProg)[t] = 0;
             }
             __syncthreads();
             cells += int64_t(V + 1) * (L + 1);
             const int end_row = nw_forward_lds_pk<CPL, NW, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride,
-                                                                  codes, d.code_stride, sc, shb, tid, fp);
+                                                                  codes, d.code_stride, sc, shb, carry, tid, fp);
             __syncthreads();
             ph.lap<kPhForward>();
-            const int alen = traceback_codes<SizeT>(g, P, V, L, end_row, codes, d.code_stride, tile, ag, ar,
-                                                    d.aln_cap, tid, kThr);
-            __syncthreads();
-            // rows -> node ids
-            for (int k = tid; k < alen; k += kThr)
+            if (wave == 0)
             {
-                const int rr = int(ag[k]);
-                if (rr > 0)
-                    ag[k] = g.sorted[rr - 1];
+                const int alen_w = traceback_codes<SizeT>(g, P, V, L, end_row, codes, d.code_stride, tile,
+                                                          tile_bytes, ag, ar, d.aln_cap, lane);
+                if (lane == 0)
+                    sh_len = alen_w;
             }
+            __syncthreads();
+            const int alen = uniform(sh_len);
             __syncthreads();
             ph.lap<kPhTraceback>();
             if (alen == -1)
@@ -1502,8 +1591,8 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
                 ph.lap<kPhAdd>();
                 if (rc == kSuccess)
                 {
-                    if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds) + d.lds_ring_off,
-                                            d.lds_sh_off - d.lds_ring_off, AX.sh, lane))
+                    // scratch: the read and the ring (both free after the add)
+                    if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, AX.sh, lane))
                     {
                         if (lane == 0)
                             topsort_kahn<SizeT>(g, nc, cscore);

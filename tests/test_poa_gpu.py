@@ -221,15 +221,14 @@ def test_lds_kernel_empty_and_tiny_reads():
 
 @pytest.mark.parametrize("shape", ["8,1", "16,1", "24,1", "32,1", "8,2", "8,3", "8,4", "16,4"])
 def test_lds_forward_shapes(shape, monkeypatch):
-    # every (columns per lane, waves per window) forward-pass shape; one sweep
-    # covers max_seq, so reads fill the spans up to the last one (idle lanes
-    # and idle waves included)
+    # every (columns per lane, waves per window) forward-pass shape; reads
+    # longer than one sweep (NW*64*CPL columns) take several sweeps, and span /
+    # sweep boundaries (512, 513, 1024, 1025 columns) are hit exactly
     monkeypatch.setenv("GWAMD_POA_LDS_SHAPE", shape)
-    c, n = map(int, shape.split(","))
-    max_seq = min(64 * c * n, 1100)
-    bb = max_seq - 60
-    wins = synth.poa_windows(301, 5, bb, 12, 25, 25, 25)
-    wins.append([b"ACGT" * (max_seq // 4), b"ACGT" * (max_seq // 4 - 1) + b"A", b"", b"ACGTTGCA" * (max_seq // 9)])
+    max_seq = 1100
+    wins = synth.poa_windows(301, 4, 1040, 12, 25, 25, 25)
+    wins.append([b"ACGT" * 256, b"ACGT" * 256 + b"A", b"", b"ACGTTGCA" * 64, b"ACGTTGCA" * 64 + b"G",
+                 b"ACGT" * 128, b"C" * 1100])
     b = run_gpu(wins, max_seq, 12)
     assert b.kernel_variant() == 2
     cons, cov, st = b.get_consensus()
