@@ -455,11 +455,10 @@ private:
 
     // LDS-resident kernel (poa_window_kernel_lds): full alignment with 16-bit
     // scores and node ids.  LDS image per window: read | ring of E rows (also
-    // the traceback tile + staged row program, the add-alignment scratch and,
-    // together with the read, the topological-sort scratch) | shared words.
-    // The row program, predecessor lists and span carries live in HBM next to
-    // the traceback codes.  About 20 KiB per window for 1 kb reads: 8 windows
-    // per CU.
+    // the traceback tile and the add-alignment scratch) | row program |
+    // predecessor lists | shared words; the topological sort reuses everything
+    // below the shared words.  Span carries of multi-sweep reads live in HBM
+    // next to the traceback codes.
     void plan_lds_kernel()
     {
         dims_.lds_kernel = 0;
@@ -491,11 +490,16 @@ private:
             }
         }
         const int64_t add_b  = 5 * a16(dims_.max_seq_len + 16) + 2 * (int64_t(dims_.max_nodes) + dims_.max_seq_len);
-        const int64_t tile_b = int64_t(gwamd::poa::kTileRows) * gwamd::poa::kTileCols + gwamd::poa::kTileRows * 4 +
-                               gwamd::poa::kTileXlMin * 2;
+        const int64_t tile_b = int64_t(gwamd::poa::kTileRows) * gwamd::poa::kTileCols;
         const int64_t ring_b = a16(std::max<int64_t>({int64_t(ring_rows) * dims_.score_stride * 2, tile_b, add_b}));
+        const int64_t rec_b  = a16(int64_t(dims_.max_nodes + 2) * 4);
         const int64_t sh_b   = a16(gwamd::poa::kShBytes(nw));
-        int64_t total        = read_b + ring_b + sh_b;
+        const int64_t fixed  = read_b + ring_b + rec_b + sh_b;
+        const int64_t target = 40960 - 16; // 4 workgroups per CU incl. static LDS: one batch of
+                                           // 1024 windows is resident on the 256 CUs at once
+        int64_t xl_cap       = std::max<int64_t>(1024, (target - fixed) / 2);
+        xl_cap               = std::min<int64_t>(xl_cap, 65535);
+        int64_t total        = fixed + a16(xl_cap * 2);
         if (const char* pad = std::getenv("GWAMD_POA_LDS_PAD")) // diagnostic: fewer windows per CU
             total += a16(std::atoi(pad));
         if (total > 65536)
@@ -503,22 +507,19 @@ private:
         dims_.lds_kernel    = 1;
         dims_.lds_ring_off  = int32_t(read_b);
         dims_.lds_ring_rows = ring_rows;
+        dims_.lds_rec_off   = int32_t(read_b + ring_b);
+        dims_.lds_xl_off    = int32_t(read_b + ring_b + rec_b);
+        dims_.lds_xl_cap    = int32_t(xl_cap);
+        dims_.lds_sh_off    = int32_t(read_b + ring_b + rec_b + a16(xl_cap * 2));
         dims_.lds_bytes     = int32_t(total);
-        dims_.lds_sh_off    = int32_t(read_b + ring_b);
         dims_.lds_cpl       = cpl;
         dims_.lds_waves     = nw;
         dims_.code_stride   = int32_t(a16(int64_t(dims_.max_seq_len) + 48));
-        // HBM side buffer per window
+        // HBM side buffer per window: traceback codes, span carries
         const int64_t code_b = int64_t(dims_.score_rows) * dims_.code_stride;
-        const int64_t rec_b  = a16(int64_t(dims_.max_nodes + 2) * 4);
-        const int64_t xl_cap = std::min<int64_t>(int64_t(dims_.max_nodes) * 8, 1 << 20);
-        const int64_t xl_b   = a16(xl_cap * 2);
         const int64_t cr_b   = a16(int64_t(dims_.max_nodes + 2) * 2);
-        dims_.aux_rec_off    = int32_t(code_b);
-        dims_.aux_xl_off     = int32_t(code_b + rec_b);
-        dims_.aux_xl_cap     = int32_t(xl_cap);
-        dims_.aux_carry_off  = int32_t(code_b + rec_b + xl_b);
-        dims_.aux_stride     = code_b + rec_b + xl_b + cr_b;
+        dims_.aux_carry_off  = int32_t(code_b);
+        dims_.aux_stride     = code_b + cr_b;
     }
 
     // Non-score bytes of the reference slab for max_poas windows

@@ -64,14 +64,14 @@ struct Dims
     int32_t lds_ring_off;   // E-domain score rows ring (int16)
     int32_t lds_ring_rows;  // power of two
     int32_t lds_sh_off;     // small shared region (layout: kSh* below)
+    int32_t lds_rec_off;    // per-row program (u32 per row)
+    int32_t lds_xl_off;     // predecessor lists (u16)
+    int32_t lds_xl_cap;
     int32_t lds_cpl;        // forward pass: columns per lane
     int32_t lds_waves;      // forward pass: waves per window
     int32_t code_stride;    // bytes per traceback-code row
     int64_t aux_stride;     // bytes per window of the HBM side buffer:
-    int32_t aux_rec_off;    //   codes [score_rows x code_stride] | row program (u32 per row)
-    int32_t aux_xl_off;     //   | predecessor lists (u16) | per-row span carries (int16)
-    int32_t aux_xl_cap;
-    int32_t aux_carry_off;
+    int32_t aux_carry_off;  //   codes [score_rows x code_stride] | per-row span carries (int16)
 };
 
 // Small shared region of the LDS kernel (kShBytes(waves) at Dims::lds_sh_off):

@@ -721,20 +721,24 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
             Eprev[i] = 0;
         int cin_prev = 0;
         int hbm_c    = 0; // carries of 64 rows from the previous sweep, one per lane
-        // software pipeline: predecessor rows of row r (pv_c), record of row r+1
+        // software pipeline: predecessor rows of
+        // rows r and r+1, records of rows r+1 and r+2; row r issues the loads
+        // of row r+2's predecessors and row r+3's record
         uint32_t rec_c = uniform(int(P.rec[1]));
-        int np_c;
+        uint32_t rec_a = uniform(int(P.rec[min(2, V)]));
+        uint32_t rec_b = uniform(int(P.rec[min(3, V)]));
+        int np_c, np_a = 1;
         int pv_c       = row_preds<SizeT>(P, g, 1, rec_c, lane, np_c);
-        uint32_t rec_n = uniform(int(P.rec[min(2, V)]));
+        int pv_a       = V >= 2 ? row_preds<SizeT>(P, g, 2, rec_a, lane, np_a) : 0;
         uint8_t* crow  = codes + code_stride;
         int16_t* srow  = spill + stride;
         for (int r = 1; r <= V; r++, crow += code_stride, srow += stride)
         {
             GWAMD_FP_START(fp);
-            int np_n = 1, pv_n = 0;
-            if (r < V)
-                pv_n = row_preds<SizeT>(P, g, r + 1, rec_n, lane, np_n);
-            const uint32_t rec_nn = P.rec[min(r + 2, V)];
+            int np_b = 1, pv_b = 0;
+            if (r + 2 <= V)
+                pv_b = row_preds<SizeT>(P, g, r + 2, rec_b, lane, np_b);
+            const uint32_t rec_bb = P.rec[min(r + 3, V)];
 
             const uint32_t rec = rec_c;
             const int np       = np_c;
@@ -972,10 +976,13 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
             for (int i = 0; i < NR; i++)
                 Eprev[i] = E[i];
             cin_prev = cin;
-            rec_c    = rec_n;
-            np_c     = np_n;
-            pv_c     = pv_n;
-            rec_n    = uniform(int(rec_nn));
+            rec_c    = rec_a;
+            np_c     = np_a;
+            pv_c     = pv_a;
+            rec_a    = rec_b;
+            np_a     = np_b;
+            pv_a     = pv_b;
+            rec_b    = uniform(int(rec_bb));
             GWAMD_FP_LAP(fp, 3);
         }
     }
@@ -1001,15 +1008,10 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
 // rows become node ids at the store.
 template <typename SizeT>
 __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V, int L, int end_row,
-                               const uint8_t* codes, int code_stride, uint8_t* tile, int tile_bytes, SizeT* ag,
-                               SizeT* ar, int aln_cap, int lane)
+                               const uint8_t* codes, int code_stride, uint8_t* tile, SizeT* ag, SizeT* ar,
+                               int aln_cap, int lane)
 {
-    // staged with each code tile: the row records of its rows and the
-    // predecessor-list entries they index (the row program lives in HBM)
-    uint32_t* trec    = reinterpret_cast<uint32_t*>(tile + kTileRows * kTileCols);
-    uint16_t* txl     = reinterpret_cast<uint16_t*>(trec + kTileRows);
-    const int txl_cap = (tile_bytes - kTileRows * kTileCols - kTileRows * 4) / 2;
-    int xlo = 0, xcnt = 0;
+
     V       = uniform(V);
     L       = uniform(L);
     int i   = uniform(end_row), j = L;
@@ -1054,29 +1056,10 @@ __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V
                         v = *reinterpret_cast<const uint4*>(codes + size_t(rr) * code_stride + tj0 + tc);
                     *reinterpret_cast<uint4*>(tile + tr * kTileCols + tc) = v;
                 }
-                int lo = INT_MAX, hi = 0;
-                for (int t = lane; t < kTileRows; t += kWave)
-                {
-                    const int rr     = ti0 + t;
-                    const uint32_t v = (rr >= 1 && rr <= V) ? P.rec[rr] : 0u;
-                    trec[t]          = v;
-                    const int np     = int((v >> 8) & 63);
-                    if (np >= 2 && np != int(kRecEscape))
-                    {
-                        lo = min(lo, int(v >> 16));
-                        hi = max(hi, int(v >> 16) + np);
-                    }
-                }
-                lo   = -wave_max(-lo);
-                hi   = wave_max(hi);
-                xlo  = uniform(lo);
-                xcnt = (hi > xlo && hi - xlo <= txl_cap) ? uniform(hi - xlo) : 0;
-                for (int t = lane; t < xcnt; t += kWave)
-                    txl[t] = P.xl[xlo + t];
                 wave_sync();
             }
             const int code_v   = int(tile[(i - ti0) * kTileCols + (cj - tj0)]);
-            const int rec_v    = int(trec[i - ti0]);
+            const int rec_v    = int(P.rec[i]);
             const int code     = uniform(code_v);
             const uint32_t rec = uint32_t(uniform(rec_v));
             const int dir      = code & 3;
@@ -1087,15 +1070,7 @@ __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V
             }
             else
             {
-                const int np   = int((rec >> 8) & 63);
-                const int slot = code >> 2;
-                if (np >= 2 && np != int(kRecEscape))
-                {
-                    const int x = int(rec >> 16) + slot - xlo;
-                    pi          = uniform(x >= 0 && x < xcnt ? int(txl[x]) : int(P.xl[int(rec >> 16) + slot]));
-                }
-                else
-                    pi = uniform(prog_pred(P, g, i, rec, slot));
+                pi = uniform(prog_pred(P, g, i, rec, code >> 2));
                 pj = dir == 0 ? j - 1 : j;
             }
         }
@@ -1465,7 +1440,6 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
     uint8_t* lread   = lds;
     int16_t* ring    = reinterpret_cast<int16_t*>(lds + d.lds_ring_off);
     uint8_t* tile    = lds + d.lds_ring_off; // traceback tiles reuse the ring
-    const int tile_bytes = d.lds_sh_off - d.lds_ring_off;
     const int rstride = d.score_stride;      // ring / spill row stride (elements)
     GWAMD_LDS uint8_t* shb = (GWAMD_LDS uint8_t*)(lds) + d.lds_sh_off;
     AddScratch AX;
@@ -1499,8 +1473,8 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
     SizeT* ar        = static_cast<SizeT*>(b.ar) + size_t(w) * d.aln_cap;
     int16_t* spill   = static_cast<int16_t*>(b.scores) + size_t(w) * d.score_rows * size_t(rstride);
     uint8_t* codes   = b.codes + size_t(w) * size_t(d.aux_stride);
-    uint32_t* rec    = reinterpret_cast<uint32_t*>(codes + d.aux_rec_off);
-    uint16_t* xl     = reinterpret_cast<uint16_t*>(codes + d.aux_xl_off);
+    uint32_t* rec    = reinterpret_cast<uint32_t*>(lds + d.lds_rec_off);
+    uint16_t* xl     = reinterpret_cast<uint16_t*>(lds + d.lds_xl_off);
     int16_t* carry   = reinterpret_cast<int16_t*>(codes + d.aux_carry_off);
     RowProg P{rec, xl, d.lds_ring_rows - 1};
     int32_t* cscore  = b.cscore + w * mn;
@@ -1542,7 +1516,7 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
                 lread[j] = j < L ? read_g[j] : 0;
             const int V = node_count;
             if (wave == 0)
-                build_row_program<SizeT>(g, V, rec, xl, d.aux_xl_cap, d.lds_ring_rows, lane);
+                build_row_program<SizeT>(g, V, rec, xl, d.lds_xl_cap, d.lds_ring_rows, lane);
             if (NW > 1)
             {
                 // forward-pass channels and progress words start empty
@@ -1557,8 +1531,8 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
             ph.lap<kPhForward>();
             if (wave == 0)
             {
-                const int alen_w = traceback_codes<SizeT>(g, P, V, L, end_row, codes, d.code_stride, tile,
-                                                          tile_bytes, ag, ar, d.aln_cap, lane);
+                const int alen_w = traceback_codes<SizeT>(g, P, V, L, end_row, codes, d.code_stride, tile, ag, ar,
+                                                          d.aln_cap, lane);
                 if (lane == 0)
                     sh_len = alen_w;
             }
