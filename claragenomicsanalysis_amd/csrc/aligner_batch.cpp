@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -21,6 +22,8 @@
 
 extern "C" hipError_t gwamd_internal_align_launch(const gwamd::aln::Args* a, int algo, int grid, hipStream_t stream);
 extern "C" hipError_t gwamd_internal_align_occupancy(int algo, int lds_bytes, int* blocks_per_cu);
+extern "C" hipError_t gwamd_internal_banded_launch(const gwamd::aln::Args* a, int algo, int grid, hipStream_t stream);
+extern "C" hipError_t gwamd_internal_banded_occupancy(int algo, int lds_bytes, int* blocks_per_cu);
 
 namespace claraparabricks
 {
@@ -182,6 +185,10 @@ public:
             throw std::invalid_argument("max_query_length above 16384 is not supported by this aligner.");
         if (algo_ == GWAMD_ALIGNER_MYERS && max_q_ > 8192)
             throw std::invalid_argument("max_query_length above 8192 is not supported by the full Myers aligner.");
+        if (algo_ == GWAMD_ALIGNER_MYERS_BANDED && max_q_ > gwamd::aln::kBandChunks * gwamd::aln::kChunkWords * 32)
+            throw std::invalid_argument("max_query_length above 8192 is not supported by the banded Myers aligner.");
+        if (algo_ == GWAMD_ALIGNER_UKKONEN && ukkonen_band_rows() > gwamd::aln::kUkChunks * gwamd::aln::kWave)
+            throw std::invalid_argument("max_target_length too large for the Ukkonen aligner's band.");
         if (max_t_ > 65535)
             throw std::invalid_argument("max_target_length above 65535 is not supported by this aligner.");
         stride_     = std::max(max_q_, max_t_);
@@ -217,6 +224,9 @@ public:
     StatusType add_alignment(const char* query, int32_t query_length, const char* target, int32_t target_length,
                              bool rc_query, bool rc_target) override
     {
+        // AlignerGlobalUkkonen::add_alignment (aligner_global_ukkonen.cpp:47-57)
+        if (algo_ == GWAMD_ALIGNER_UKKONEN && std::abs(query_length - target_length) > ukkonen_max_difference())
+            return StatusType::exceeded_max_alignment_difference;
         // aligner_global.cpp:60-118
         if (query_length < 0 || target_length < 0)
             return StatusType::generic_error;
@@ -292,7 +302,10 @@ public:
         ScopedDevice dev(device_id_);
         gwamd::aln::Args a = args();
         const int grid     = std::min<int>(int(alignments_.size()), slots_);
-        GWAMD_HIP_CHECK(gwamd_internal_align_launch(&a, algo_, grid, stream_));
+        if (algo_ == GWAMD_ALIGNER_MYERS_BANDED || algo_ == GWAMD_ALIGNER_UKKONEN)
+            GWAMD_HIP_CHECK(gwamd_internal_banded_launch(&a, algo_, grid, stream_));
+        else
+            GWAMD_HIP_CHECK(gwamd_internal_align_launch(&a, algo_, grid, stream_));
     }
     void download()
     {
@@ -316,9 +329,62 @@ public:
 private:
     static int64_t a16(int64_t v) { return (v + 15) & ~int64_t(15); }
 
+    // aligner_global_ukkonen.cpp:23,32: float 0.1 times max_target_length, truncated
+    int32_t ukkonen_max_difference() const
+    {
+        return int32_t(float(max_t_) * 0.1f);
+    }
+    // ukkonen_max_score_matrix_size (ukkonen_gpu.cu:313-324): band rows for the
+    // largest allowed length difference
+    int32_t ukkonen_band_rows() const
+    {
+        return (1 + ukkonen_max_difference() + 2 * gwamd::aln::kUkkonenP + 1) / 2;
+    }
+
+    void plan_banded()
+    {
+        using namespace gwamd::aln;
+        const int pat_words = (max_q_ + kWordBits - 1) / kWordBits;
+        const int64_t ws_cap = int64_t(8) << 30; // resident workspace slots within 8 GiB
+        if (algo_ == GWAMD_ALIGNER_MYERS_BANDED)
+        {
+            lds_target_off_  = 0;
+            lds_pat_off_     = int32_t(a16(max_t_ + 16));
+            lds_tile_off_    = int32_t(lds_pat_off_ + a16(int64_t(pat_words) * 32 + 16));
+            tile_bytes_      = 24576; // 2048 (pv, mv, score) entries >= 2 band columns of 256 words
+            lds_bytes_       = lds_tile_off_ + tile_bytes_;
+            // band matrices of the widest band (the whole query): pv, mv, score
+            slot_bytes_ = a16(int64_t(pat_words) * (max_t_ + 1) * 12 + 64);
+        }
+        else
+        {
+            lds_target_off_  = 0;
+            lds_seq2_off_    = int32_t(a16(stride_ + 16));
+            lds_tile_off_    = int32_t(lds_seq2_off_ + a16(stride_ + 16));
+            tile_bytes_      = 16384; // >= 3 columns of 512 band rows
+            lds_bytes_       = lds_tile_off_ + tile_bytes_;
+            // int16 (k, l) matrix: band rows x (n + m) columns
+            slot_bytes_ = a16(int64_t(ukkonen_band_rows()) * (int64_t(max_q_) + max_t_ + 2) * 2 + 64);
+        }
+        if (lds_bytes_ > 65536)
+            throw std::invalid_argument("aligner problem size does not fit in LDS");
+        pat_words_ = pat_words;
+        int per_cu = 1, cus = 1;
+        GWAMD_HIP_CHECK(gwamd_internal_banded_occupancy(algo_, lds_bytes_, &per_cu));
+        GWAMD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
+        slots_ = std::max(1, per_cu * cus);
+        slots_ = int32_t(std::max<int64_t>(1, std::min<int64_t>(slots_, ws_cap / slot_bytes_)));
+        slots_ = std::min(slots_, max_n_);
+    }
+
     void plan()
     {
         using namespace gwamd::aln;
+        if (algo_ == GWAMD_ALIGNER_MYERS_BANDED || algo_ == GWAMD_ALIGNER_UKKONEN)
+        {
+            plan_banded();
+            return;
+        }
         const int pat_words = (max_q_ + kWordBits - 1) / kWordBits;
         lds_target_off_     = 0;
         lds_pat_off_        = int32_t(a16(max_t_ + 16));
@@ -368,6 +434,10 @@ private:
         a.lds_bytes        = lds_bytes_;
         a.pat_words        = pat_words_;
         a.scratch_bytes    = scratch_bytes_;
+        a.lds_seq2_off     = lds_seq2_off_;
+        a.lds_tile_off     = lds_tile_off_;
+        a.tile_bytes       = tile_bytes_;
+        a.ukkonen_p        = gwamd::aln::kUkkonenP;
         return a;
     }
 
@@ -378,6 +448,7 @@ private:
     int32_t stride_ = 0, max_result_ = 0;
     int32_t lds_target_off_ = 0, lds_pat_off_ = 0, lds_scratch_off_ = 0, lds_stack_off_ = 0, lds_bytes_ = 0;
     int32_t pat_words_ = 0, scratch_bytes_ = 0;
+    int32_t lds_seq2_off_ = 0, lds_tile_off_ = 0, tile_bytes_ = 0;
     int32_t slots_ = 1;
     int64_t slot_bytes_ = 0, device_bytes_ = 0;
     char* d_seqs_     = nullptr;
@@ -399,6 +470,17 @@ std::unique_ptr<Aligner> create_aligner(int32_t max_query_length, int32_t max_ta
         return std::make_unique<AlignerGlobalHip>(max_query_length, max_target_length, max_alignments,
                                                   GWAMD_ALIGNER_HIRSCHBERG_MYERS, stream, device_id);
     throw std::runtime_error("Aligner for specified type not implemented yet.");
+}
+
+std::unique_ptr<Aligner> create_global_aligner(int32_t max_query_length, int32_t max_target_length,
+                                               int32_t max_alignments, GlobalAlgorithm algorithm, hipStream_t stream,
+                                               int32_t device_id)
+{
+    const int algo = int(algorithm);
+    if (algo < GWAMD_ALIGNER_HIRSCHBERG_MYERS || algo > GWAMD_ALIGNER_UKKONEN)
+        throw std::invalid_argument("unknown aligner algorithm");
+    return std::make_unique<AlignerGlobalHip>(max_query_length, max_target_length, max_alignments, algo, stream,
+                                              device_id);
 }
 
 std::unique_ptr<Aligner> create_aligner(int32_t max_query_length, int32_t max_target_length, int32_t max_alignments,
@@ -469,7 +551,7 @@ int32_t gwamd_aligner_create(gwamd_aligner** out, int32_t max_query_length, int3
                                         "available GPU memory) or greater or equal than 0.");
         if (alignment_type != ca::AlignmentType::global_alignment)
             throw std::runtime_error("Aligner for specified type not implemented yet.");
-        if (algorithm != GWAMD_ALIGNER_HIRSCHBERG_MYERS && algorithm != GWAMD_ALIGNER_MYERS)
+        if (algorithm < GWAMD_ALIGNER_HIRSCHBERG_MYERS || algorithm > GWAMD_ALIGNER_UKKONEN)
             throw std::invalid_argument("unknown aligner algorithm");
         auto h  = std::make_unique<gwamd_aligner>();
         h->impl = std::make_unique<ca::AlignerGlobalHip>(max_query_length, max_target_length, max_alignments,

@@ -21,6 +21,11 @@ constexpr int kFullMyers  = 63;  // hirschberg_myers_switch_to_myers_size (:30)
 constexpr int kMaxChunks  = 4;   // Myers block = 64 lanes x 32 bits; up to 4 blocks per sweep
 constexpr int kLeafCols   = 512; // base-case columns kept in LDS (larger leaves use HBM)
 constexpr int kLeafColBytes = 20; // per column: pv u64, mv u64, score i32
+constexpr int kChunkWords  = 32;  // banded Myers: one reference warp of 32 words per step (myers_gpu.cu:35)
+constexpr int kBandChunks  = 8;   // banded Myers: up to 8 chunks (8192 query rows)
+constexpr int kUkChunks    = 8;   // Ukkonen: band rows k held 64 per chunk, up to 512
+constexpr int kUkkonenP    = 100; // aligner_global_ukkonen.cpp:29
+constexpr int16_t kUkMax   = 32766; // numeric_limits<int16_t>::max() - 1 (ukkonen_gpu.cu:75)
 
 // AlignmentState (cudaaligner.hpp:46-52)
 enum State : int8_t
@@ -53,6 +58,11 @@ struct Args
     int32_t lds_bytes;
     int32_t pat_words;       // ceil(max_query_length / 32)
     int32_t scratch_bytes;
+    // banded aligners (aligner_banded.hip)
+    int32_t lds_seq2_off;    // Ukkonen: the longer sequence
+    int32_t lds_tile_off;    // backtrace staging tile
+    int32_t tile_bytes;
+    int32_t ukkonen_p;       // AlignerGlobalUkkonen::ukkonen_p_ (aligner_global_ukkonen.cpp:29)
 };
 
 } // namespace aln

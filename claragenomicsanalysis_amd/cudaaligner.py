@@ -17,7 +17,7 @@ SUCCESS, UNINITIALIZED, EXCEEDED_MAX_ALIGNMENTS, EXCEEDED_MAX_LENGTH = 0, 1, 2, 
 # AlignmentState (cudaaligner.hpp:45-52)
 MATCH, MISMATCH, INSERTION, DELETION = 0, 1, 2, 3
 _STATE_STR = {MATCH: "m", MISMATCH: "mm", INSERTION: "i", DELETION: "d"}
-ALGORITHMS = {"hirschberg_myers": 0, "myers": 1}
+ALGORITHMS = {"hirschberg_myers": 0, "myers": 1, "myers_banded": 2, "ukkonen": 3}
 
 
 def _declare(L):

@@ -46,6 +46,22 @@ std::unique_ptr<Aligner> create_aligner(int32_t max_query_length, int32_t max_ta
                                         int32_t max_alignments, AlignmentType type, hipStream_t stream,
                                         int32_t device_id, int64_t max_device_memory_allocator_caching_size = -1);
 
+/// The reference's other global aligners, which its tests construct directly
+/// (cudaaligner/src/aligner_global_{myers,myers_banded,ukkonen}.hpp;
+/// Test_AlignerGlobal.cpp:181-216).  create_aligner() keeps returning the
+/// Hirschberg + Myers aligner, as in the reference.
+enum class GlobalAlgorithm : int32_t
+{
+    hirschberg_myers = 0, ///< AlignerGlobalHirschbergMyers (create_aligner's choice)
+    myers            = 1, ///< AlignerGlobalMyers: full bit-vector matrix + backtrace
+    myers_banded     = 2, ///< AlignerGlobalMyersBanded: Ukkonen-banded Myers with band doubling
+    ukkonen          = 3, ///< AlignerGlobalUkkonen: banded NW, p = 100, |q - t| <= 10% of max_target_length
+};
+
+std::unique_ptr<Aligner> create_global_aligner(int32_t max_query_length, int32_t max_target_length,
+                                               int32_t max_alignments, GlobalAlgorithm algorithm,
+                                               hipStream_t stream, int32_t device_id);
+
 } // namespace cudaaligner
 } // namespace genomeworks
 } // namespace claraparabricks

@@ -6,7 +6,9 @@
  * own FFI (pygenomeworks/genomeworks/cudaaligner/cudaaligner.pxd) binds:
  *
  *   gwamd_aligner_create          create_aligner(...)                      aligner.hpp:90,103
- *                                 (algorithm 1: AlignerGlobalMyers,        aligner_global_myers.hpp:28)
+ *                                 (algorithm 1: AlignerGlobalMyers,        aligner_global_myers.hpp:24
+ *                                  algorithm 2: AlignerGlobalMyersBanded,  aligner_global_myers_banded.hpp:24
+ *                                  algorithm 3: AlignerGlobalUkkonen)      aligner_global_ukkonen.hpp:28
  *   gwamd_aligner_destroy         ~Aligner                                 aligner.hpp:45
  *   gwamd_aligner_add_alignment   Aligner::add_alignment                   aligner.hpp:70-71
  *   gwamd_aligner_align_all       Aligner::align_all                       aligner.hpp:55
@@ -41,6 +43,8 @@ extern "C" {
 
 #define GWAMD_ALIGNER_HIRSCHBERG_MYERS 0 /* create_aligner(global_alignment) */
 #define GWAMD_ALIGNER_MYERS 1            /* AlignerGlobalMyers (full matrix) */
+#define GWAMD_ALIGNER_MYERS_BANDED 2     /* AlignerGlobalMyersBanded */
+#define GWAMD_ALIGNER_UKKONEN 3          /* AlignerGlobalUkkonen (p = 100) */
 
 typedef struct gwamd_aligner gwamd_aligner;
 

@@ -307,11 +307,460 @@ uint32_t query_pattern(const char* q, int Q, char x, int word, bool reverse)
     return r;
 }
 
+// ---------------------------------------------------------------------------
+// Banded Myers (AlignerGlobalMyersBanded, myers_gpu.cu:377-780).
+//
+// Literal restatement of the reference's word-level arithmetic: the band is a
+// column-major matrix of nwb 32-bit words per target column (pv, mv and the
+// score of each word's tracked row), processed in chunks of 32 words (one CUDA
+// warp; myers_advance_block over a chunk is one 1024-bit Myers step), with the
+// reference's boundary assumptions (+1 entering the band's top row, +1 for the
+// row that enters the diagonal band at the bottom) and its chunk hand-over
+// (the diagonal phase passes the vertical delta of the chunk's last row to the
+// next chunk, :597-611).  The backtrace reads the band exactly as
+// myers_backtrace_banded does (:377-494), including its index arithmetic at
+// the band edges (get_myers_score with C division/remainder, column-major
+// flat indexing, and PTX shift semantics: a shift count outside [0, 31]
+// yields 0).
+namespace
+{
+
+constexpr int kWB = 32; // myers::word_size
+
+struct BandMats
+{
+    int nwb = 0, cols = 0;
+    std::vector<uint32_t> pv, mv;
+    std::vector<int32_t> sc;
+    size_t at(int w, int t) const { return size_t(w) + size_t(nwb) * size_t(t); }
+};
+
+// (~1u) << b with the reference GPU's shl semantics (shift >= 32 -> 0)
+inline uint32_t shl_ptx(uint32_t x, int b) { return (b < 0 || b >= 32) ? 0u : (x << b); }
+
+// query pattern words, [word][char_idx] with char_idx 0..3 = A C T G
+// (myers_generate_query_pattern, myers_gpu.cu:127-138)
+std::vector<uint32_t> band_patterns(const char* q, int Q)
+{
+    const int nw = (Q + kWB - 1) / kWB;
+    std::vector<uint32_t> P(size_t(nw) * 4, 0u);
+    static const char letters[4] = {'A', 'C', 'T', 'G'};
+    for (int w = 0; w < nw; w++)
+        for (int L = 0; L < 4; L++)
+            P[size_t(w) * 4 + L] = query_pattern(q, Q, letters[L], w, false);
+    return P;
+}
+
+// get_query_pattern (myers_gpu.cu:140-171)
+inline uint32_t band_eq(const std::vector<uint32_t>& P, int nwq, int idx, int off, char x)
+{
+    const int ci = (int32_t(x) >> 1) & 3;
+    const int io = off / kWB, sh = off % kWB;
+    uint32_t r   = P[size_t(idx + io) * 4 + ci];
+    if (sh != 0)
+    {
+        r >>= sh;
+        if (idx + io + 1 < nwq)
+            r |= P[size_t(idx + io + 1) * 4 + ci] << (kWB - sh);
+    }
+    return r;
+}
+
+// myers_advance_block over one chunk of cnt words (myers_gpu.cu:95-125):
+// carry_in enters lane 0 only; out[l] = delta at hb[l].
+void advance_chunk(uint32_t* pv, uint32_t* mv, const uint32_t* eq_in, const uint32_t* hb, int cnt, int carry_in,
+                   int* out)
+{
+    uint32_t eq[kWB] = {}, xv[kWB] = {}, ph[kWB] = {}, mh[kWB] = {};
+    for (int l = 0; l < cnt; l++)
+    {
+        eq[l] = eq_in[l];
+        xv[l] = eq[l] | mv[l];
+    }
+    if (carry_in < 0)
+        eq[0] |= 1u;
+    uint64_t carry = 0;
+    for (int l = 0; l < cnt; l++)
+    {
+        const uint64_t s  = uint64_t(eq[l] & pv[l]) + uint64_t(pv[l]) + carry;
+        const uint32_t xh = (uint32_t(s) ^ pv[l]) | eq[l];
+        carry             = s >> 32;
+        ph[l]             = mv[l] | ~(xh | pv[l]);
+        mh[l]             = pv[l] & xh;
+        out[l]            = ((ph[l] & hb[l]) ? 1 : 0) - ((mh[l] & hb[l]) ? 1 : 0);
+    }
+    for (int l = cnt - 1; l >= 0; l--)
+    {
+        ph[l] = (ph[l] << 1) | (l > 0 ? ph[l - 1] >> 31 : 0u);
+        mh[l] = (mh[l] << 1) | (l > 0 ? mh[l - 1] >> 31 : 0u);
+    }
+    if (carry_in < 0)
+        mh[0] |= 1u;
+    if (carry_in > 0)
+        ph[0] |= 1u;
+    for (int l = 0; l < cnt; l++)
+    {
+        pv[l] = mh[l] | ~(xv[l] | ph[l]);
+        mv[l] = ph[l] & xv[l];
+    }
+}
+
+// myers_compute_scores_horizontal_band_impl (myers_gpu.cu:496-538)
+void band_horizontal(BandMats& M, const std::vector<uint32_t>& P, int nwq, const char* t, int tb, int te, int width,
+                     int po)
+{
+    const int nw = M.nwb;
+    for (int c = tb; c < te; c++)
+    {
+        int carry = 1; // worst case for the band's top row
+        for (int w0 = 0; w0 < nw; w0 += kWB)
+        {
+            const int cnt = std::min(kWB, nw - w0);
+            uint32_t pv[kWB], mv[kWB], eq[kWB], hb[kWB];
+            int out[kWB];
+            for (int l = 0; l < cnt; l++)
+            {
+                const int w = w0 + l;
+                pv[l]       = M.pv[M.at(w, c - 1)];
+                mv[l]       = M.mv[M.at(w, c - 1)];
+                hb[l]       = 1u << (w == nw - 1 ? width - (nw - 1) * kWB - 1 : kWB - 1);
+                eq[l]       = band_eq(P, nwq, w, po, t[c - 1]);
+            }
+            advance_chunk(pv, mv, eq, hb, cnt, carry, out);
+            for (int l = 0; l < cnt; l++)
+            {
+                const int w          = w0 + l;
+                M.sc[M.at(w, c)]     = M.sc[M.at(w, c - 1)] + out[l];
+                M.pv[M.at(w, c)]     = pv[l];
+                M.mv[M.at(w, c)]     = mv[l];
+            }
+            carry = cnt == kWB ? out[kWB - 1] : 0;
+        }
+    }
+}
+
+// myers_compute_scores_diagonal_band_impl (myers_gpu.cu:540-614)
+void band_diagonal(BandMats& M, const std::vector<uint32_t>& P, int nwq, const char* t, int tb, int te, int bw)
+{
+    const int nw = M.nwb;
+    for (int c = tb; c < te; c++)
+    {
+        int carry_down = 1;
+        for (int w0 = 0; w0 < nw; w0 += kWB)
+        {
+            const int cnt = std::min(kWB, nw - w0);
+            uint32_t opv[kWB], omv[kWB], pv[kWB], mv[kWB], eq[kWB], crb[kWB];
+            int out[kWB];
+            for (int l = 0; l < cnt; l++)
+            {
+                opv[l] = M.pv[M.at(w0 + l, c - 1)];
+                omv[l] = M.mv[M.at(w0 + l, c - 1)];
+            }
+            for (int l = 0; l < cnt; l++)
+            {
+                const int w = w0 + l;
+                pv[l]       = (opv[l] >> 1) | (l + 1 < cnt ? opv[l + 1] << (kWB - 1) : 0u);
+                mv[l]       = (omv[l] >> 1) | (l + 1 < cnt ? omv[l + 1] << (kWB - 1) : 0u);
+                if (l == kWB - 1 && w < nw - 1)
+                {
+                    pv[l] |= M.pv[M.at(w + 1, c - 1)] << (kWB - 1);
+                    mv[l] |= M.mv[M.at(w + 1, c - 1)] << (kWB - 1);
+                }
+                crb[l]             = 1u << (w == nw - 1 ? bw - (nw - 1) * kWB - 2 : kWB - 2);
+                const uint32_t cdb = crb[l] << 1;
+                eq[l]              = band_eq(P, nwq, w, c - tb + 1, t[c - 1]);
+                if (w == nw - 1)
+                {
+                    pv[l] |= cdb;
+                    mv[l] &= ~cdb;
+                }
+            }
+            advance_chunk(pv, mv, eq, crb, cnt, carry_down, out);
+            int cd_last = 0;
+            for (int l = 0; l < cnt; l++)
+            {
+                const int w        = w0 + l;
+                const uint32_t cdb = crb[l] << 1;
+                const int cd       = ((pv[l] & cdb) ? 1 : 0) - ((mv[l] & cdb) ? 1 : 0);
+                M.sc[M.at(w, c)]   = M.sc[M.at(w, c - 1)] + out[l] + cd;
+                M.pv[M.at(w, c)]   = pv[l];
+                M.mv[M.at(w, c)]   = mv[l];
+                cd_last            = cd;
+            }
+            carry_down = cnt == kWB ? cd_last : 0;
+        }
+    }
+}
+
+// get_myers_score (myers_gpu.cu:173-185) on the flat column-major band
+inline int32_t band_gms(const BandMats& M, int i, int j, uint32_t lem)
+{
+    const int wi   = (i - 1) / kWB;
+    const int bi   = (i - 1) % kWB;
+    const long o   = long(wi) + long(M.nwb) * long(j);
+    if (o < 0 || size_t(o) >= M.sc.size())
+        return 0; // outside the band matrix (never reached on valid inputs)
+    uint32_t mask = shl_ptx(~1u, bi);
+    if (wi == M.nwb - 1)
+        mask &= lem;
+    return M.sc[o] - __builtin_popcount(mask & M.pv[o]) + __builtin_popcount(mask & M.mv[o]);
+}
+
+// myers_backtrace_banded (myers_gpu.cu:377-494)
+int band_backtrace(const BandMats& M, int db, int de, int bw, int T, int8_t* path)
+{
+    int i = bw, j = T, pos = 0;
+    const uint32_t lem = (bw % kWB) != 0 ? (1u << (bw % kWB)) - 1u : ~0u;
+    // The reference starts from score(band_width / 32, T) (:393), one word past
+    // the band when band_width % 32 == 0 (a read of uninitialised workspace);
+    // both implementations here start from the band's last word, which is the
+    // same word in every other case.
+    int32_t s          = M.sc[M.at((bw - 1) / kWB, j)];
+    auto step_hv = [&](int32_t left, int32_t above, int32_t diag, int di_left, int di_above, int di_diag, int dj_diag) {
+        int8_t r;
+        if (left + 1 == s)
+        {
+            r = kInsertion;
+            s = left;
+            i += di_left;
+            --j;
+        }
+        else if (above + 1 == s)
+        {
+            r = kDeletion;
+            s = above;
+            i += di_above;
+        }
+        else
+        {
+            r = (diag == s) ? kMatch : kMismatch;
+            s = diag;
+            i += di_diag;
+            j += dj_diag;
+        }
+        path[pos++] = r;
+    };
+    while (j >= de)
+    {
+        const int32_t above = i <= 1 ? j : band_gms(M, i - 1, j, lem);
+        const int32_t diag  = i <= 1 ? j - 1 : band_gms(M, i - 1, j - 1, lem);
+        const int32_t left  = band_gms(M, i, j - 1, lem);
+        step_hv(left, above, diag, 0, -1, -1, -1);
+    }
+    while (j >= db)
+    {
+        const int32_t above = i <= 1 ? j : band_gms(M, i - 1, j, lem);
+        const int32_t diag  = i <= 0 ? j - 1 : band_gms(M, i, j - 1, lem);
+        const int32_t left  = band_gms(M, i + 1, j - 1, lem);
+        step_hv(left, above, diag, +1, -1, 0, -1);
+    }
+    while (i > 0 && j > 0)
+    {
+        const int32_t above = i == 1 ? j : band_gms(M, i - 1, j, lem);
+        const int32_t diag  = i == 1 ? j - 1 : band_gms(M, i - 1, j - 1, lem);
+        const int32_t left  = band_gms(M, i, j - 1, lem);
+        step_hv(left, above, diag, 0, -1, -1, -1);
+    }
+    while (i > 0)
+    {
+        path[pos++] = kDeletion;
+        --i;
+    }
+    while (j > 0)
+    {
+        path[pos++] = kInsertion;
+        --j;
+    }
+    return pos;
+}
+
+} // namespace
+
+// Banded Myers aligner (myers_banded_kernel, myers_gpu.cu:706-780): Ukkonen
+// band doubling from the estimate |T-Q| + min(T,Q)/20.  Empty sequences
+// (the reference asserts non-empty) give the all-insertion / all-deletion path.
+// Outputs the accepted band width and the number of tries when non-null.
+int myers_banded(const char* q, int Q, const char* t, int T, int8_t* path, int* band_out, int* tries_out)
+{
+    if (Q == 0 || T == 0)
+    {
+        int pos = 0;
+        for (int k = 0; k < Q; k++)
+            path[pos++] = kDeletion;
+        for (int k = 0; k < T; k++)
+            path[pos++] = kInsertion;
+        return pos;
+    }
+    const int nwq               = (Q + kWB - 1) / kWB;
+    const std::vector<uint32_t> P = band_patterns(q, Q);
+    const int dlen              = std::abs(T - Q);
+    int est                     = std::max(1, dlen + std::min(T, Q) / 20);
+    for (int tries = 1;; tries++)
+    {
+        int p  = std::min(std::min(T, Q), (est - dlen) / 2);
+        int bw = std::min(1 + 2 * p + dlen, Q);
+        if (bw % kWB == 1 && bw != Q)
+        {
+            p += 1;
+            bw = std::min(1 + 2 * p + dlen, Q);
+        }
+        BandMats M;
+        M.nwb  = (bw + kWB - 1) / kWB;
+        M.cols = T + 1;
+        M.pv.assign(size_t(M.nwb) * (T + 1), 0u);
+        M.mv.assign(size_t(M.nwb) * (T + 1), 0u);
+        M.sc.assign(size_t(M.nwb) * (T + 1), 0);
+        for (int w = 0; w < M.nwb; w++)
+        {
+            M.pv[M.at(w, 0)] = ~0u;
+            M.mv[M.at(w, 0)] = 0u;
+            M.sc[M.at(w, 0)] = std::min((w + 1) * kWB, bw);
+        }
+        int db, de;
+        if (bw >= Q)
+        {
+            db = de = T + 1;
+            band_horizontal(M, P, nwq, t, 1, T + 1, Q, 0);
+        }
+        else
+        {
+            db = Q < T ? T - Q + p + 2 : p + 2;
+            de = Q < T ? Q - p + 1 : Q - (Q - T) - p + 1;
+            band_horizontal(M, P, nwq, t, 1, db, bw, 0);
+            band_diagonal(M, P, nwq, t, db, de, bw);
+            band_horizontal(M, P, nwq, t, de, T + 1, bw, Q - bw);
+        }
+        const int ed = M.sc[M.at(M.nwb - 1, T)];
+        if (ed <= est || bw == Q)
+        {
+            if (band_out)
+                *band_out = bw;
+            if (tries_out)
+                *tries_out = tries;
+            return band_backtrace(M, db, de, bw, T, path);
+        }
+        est *= 2;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Ukkonen (AlignerGlobalUkkonen, ukkonen_gpu.cu:59-329): banded NW with unit
+// costs over the diagonals [-p, n-m+p] of the (shorter x longer) matrix, in
+// the reference's (k, l) coordinates k = (j - i + p) / 2, l = i + j, int16
+// scores with 32766 for cells outside the band.  The matrix is initialised and
+// filled exactly as ukkonen_init_score_matrix / ukkonen_compute_score_matrix_
+// {even,odd} do, and the backtrace reads it through to_band_indices with C
+// division (ukkonen_backtrace_kernel, :59-141).  Characters compare raw.
+constexpr int kUkkonenP        = 100;   // aligner_global_ukkonen.cpp:29
+constexpr int16_t kUkkonenMax  = 32766; // numeric_limits<int16_t>::max() - 1
+
+int ukkonen(const char* q, int Q, const char* t, int T, int p, int8_t* path)
+{
+    int m = Q + 1, n = T + 1;
+    const char* a = q; // along i (the shorter sequence after the swap)
+    const char* b = t; // along j
+    int8_t ins = kInsertion, del = kDeletion;
+    if (m > n)
+    {
+        std::swap(n, m);
+        std::swap(a, b);
+        std::swap(ins, del);
+    }
+    const int bw   = (1 + n - m + 2 * p + 1) / 2;
+    const int cols = n + m;
+    std::vector<int16_t> S(size_t(bw) * cols);
+    auto at = [&](int k, int l) -> int16_t& { return S[size_t(k) + size_t(bw) * size_t(l)]; };
+    for (int k = 0; k < bw; k++)
+        for (int l = 0; l < cols; l++)
+        {
+            const int j = k - (p + l) / 2 + l;
+            const int i = l - j;
+            at(k, l)    = i == 0 ? int16_t(j) : j == 0 ? int16_t(i) : kUkkonenMax;
+        }
+    const int kmax_odd  = (n - m + 2 * p - 1) / 2 + 1;
+    const int kmax_even = (n - m + 2 * p) / 2 + 1;
+    const int M         = kUkkonenMax;
+    for (int l = 0; l < cols; l++)
+    {
+        const bool even = ((l - p) & 1) == 0;
+        const int kmax  = even ? kmax_even : kmax_odd;
+        for (int k = 0; k < kmax && k < bw; k++)
+        {
+            const int d    = even ? 2 * k : 2 * k + 1; // 2k(+1) - p + p
+            const int lmin = std::abs(d - p);
+            const int lmax = d <= p ? 2 * (m - p + d) + lmin : 2 * std::min(m, n - d + p) + lmin;
+            if (!(lmin + 1 <= l && l < lmax))
+                continue;
+            const int j    = k - (p + l) / 2 + l;
+            const int i    = l - j;
+            const int diag = l - 2 < 0 ? M : at(k, l - 2) + (a[i - 1] == b[j - 1] ? 0 : 1);
+            int left, above;
+            if (even)
+            {
+                left  = (k - 1 < 0 || l - 1 < 0) ? M : at(k - 1, l - 1) + 1;
+                above = l - 1 < 0 ? M : at(k, l - 1) + 1;
+            }
+            else
+            {
+                left  = l - 1 < 0 ? M : at(k, l - 1) + 1;
+                above = (l - 1 < 0 || k + 1 >= bw) ? M : at(k + 1, l - 1) + 1;
+            }
+            at(k, l) = int16_t(std::min(diag, std::min(left, above)));
+        }
+    }
+    auto val = [&](int i, int j) -> int {
+        const int k = (j - i + p) / 2;
+        const int l = j + i;
+        return (k < 0 || k >= bw || l < 0 || l >= cols) ? M : int(at(k, l));
+    };
+    int i = m - 1, j = n - 1, pos = 0;
+    int s = val(i, j);
+    while (i > 0 && j > 0)
+    {
+        const int above = val(i - 1, j);
+        const int diag  = val(i - 1, j - 1);
+        const int left  = val(i, j - 1);
+        int8_t r;
+        if (left + 1 == s)
+        {
+            r = ins;
+            s = left;
+            --j;
+        }
+        else if (above + 1 == s)
+        {
+            r = del;
+            s = above;
+            --i;
+        }
+        else
+        {
+            r = (diag == s) ? kMatch : kMismatch;
+            s = diag;
+            --i;
+            --j;
+        }
+        path[pos++] = r;
+    }
+    while (i > 0)
+    {
+        path[pos++] = del;
+        --i;
+    }
+    while (j > 0)
+    {
+        path[pos++] = ins;
+        --j;
+    }
+    return pos;
+}
+
 } // namespace oracle_aligner
 
 extern "C" {
 
-// algo: 0 = Hirschberg-Myers (create_aligner default), 1 = full Myers.
+// algo: 0 = Hirschberg-Myers (create_aligner default), 1 = full Myers,
+// 2 = banded Myers, 3 = Ukkonen (p = 100).
 // Writes the path in emission order (end -> start, as the device kernels do;
 // the host reverses it, aligner_global.cpp:185).  Returns the length, or -1 if
 // path_cap is too small.
@@ -319,8 +768,14 @@ int oracle_align(int algo, const char* q, int qlen, const char* t, int tlen, int
                  int path_cap)
 {
     std::vector<int8_t> buf(size_t(qlen) + tlen + 8);
-    int n = algo == 0 ? oracle_aligner::hirschberg_myers(q, qlen, t, tlen, max_query_length, buf.data())
-                      : oracle_aligner::full_myers(q, qlen, t, tlen, buf.data());
+    int n = 0;
+    switch (algo)
+    {
+    case 0: n = oracle_aligner::hirschberg_myers(q, qlen, t, tlen, max_query_length, buf.data()); break;
+    case 1: n = oracle_aligner::full_myers(q, qlen, t, tlen, buf.data()); break;
+    case 2: n = oracle_aligner::myers_banded(q, qlen, t, tlen, buf.data(), nullptr, nullptr); break;
+    default: n = oracle_aligner::ukkonen(q, qlen, t, tlen, oracle_aligner::kUkkonenP, buf.data()); break;
+    }
     if (n > path_cap)
         return -1;
     std::memcpy(path, buf.data(), size_t(n));
@@ -356,6 +811,18 @@ int oracle_edit_distance(const char* q, int qlen, const char* t, int tlen)
     std::vector<int32_t> row;
     oracle_aligner::ed_last_row(q, qlen, t, tlen, false, row);
     return row[tlen];
+}
+
+// Banded Myers with the accepted band width and number of tries.
+int oracle_myers_banded(const char* q, int qlen, const char* t, int tlen, int8_t* path, int* band, int* tries)
+{
+    return oracle_aligner::myers_banded(q, qlen, t, tlen, path, band, tries);
+}
+
+// Ukkonen with an explicit p (the aligner uses 100).
+int oracle_ukkonen(const char* q, int qlen, const char* t, int tlen, int p, int8_t* path)
+{
+    return oracle_aligner::ukkonen(q, qlen, t, tlen, p, path);
 }
 
 uint32_t oracle_query_pattern(const char* q, int qlen, char x, int word, int reverse)

@@ -57,6 +57,10 @@ def _declare(L):
     L.oracle_edit_distance.restype = C.c_int
     L.oracle_edit_distance.argtypes = [C.c_char_p, i32, C.c_char_p, i32]
     L.oracle_query_pattern.restype = C.c_uint32
+    L.oracle_myers_banded.restype = C.c_int
+    L.oracle_myers_banded.argtypes = [C.c_char_p, i32, C.c_char_p, i32, vp, vp, vp]
+    L.oracle_ukkonen.restype = C.c_int
+    L.oracle_ukkonen.argtypes = [C.c_char_p, i32, C.c_char_p, i32, i32, vp]
     L.oracle_query_pattern.argtypes = [C.c_char_p, i32, C.c_char, i32, i32]
 
 
@@ -275,7 +279,8 @@ def consensus_raw(nodes, sorted_graph, aligned, outgoing, coverage, weights, max
 
 # ---------------------------------------------------------------------------
 # cudaaligner restatement (oracle/aligner_oracle.cpp)
-ALIGN_HM, ALIGN_MYERS = 0, 1
+ALIGN_HM, ALIGN_MYERS, ALIGN_MYERS_BANDED, ALIGN_UKKONEN = 0, 1, 2, 3
+UKKONEN_P = 100  # aligner_global_ukkonen.cpp:29
 _CIGAR = {0: "M", 1: "M", 2: "I", 3: "D"}
 
 
@@ -329,6 +334,23 @@ def format_alignment(query, target, states):
 def edit_distance(query, target):
     q, t = _b(query), _b(target)
     return lib().oracle_edit_distance(q, len(q), t, len(t))
+
+
+def myers_banded(query, target):
+    """Banded Myers: (states start -> end, accepted band width, tries)."""
+    q, t = _b(query), _b(target)
+    buf = np.zeros(len(q) + len(t) + 8, np.int8)
+    bw, tries = C.c_int(0), C.c_int(0)
+    n = lib().oracle_myers_banded(q, len(q), t, len(t), _p(buf), C.byref(bw), C.byref(tries))
+    return buf[:n][::-1].tolist(), bw.value, tries.value
+
+
+def ukkonen(query, target, p=UKKONEN_P):
+    """Ukkonen banded NW with band parameter p: states start -> end."""
+    q, t = _b(query), _b(target)
+    buf = np.zeros(len(q) + len(t) + 8, np.int8)
+    n = lib().oracle_ukkonen(q, len(q), t, len(t), int(p), _p(buf))
+    return buf[:n][::-1].tolist()
 
 
 def query_pattern(query, x, word, reverse=False):

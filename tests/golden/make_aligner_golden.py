@@ -83,6 +83,16 @@ def distance_cases():
     return [{"target": t, "query": q, "distance": naive_nw(t, q)} for t, q in pairs]
 
 
+def ukkonen_cases():
+    # cudaaligner/tests/Test_NeedlemanWunschImplementation.cpp:40-91: (target,
+    # query, p); the reference checks the banded score matrix against the naive
+    # one inside the band and the CPU and GPU Ukkonen backtraces against each
+    # other (:194-206, :280-286).  The distance is the naive NW's.
+    pairs = [("ACTG", "ACTG", 0), ("ACTG", "ATCG", 3), ("ACTG", "ATG", 2), ("ACTG", "", 0), ("ACTGGTCA", "ACTG", 4),
+             ("ACTG", "BDEF", 4)]
+    return [{"target": t, "query": q, "p": p, "distance": naive_nw(t, q)} for t, q, p in pairs]
+
+
 def add_cases():
     # cudaaligner/tests/Test_AlignerGlobal.cpp:58-83: aligner(10, 10, 5)
     return {"max_query_length": 10, "max_target_length": 10, "max_alignments": 5,
@@ -92,9 +102,19 @@ def add_cases():
             "final_count": 5}
 
 
+def add_cases_ukkonen():
+    # Test_AlignerGlobal.cpp:58-83 runs on AlignerGlobalUkkonen(10, 10, 5): the
+    # length-difference check (|q - t| > int(10 * 0.1f) = 1 ->
+    # exceeded_max_alignment_difference, aligner_global_ukkonen.cpp:47-57)
+    # comes before the length checks; the two over-long pairs differ by 1.
+    c = add_cases()
+    c["calls"] = c["calls"] + [["ACG", "ACGTA", 4]]
+    return c
+
+
 def main():
     data = {"cigar": cigar_cases(), "patterns": pattern_cases(), "distances": distance_cases(),
-            "add_alignment": add_cases()}
+            "add_alignment": add_cases(), "ukkonen": ukkonen_cases(), "add_alignment_ukkonen": add_cases_ukkonen()}
     with open(os.path.join(HERE, "aligner_kat.json"), "w") as f:
         json.dump(data, f, indent=1)
     print("wrote", os.path.join(HERE, "aligner_kat.json"))

@@ -13,7 +13,8 @@ from oracle import oracle
 pytestmark = pytest.mark.gpu
 
 GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "aligner_kat.json")))
-ALGOS = [("hirschberg_myers", oracle.ALIGN_HM), ("myers", oracle.ALIGN_MYERS)]
+ALGOS = [("hirschberg_myers", oracle.ALIGN_HM), ("myers", oracle.ALIGN_MYERS),
+         ("myers_banded", oracle.ALIGN_MYERS_BANDED), ("ukkonen", oracle.ALIGN_UKKONEN)]
 
 
 def run(pairs, max_q=None, max_t=None, algorithm="hirschberg_myers", rc=None):
@@ -33,10 +34,10 @@ def states(al):
 
 
 @pytest.mark.parametrize("case", GOLD["cigar"], ids=lambda c: c["source"])
-@pytest.mark.parametrize("algo", ["hirschberg_myers", "myers"])
+@pytest.mark.parametrize("algo", ["hirschberg_myers", "myers", "myers_banded", "ukkonen"])
 def test_cigar_kats(case, algo):
-    if algo == "myers" and "myers" not in case["algorithms"]:
-        pytest.skip("KAT not stated for full Myers")
+    if algo != "hirschberg_myers" and algo not in case["algorithms"]:
+        pytest.skip("KAT not stated for this aligner")
     pairs = [(p["query"], p["target"]) for p in case["pairs"]]
     _, al = run(pairs, case["max_query_length"], case["max_target_length"], algo)
     assert [a.cigar for a in al] == [p["cigar"] for p in case["pairs"]]
@@ -66,7 +67,10 @@ def _rand_pairs(seed, n, lo, hi, err):
 def test_random_pairs_match_oracle(algo, oalgo, lo, hi, err):
     pairs = _rand_pairs(lo * 7 + hi, 24 if hi < 2000 else 6, lo, hi, err)
     mq = max(len(q) for q, _ in pairs)
-    _, al = run(pairs, mq, max(len(t) for _, t in pairs), algo)
+    mt = max(len(t) for _, t in pairs)
+    if algo == "ukkonen":  # |q - t| within 10% of max_target_length (aligner_global_ukkonen.cpp:47-57)
+        pairs = [(q, t) for q, t in pairs if abs(len(q) - len(t)) <= int(mt * 0.1)]
+    _, al = run(pairs, mq, mt, algo)
     for (q, t), a in zip(pairs, al):
         assert states(a) == oracle.align(q, t, oalgo, mq), (len(q), len(t))
 
@@ -95,6 +99,8 @@ def test_edge_cases(algo, oalgo):
     pairs = [("", "ACGT"), ("ACGT", ""), ("A", "T"), ("A", "TTTA"), ("G", "ACGTGT"), ("C", "C"),
              ("ACGNNT", "ACGGGT"), ("acgt", "ACGT"), ("NNNN", "ACGT"), ("ACGT" * 20, "TTTT"),
              ("T" * 70, "T" * 69 + "A"), ("", "")]
+    if algo == "ukkonen":  # allowed length difference: int(80 * 0.1f) = 8
+        pairs = [(q, t) for q, t in pairs if abs(len(q) - len(t)) <= 8]
     _, al = run(pairs, 80, 80, algo)
     for (q, t), a in zip(pairs, al):
         assert states(a) == oracle.align(q, t, oalgo, 80), (q, t)
@@ -157,3 +163,55 @@ def test_invalid_construction():
         CudaAlignerBatch(10, 10, 1, alignment_type="local")
     with pytest.raises(ValueError):
         CudaAlignerBatch(10, 10, 1, max_device_memory_allocator_caching_size=-2)
+
+
+# --- banded Myers / Ukkonen specifics ------------------------------------------
+
+def test_banded_multichunk_and_band_growth():
+    # unrelated strings: the band doubles past 1024 rows (several 32-word
+    # chunks in the diagonal phase, myers_gpu.cu:597-611) up to the full query;
+    # query longer and shorter than the target; Q % 32 == 0 full bands
+    rng = random.Random(21)
+    pairs = []
+    for ql, tl in [(2500, 2600), (2700, 2600), (2048, 2000), (1024, 1100), (64, 64), (96, 130), (3000, 2990)]:
+        pairs.append(("".join(rng.choice("ACGT") for _ in range(ql)), "".join(rng.choice("ACGT") for _ in range(tl))))
+    _, al = run(pairs, 3000, 3000, "myers_banded")
+    for (q, t), a in zip(pairs, al):
+        assert states(a) == oracle.align(q, t, oracle.ALIGN_MYERS_BANDED), (len(q), len(t))
+
+
+@pytest.mark.parametrize("algo,oalgo", [("myers_banded", oracle.ALIGN_MYERS_BANDED), ("ukkonen", oracle.ALIGN_UKKONEN)])
+def test_banded_config_d_pairs(algo, oalgo):
+    pairs = synth.aligner_pairs(1, 16, 5000)
+    _, al = run(pairs, 5000, 5000, algo)
+    for (q, t), a in zip(pairs, al):
+        st = states(a)
+        assert st == oracle.align(q, t, oalgo), (len(q), len(t))
+        assert sum(1 for s in st if s != 0) == oracle.edit_distance(q, t)
+
+
+def test_ukkonen_swapped_and_wide_difference():
+    # query longer than target (the kernel swaps and relabels insertions and
+    # deletions, ukkonen_gpu.cu:74-79) and length differences near the 10% cap
+    rng = random.Random(8)
+    pairs = []
+    for ql, tl in [(1100, 1000), (1000, 1100), (900, 990), (1090, 1000), (1, 1), (60, 50), (0, 0)]:
+        t = "".join(rng.choice("ACGT") for _ in range(tl))
+        q = (t[: min(ql, tl)] + "".join(rng.choice("ACGT") for _ in range(max(0, ql - tl))))
+        q = "".join(c if rng.random() > 0.05 else rng.choice("ACGT") for c in q)
+        pairs.append((q, t))
+    _, al = run(pairs, 1100, 1100, "ukkonen")
+    for (q, t), a in zip(pairs, al):
+        assert states(a) == oracle.align(q, t, oracle.ALIGN_UKKONEN), (len(q), len(t))
+
+
+def test_ukkonen_add_alignment_status_codes():
+    # Test_AlignerGlobal.cpp:58-83 on AlignerGlobalUkkonen(10, 10, 5)
+    case = GOLD["add_alignment_ukkonen"]
+    b = CudaAlignerBatch(case["max_query_length"], case["max_target_length"], case["max_alignments"],
+                         algorithm="ukkonen")
+    for q, t, want in case["calls"]:
+        assert b.add_alignment(q, t) == want
+    assert b.num_alignments() == case["final_count"]
+    b.align_all()
+    assert [a.cigar for a in b.get_alignments()] == [oracle.cigar(oracle.align("ATCG", "TACG", 3))] * 5

@@ -96,3 +96,77 @@ def test_format_alignment():
     q, p, t = oracle.format_alignment("ACTGA", "GCTAG", st)
     assert len(q) == len(p) == len(t) == len(st)
     assert q.replace("-", "") == "ACTGA" and t.replace("-", "") == "GCTAG"
+
+
+# --- banded Myers and Ukkonen (myers_gpu.cu:377-780, ukkonen_gpu.cu:59-329) ---
+
+@pytest.mark.parametrize("case", [c for c in GOLD["cigar"] if "ukkonen" in c["algorithms"]],
+                         ids=lambda c: c["source"])
+def test_banded_and_ukkonen_cigar_kats(case):
+    # Test_AlignerGlobal.cpp:143-147 runs the same CIGAR vectors through
+    # AlignerGlobalMyersBanded and AlignerGlobalUkkonen
+    for p in case["pairs"]:
+        for algo in (oracle.ALIGN_MYERS_BANDED, oracle.ALIGN_UKKONEN):
+            assert oracle.cigar(oracle.align(p["query"], p["target"], algo)) == p["cigar"], (algo, p)
+
+
+@pytest.mark.parametrize("case", GOLD["ukkonen"], ids=range(len(GOLD["ukkonen"])))
+def test_ukkonen_implementation_cases(case):
+    # Test_NeedlemanWunschImplementation.cpp:40-91: with the case's p the band
+    # covers an optimal path, so the banded path costs the naive distance
+    q, t = case["query"], case["target"]
+    st = oracle.ukkonen(q, t, case["p"])
+    qi = ti = cost = 0
+    for s in st:
+        if s in (0, 1):
+            assert (s == 0) == (q[qi] == t[ti])  # Ukkonen compares raw characters
+            cost += s
+            qi += 1
+            ti += 1
+        else:
+            cost += 1
+            qi += s == 3
+            ti += s == 2
+    assert qi == len(q) and ti == len(t)
+    assert cost == case["distance"]
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_wide_bands_equal_full_myers(seed):
+    # a band covering the whole matrix reduces both banded aligners to the
+    # full-matrix recurrence with the same backtrace order: banded Myers whose
+    # accepted band is the whole query, Ukkonen (query not longer than target)
+    # with p >= both lengths
+    rng = random.Random(100 + seed)
+    for _ in range(20):
+        t = "".join(rng.choice("ACGT") for _ in range(rng.randrange(1, 90)))
+        q = "".join(rng.choice("ACGT") for _ in range(rng.randrange(1, 90)))
+        full = oracle.align(q, t, oracle.ALIGN_MYERS)
+        st, bw, _ = oracle.myers_banded(q, t)
+        if bw == len(q):
+            assert st == full, (q, t)
+        if len(q) <= len(t):
+            assert oracle.ukkonen(q, t, 200) == full, (q, t)
+        assert _cost(q, t, full) == oracle.edit_distance(q, t)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_banded_paths_are_valid(seed):
+    # band doubling (estimate |T-Q| + min/20, x2 until the band's distance is
+    # within the estimate): paths consume both strings; at the config-D error
+    # rate the first band already holds an optimal path
+    rng = random.Random(seed)
+    t = "".join(rng.choice("ACGT") for _ in range(rng.randrange(500, 3000)))
+    q = _mutate(rng, t, len(t) // 25)
+    st, bw, tries = oracle.myers_banded(q, t)
+    assert _cost(q, t, st) == oracle.edit_distance(q, t)
+    u = oracle.ukkonen(q, t)
+    assert sum(1 for s in u if s != 0) == oracle.edit_distance(q, t)
+    # unrelated strings: the band grows (several tries, multi-chunk bands)
+    t = "".join(rng.choice("ACGT") for _ in range(2600))
+    q2 = "".join(rng.choice("ACGT") for _ in range(2500 + 50 * seed))
+    st2, bw2, tries2 = oracle.myers_banded(q2, t)
+    assert tries2 > 1 and bw2 > 1024
+    # the banded backtrace labels match / mismatch by score equality
+    # (myers_gpu.cu:420-425), so only the consumption is checked here
+    assert sum(s != 2 for s in st2) == len(q2) and sum(s != 3 for s in st2) == len(t)
