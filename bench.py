@@ -33,7 +33,40 @@ ALIGNER_CONFIGS = {
     # (create_aligner default) and, separately, full Myers
     "D": dict(pairs=100000, length=5000, algorithm="hirschberg_myers"),
     "D_myers": dict(pairs=100000, length=5000, algorithm="myers"),
+    # the reference's other global aligners on the same pairs (secondary rows)
+    "D_banded": dict(pairs=100000, length=5000, algorithm="myers_banded"),
+    "D_ukkonen": dict(pairs=100000, length=5000, algorithm="ukkonen"),
 }
+
+# per algorithm: oracle id, dominant kernel
+ALIGNER_ALGOS = {
+    "hirschberg_myers": (0, "hm_kernel"),
+    "myers": (1, "myers_kernel"),
+    "myers_banded": (2, "myers_banded_kernel"),
+    "ukkonen": (3, "ukkonen_kernel"),
+}
+
+
+def aligner_alg_bytes(algorithm, q, t):
+    """Algorithmic HBM bytes of one pair (measurement): the
+    bit-vector / score state the aligner stores once per pair."""
+    Q, T = len(q), len(t)
+    if algorithm == "myers_banded":
+        # first band of myers_banded_kernel (myers_gpu.cu:749-760): pv, mv, score
+        # per band word and target column (config D pairs are accepted on it)
+        d = abs(T - Q)
+        est = max(1, d + min(T, Q) // 20)
+        p = min(T, Q, (est - d) // 2)
+        bw = min(1 + 2 * p + d, Q)
+        if bw % 32 == 1 and bw != Q:
+            bw = min(1 + 2 * (p + 1) + d, Q)
+        return ((bw + 31) // 32) * (T + 1) * 12
+    if algorithm == "ukkonen":
+        # int16 (k, l) band matrix, bw rows x (n + m) columns (ukkonen_gpu.cu:192-197)
+        m, n = min(Q, T) + 1, max(Q, T) + 1
+        return ((1 + n - m + 200 + 1) // 2) * (n + m) * 2
+    # full Myers state (SURVEY 8(d)): ceil(q/32) words x (t+1) columns x 12 B
+    return ((Q + 31) // 32) * (T + 1) * 12
 
 CONFIGS = {
     # name: (backbone, reads, mut, ins, del, max_seq, banded, band_width, windows per GPU)
@@ -124,13 +157,13 @@ def bench_aligner(args):
     b.synchronize()
     paths, plen = b.raw_paths()
     cells = sum(len(q) * len(t) for q, t in zip(qs, ts))
-    alg_bytes = sum(((len(q) + 31) // 32) * (len(t) + 1) * 12 for q, t in zip(qs, ts))
+    alg_bytes = sum(aligner_alg_bytes(cfg["algorithm"], q, t) for q, t in zip(qs, ts))
     out = None
     if rank == 0:
         from oracle import oracle
         k = min(8, n)
         ok = True
-        algo = oracle.ALIGN_HM if cfg["algorithm"] == "hirschberg_myers" else oracle.ALIGN_MYERS
+        algo = ALIGNER_ALGOS[cfg["algorithm"]][0]
         for i in range(k):
             want = oracle.align(qs[i], ts[i], algo, L)
             got = paths[i, :plen[i]][::-1].tolist()
@@ -167,7 +200,8 @@ def bench_aligner(args):
             "unit": "alignments/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(wall_max / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 bit-vectors",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "int16" if cfg["algorithm"] == "ukkonen" else "u32 bit-vectors",
             "data": "synthetic (reference genomeutils generators, seeds 1..N)",
             "config": {"workload": "cudaaligner global, %d pairs/GPU x %d bp, ~10%% difference, %s"
                                    % (n, L, cfg["algorithm"]),
@@ -177,7 +211,7 @@ def bench_aligner(args):
                        "parallelism": "dp%d (pairs sharded)" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "hm_kernel" if cfg["algorithm"] == "hirschberg_myers" else "myers_kernel",
+                         "kernel": ALIGNER_ALGOS[cfg["algorithm"]][1],
                          "kernel_ms": round(kernel_ms, 3), "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "parity": parity,

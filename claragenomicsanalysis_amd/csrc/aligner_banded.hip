@@ -123,19 +123,105 @@ __device__ __forceinline__ int chunk_step(uint32_t& pv, uint32_t& mv, uint32_t e
 
 // ---------------------------------------------------------------------------
 // Banded Myers (myers_banded_kernel, myers_gpu.cu:706-780)
+//
+// LDS: query patterns letter-major (patL[L * pat_words + k], conflict-free
+// for lanes reading consecutive words), the target as 2-bit letter codes
+// (16 per word), and one 4 KiB region that holds the per-chunk state of
+// bands wider than one chunk during the sweep and the backtrace tile after it.
+
+// Band entry of the flat column-major band matrix (entry = word + nwb *
+// column, the reference's index map): pv, mv and the score of the word's
+// tracked row, one 16-byte load or store.
+struct BandEntry
+{
+    uint32_t pv, mv;
+    int32_t sc, pad;
+};
+
+namespace
+{
+
+// LDS copies of a band entry (field-wise: address-space-qualified struct
+// assignment does not compile)
+__device__ __forceinline__ BandEntry lds_get(const GWAMD_LDS BandEntry* p)
+{
+    BandEntry e;
+    e.pv  = p->pv;
+    e.mv  = p->mv;
+    e.sc  = p->sc;
+    e.pad = 0;
+    return e;
+}
+__device__ __forceinline__ void lds_put(GWAMD_LDS BandEntry* p, const BandEntry& e)
+{
+    p->pv  = e.pv;
+    p->mv  = e.mv;
+    p->sc  = e.sc;
+    p->pad = 0;
+}
+
+__device__ void build_patterns_lm(GWAMD_LDS uint32_t* patL, int pat_words, const char* q, int Q, int lane)
+{
+    const int nw          = (Q + kWordBits - 1) / kWordBits;
+    const char letters[4] = {'A', 'C', 'T', 'G'};
+    for (int k = lane; k < nw; k += kWave)
+    {
+        uint32_t f[4] = {0, 0, 0, 0};
+        const int lim = min(Q - k * kWordBits, kWordBits);
+        for (int i = 0; i < lim; i++)
+        {
+            const char c = q[k * kWordBits + i];
+#pragma unroll
+            for (int L = 0; L < 4; L++)
+                f[L] |= (c == letters[L] ? 1u : 0u) << i;
+        }
+#pragma unroll
+        for (int L = 0; L < 4; L++)
+            patL[L * pat_words + k] = f[L];
+    }
+}
+
+// get_query_pattern (myers_gpu.cu:140-171) on the letter-major patterns; both
+// words are read unconditionally (clamped) so the two loads overlap
+__device__ __forceinline__ uint32_t band_pattern(const GWAMD_LDS uint32_t* patL, int pat_words, int nwq, int off,
+                                                 int w, int L)
+{
+    const int k  = (off >> 5) + w;
+    const int sh = off & 31;
+    const GWAMD_LDS uint32_t* row = patL + L * pat_words;
+    uint32_t lo  = row[min(k, nwq - 1)];
+    uint32_t hi  = row[min(k + 1, nwq - 1)];
+    lo           = k < nwq ? lo : 0u;
+    hi           = k + 1 < nwq ? hi : 0u;
+    return sh != 0 ? (lo >> sh) | (hi << (32 - sh)) : lo;
+}
+
+// target letter codes ("ACTG"[(c >> 1) & 3] index), 16 per word
+__device__ void pack_target(GWAMD_LDS uint32_t* tc, const char* t, int T, int lane)
+{
+    for (int k = lane; k * 16 < T; k += kWave)
+    {
+        uint32_t v    = 0;
+        const int lim = min(T - k * 16, 16);
+        for (int i = 0; i < lim; i++)
+            v |= uint32_t(letter(t[k * 16 + i])) << (2 * i);
+        tc[k] = v;
+    }
+}
+
+} // namespace
+
 __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
 {
     extern __shared__ __align__(16) uint8_t lds[];
-    const int lane          = threadIdx.x;
-    GWAMD_LDS uint8_t* base = (GWAMD_LDS uint8_t*)(lds);
-    GWAMD_LDS uint8_t* tgt  = base + a.lds_target_off;
-    GWAMD_LDS uint32_t* pat = (GWAMD_LDS uint32_t*)(base + a.lds_pat_off);
-    const int TL            = a.tile_bytes / 12; // tile elements per array
-    GWAMD_LDS uint32_t* tpv = (GWAMD_LDS uint32_t*)(base + a.lds_tile_off);
-    GWAMD_LDS uint32_t* tmv = tpv + TL;
-    GWAMD_LDS int32_t* tsc  = (GWAMD_LDS int32_t*)(tmv + TL);
-    uint8_t* ws             = a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes);
-    const bool chunk_lane   = lane < kChunkWords;
+    const int lane           = threadIdx.x;
+    GWAMD_LDS uint8_t* base  = (GWAMD_LDS uint8_t*)(lds);
+    GWAMD_LDS uint32_t* tcod = (GWAMD_LDS uint32_t*)(base + a.lds_target_off);
+    GWAMD_LDS uint32_t* patL = (GWAMD_LDS uint32_t*)(base + a.lds_pat_off);
+    GWAMD_LDS BandEntry* reg = (GWAMD_LDS BandEntry*)(base + a.lds_tile_off); // chunk state / tile
+    const int TLE            = a.tile_bytes / int(sizeof(BandEntry));
+    BandEntry* E             = reinterpret_cast<BandEntry*>(a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes));
+    const int pw_stride      = a.pat_words;
 
     for (int idx = blockIdx.x; idx < a.n; idx += gridDim.x)
     {
@@ -153,17 +239,19 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                 a.path_len[idx] = pw.overflow ? -1 : pw.pos;
             continue;
         }
-        for (int k = lane; k < T; k += kWave)
-            tgt[k] = uint8_t(tg[k]);
-        build_patterns(pat, q, Q, lane);
+        wave_sync();
+        pack_target(tcod, tg, T, lane);
+        build_patterns_lm(patL, pw_stride, q, Q, lane);
         wave_sync();
         const int nwq  = (Q + kWordBits - 1) / kWordBits;
         const int dlen = Q > T ? Q - T : T - Q;
         int est        = max(1, dlen + min(T, Q) / 20); // initial_distance_guess_factor (:36, :749)
         int bw = 0, nwb = 0, db = 0, de = 0;
-        uint32_t* wpv = nullptr;
-        uint32_t* wmv = nullptr;
-        int32_t* wsc  = nullptr;
+        // letter code of target column t (1-based)
+        auto code_of = [&](int t) -> int {
+            const uint32_t w = uniu(tcod[(t - 1) >> 4]);
+            return int((w >> (2 * ((t - 1) & 15))) & 3u);
+        };
         while (true)
         {
             int p = min(min(T, Q), (est - dlen) / 2);
@@ -175,9 +263,6 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
             }
             nwb           = (bw + kWordBits - 1) / kWordBits;
             const int nch = uni((nwb + kChunkWords - 1) / kChunkWords);
-            wpv           = reinterpret_cast<uint32_t*>(ws);
-            wmv           = wpv + size_t(nwb) * (T + 1);
-            wsc           = reinterpret_cast<int32_t*>(wmv + size_t(nwb) * (T + 1));
             if (bw >= Q)
                 db = de = T + 1;
             else
@@ -185,231 +270,245 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                 db = Q < T ? T - Q + p + 2 : p + 2;
                 de = Q < T ? Q - p + 1 : Q - (Q - T) - p + 1;
             }
-            const int lastw      = nwb - 1;
-            const int top_last   = bw - lastw * kWordBits; // rows of the last word
-            uint32_t pv[kBandChunks], mv[kBandChunks];
-            int sc[kBandChunks];
-            uint64_t act[kBandChunks];
-#pragma unroll
-            for (int c = 0; c < kBandChunks; c++)
+            const int lastw    = nwb - 1;
+            const int top_last = bw - lastw * kWordBits; // rows of the last word (>= 2 when banded)
+            // pattern offset of column t: 0 (top stripe), t - db + 1 (diagonal
+            // band), Q - bw (bottom stripe)
+            auto col_off = [&](int t) { return t < db ? 0 : (t < de ? t - db + 1 : Q - bw); };
+            int ed       = 0;
+            if (nch == 1)
             {
-                const int w  = c * kChunkWords + lane;
-                const bool v = chunk_lane && c < nch && w < nwb;
-                act[c]       = ballot(v);
-                pv[c]        = ~0u;
-                mv[c]        = 0u;
-                sc[c]        = min((w + 1) * kWordBits, bw);
-                if (v)
+                // one chunk: the band's words live in lanes 0..nwb-1 for the whole sweep
+                const bool act_l   = lane < nwb;
+                const uint64_t act = ballot(act_l);
+                const bool is_last = lane == lastw;
+                const uint32_t hbH = is_last ? 1u << (top_last - 1) : 0x80000000u;
+                const uint32_t crb = is_last ? 1u << max(top_last - 2, 0) : 0x40000000u;
+                const uint32_t cdb = crb << 1;
+                uint32_t pv = ~0u, mv = 0u;
+                int sc      = min((lane + 1) * kWordBits, bw);
+                if (act_l)
+                    E[lane] = BandEntry{pv, mv, sc, 0};
+                uint32_t eqn = band_pattern(patL, pw_stride, nwq, col_off(1), lane, code_of(1));
+                for (int t = 1; t <= T; t++)
                 {
-                    wpv[w] = ~0u;
-                    wmv[w] = 0u;
-                    wsc[w] = sc[c];
-                }
-            }
-            int tv = 0;
-            for (int t = 1; t <= T; t++)
-            {
-                const int tl = (t - 1) & (kWave - 1);
-                if (tl == 0)
-                {
-                    const int x = t - 1 + lane;
-                    tv          = x < T ? int(tgt[x]) : 0;
-                }
-                const int code  = letter(uni(__builtin_amdgcn_readlane(tv, tl)));
-                const bool diag = t >= db && t < de;
-                if (!diag)
-                {
-                    // horizontal stripe (myers_compute_scores_horizontal_band_impl, :496-538)
-                    const int po = t >= de ? Q - bw : 0;
-                    int carry    = 1; // worst case for the band's top row
-#pragma unroll
-                    for (int c = 0; c < kBandChunks; c++)
+                    const uint32_t eq = eqn;
+                    if (t < T) // next column's pattern word, in flight during this one
+                        eqn = band_pattern(patL, pw_stride, nwq, col_off(t + 1), lane, code_of(t + 1));
+                    if (t < db || t >= de)
                     {
-                        if (c < nch)
-                        {
-                            const int w         = c * kChunkWords + lane;
-                            const uint32_t eq   = seg_pattern(pat, nwq, po, w, code);
-                            const uint32_t hbit = 1u << (w == lastw ? top_last - 1 : kWordBits - 1);
-                            const int out       = chunk_step(pv[c], mv[c], eq, carry, hbit, act[c], lane);
-                            sc[c] += out;
-                            if ((act[c] >> lane) & 1u)
-                            {
-                                const size_t o = size_t(t) * nwb + w;
-                                wpv[o]         = pv[c];
-                                wmv[o]         = mv[c];
-                                wsc[o]         = sc[c];
-                            }
-                            carry = uni(__builtin_amdgcn_readlane(out, kChunkWords - 1));
-                        }
+                        // horizontal stripe (myers_compute_scores_horizontal_band_impl, :496-538)
+                        sc += chunk_step(pv, mv, eq, 1, hbH, act, lane);
                     }
-                }
-                else
-                {
-                    // diagonal band (myers_compute_scores_diagonal_band_impl, :540-614)
-                    const int po   = t - db + 1;
-                    int carry_down = 1;
-#pragma unroll
-                    for (int c = 0; c < kBandChunks; c++)
+                    else
                     {
-                        if (c < nch)
+                        // diagonal band (myers_compute_scores_diagonal_band_impl, :540-614):
+                        // the previous column moves up one row; the new bottom row
+                        // has no left neighbour and is assumed +1
+                        const uint32_t PB = uint32_t(ballot(pv & 1u) & act);
+                        const uint32_t MB = uint32_t(ballot(mv & 1u) & act);
+                        uint32_t p2       = (pv >> 1) | (bit_of(PB >> 1, lane) << 31);
+                        uint32_t m2       = (mv >> 1) | (bit_of(MB >> 1, lane) << 31);
+                        if (is_last)
                         {
-                            const int w = c * kChunkWords + lane;
-                            // shift the previous column down one row across the chunk
-                            const uint32_t PB = uint32_t(ballot(pv[c] & 1u) & act[c]);
-                            const uint32_t MB = uint32_t(ballot(mv[c] & 1u) & act[c]);
-                            uint32_t p2       = (pv[c] >> 1) | (bit_of(PB >> 1, lane) << 31);
-                            uint32_t m2       = (mv[c] >> 1) | (bit_of(MB >> 1, lane) << 31);
-                            if (c + 1 < kBandChunks && c + 1 < nch)
+                            p2 |= cdb;
+                            m2 &= ~cdb;
+                        }
+                        const int right = chunk_step(p2, m2, eq, 1, crb, act, lane);
+                        const int down  = int((p2 & cdb) != 0u) - int((m2 & cdb) != 0u);
+                        pv              = p2;
+                        mv              = m2;
+                        sc += right + down;
+                    }
+                    if (act_l)
+                        E[size_t(t) * nwb + lane] = BandEntry{pv, mv, sc, 0};
+                }
+                ed = uni(__builtin_amdgcn_readlane(sc, lastw));
+            }
+            else
+            {
+                // wider bands: chunk c (words 32c..32c+31) in lanes 0..31 in turn,
+                // its state in LDS between columns
+                for (int w = lane; w < nwb; w += kWave)
+                {
+                    const BandEntry e0{~0u, 0u, min((w + 1) * kWordBits, bw), 0};
+                    lds_put(reg + w, e0);
+                    E[w] = e0;
+                }
+                wave_sync();
+                for (int t = 1; t <= T; t++)
+                {
+                    const int code  = code_of(t);
+                    const int off   = col_off(t);
+                    const bool diag = t >= db && t < de;
+                    int carry       = 1; // +1 into the band's top row
+                    for (int c = 0; c < nch; c++)
+                    {
+                        const int w        = c * kChunkWords + lane;
+                        const bool valid   = lane < kChunkWords && w < nwb;
+                        const uint64_t act = ballot(valid);
+                        const BandEntry e  = lds_get(reg + (valid ? w : 0));
+                        uint32_t pv = e.pv, mv = e.mv;
+                        int sc            = e.sc;
+                        const uint32_t eq = band_pattern(patL, pw_stride, nwq, off, w, code);
+                        const bool last   = w == lastw;
+                        int hout;
+                        if (!diag)
+                        {
+                            const uint32_t hb = last ? 1u << (top_last - 1) : 0x80000000u;
+                            hout              = chunk_step(pv, mv, eq, carry, hb, act, lane);
+                            sc += hout;
+                        }
+                        else
+                        {
+                            const uint32_t PB = uint32_t(ballot(pv & 1u) & act);
+                            const uint32_t MB = uint32_t(ballot(mv & 1u) & act);
+                            uint32_t p2       = (pv >> 1) | (bit_of(PB >> 1, lane) << 31);
+                            uint32_t m2       = (mv >> 1) | (bit_of(MB >> 1, lane) << 31);
+                            if (c + 1 < nch)
                             {
-                                // word 31 takes bit 0 of the next chunk's first word (:567-573)
-                                const uint32_t np = uint32_t(ballot(pv[c + 1] & 1u)) & 1u;
-                                const uint32_t nm = uint32_t(ballot(mv[c + 1] & 1u)) & 1u;
+                                // word 31 takes bit 0 of the next chunk's first word,
+                                // still the previous column's (:567-573)
+                                const BandEntry nx = lds_get(reg + (c + 1) * kChunkWords);
                                 if (lane == kChunkWords - 1)
                                 {
-                                    p2 |= np << 31;
-                                    m2 |= nm << 31;
+                                    p2 |= (nx.pv & 1u) << 31;
+                                    m2 |= (nx.mv & 1u) << 31;
                                 }
                             }
-                            const uint32_t crb = 1u << (w == lastw ? top_last - 2 : kWordBits - 2);
+                            const uint32_t crb = last ? 1u << max(top_last - 2, 0) : 0x40000000u;
                             const uint32_t cdb = crb << 1;
-                            const uint32_t eq  = seg_pattern(pat, nwq, po, w, code);
-                            if (w == lastw)
+                            if (last)
                             {
-                                // no left neighbour for the new bottom row: assume +1
                                 p2 |= cdb;
                                 m2 &= ~cdb;
                             }
-                            const int right = chunk_step(p2, m2, eq, carry_down, crb, act[c], lane);
-                            const int down  = int((p2 & cdb) != 0u) - int((m2 & cdb) != 0u);
-                            pv[c]           = p2;
-                            mv[c]           = m2;
-                            sc[c] += right + down;
-                            if ((act[c] >> lane) & 1u)
-                            {
-                                const size_t o = size_t(t) * nwb + w;
-                                wpv[o]         = p2;
-                                wmv[o]         = m2;
-                                wsc[o]         = sc[c];
-                            }
-                            carry_down = uni(__builtin_amdgcn_readlane(down, kChunkWords - 1));
+                            const int right = chunk_step(p2, m2, eq, carry, crb, act, lane);
+                            hout            = int((p2 & cdb) != 0u) - int((m2 & cdb) != 0u);
+                            pv              = p2;
+                            mv              = m2;
+                            sc += right + hout;
+                        }
+                        // chunk hand-over: horizontal delta (stripes) or vertical
+                        // delta (diagonal band) of the chunk's last word (:527-532, :605-611)
+                        carry = uni(__builtin_amdgcn_readlane(hout, kChunkWords - 1));
+                        if (valid)
+                        {
+                            const BandEntry o{pv, mv, sc, 0};
+                            lds_put(reg + w, o);
+                            E[size_t(t) * nwb + w] = o;
                         }
                     }
                 }
+                wave_sync();
+                ed = uni(lds_get(reg + lastw).sc);
             }
-            // edit distance of the band: the last word's tracked row at column T
-            int ed = 0;
-#pragma unroll
-            for (int c = 0; c < kBandChunks; c++)
-                if (c == lastw / kChunkWords)
-                    ed = uni(__builtin_amdgcn_readlane(sc[c], lastw % kChunkWords));
             if (ed <= est || bw == Q)
                 break;
             est *= 2;
         }
         __threadfence_block();
         wave_sync();
+#ifdef GWAMD_ALN_NO_BACKTRACE // timing experiment only: forward sweep alone
+        if (lane == 0)
+            a.path_len[idx] = 0;
+        continue;
+#endif
 
-        // backtrace (myers_backtrace_banded, :377-494) over an LDS tile of the
-        // flat band arrays
+        // backtrace (myers_backtrace_banded, :377-494): the three neighbour
+        // scores of a step are evaluated by lanes 0..2 (get_myers_score,
+        // :173-185) from an LDS tile of the band columns j-1..j
         const int64_t total = int64_t(nwb) * (T + 1);
-        int64_t tb          = -1; // flat index of tile element 0
-        int64_t te          = -1;
+        const bool use_tile = 2 * nwb <= TLE;
+        int64_t tb = 0, te = 0; // tile holds flat entries [tb, te)
         auto refill = [&](int jcol) {
             const int64_t hi = min<int64_t>(total, int64_t(nwb) * (jcol + 1));
-            int64_t lo       = max<int64_t>(0, hi - TL);
+            const int64_t lo = max<int64_t>(0, hi - TLE);
             wave_sync();
             for (int64_t e = lane; e < hi - lo; e += kWave)
-            {
-                tpv[e] = wpv[lo + e];
-                tmv[e] = wmv[lo + e];
-                tsc[e] = wsc[lo + e];
-            }
+                lds_put(reg + e, E[lo + e]);
             wave_sync();
             tb = lo;
             te = hi;
         };
         const uint32_t lem = (bw % kWordBits) != 0 ? (1u << (bw % kWordBits)) - 1u : ~0u;
-        auto gms           = [&](int i, int j) -> int {
-            const int wi    = (i - 1) / kWordBits;
-            const int bi    = (i - 1) % kWordBits;
-            const int64_t o = int64_t(wi) + int64_t(nwb) * j;
-            if (o < 0 || o >= total)
-                return 0; // outside the band matrix (the oracle does the same)
-            int s;
-            uint32_t p, n;
-            if (o >= tb && o < te)
+        const int bl       = min(lane, 2);
+        int i = bw, j = T;
+        if (use_tile)
+            refill(j);
+        // start from the band's last word: the reference reads word
+        // band_width / 32 (:393), one past the band when band_width % 32 == 0
+        int s = uni(E[int64_t((bw - 1) / kWordBits) + int64_t(nwb) * j].sc);
+        while (j > 0 && (i > 0 || j >= db))
+        {
+            const int phase = j >= de ? 3 : (j >= db ? 2 : 1);
+            if (use_tile && int64_t(nwb) * (j - 1) < tb)
+                refill(j);
+            // lane 0: above, lane 1: diagonal, lane 2: left
+            int gi, gj, spv;
+            bool special;
+            if (bl == 0)
             {
-                s = tsc[o - tb];
-                p = tpv[o - tb];
-                n = tmv[o - tb];
+                gi      = i - 1;
+                gj      = j;
+                special = i <= 1;
+                spv     = j;
+            }
+            else if (bl == 1)
+            {
+                gi      = phase == 2 ? i : i - 1;
+                gj      = j - 1;
+                special = phase == 2 ? i <= 0 : i <= 1;
+                spv     = j - 1;
             }
             else
             {
-                s = wsc[o];
-                p = wpv[o];
-                n = wmv[o];
+                gi      = phase == 2 ? i + 1 : i;
+                gj      = j - 1;
+                special = false;
+                spv     = 0;
             }
+            const int wi    = (gi - 1) / kWordBits;
+            const int bi    = (gi - 1) % kWordBits;
+            const int64_t o = int64_t(wi) + int64_t(nwb) * gj;
+            const bool inr  = o >= 0 && o < total;
+            BandEntry e{0u, 0u, 0, 0};
+            if (o >= tb && o < te)
+                e = lds_get(reg + (o - tb));
+            else if (inr)
+                e = E[o];
             uint32_t mask = shl_ptx(~1u, bi);
             if (wi == nwb - 1)
                 mask &= lem;
-            return uni(s - __builtin_popcount(mask & uniu(p)) + __builtin_popcount(mask & uniu(n)));
-        };
-        int i = bw, j = T;
-        refill(j);
-        // start from the band's last word: the reference reads word
-        // band_width / 32 (:393), one past the band when band_width % 32 == 0
-        int s = uni(wsc[int64_t((bw - 1) / kWordBits) + int64_t(nwb) * j]);
-        auto ensure = [&](int jj) {
-            if (int64_t(nwb) * (jj - 1) < tb)
-                refill(jj);
-        };
-        auto choose = [&](int left, int above, int diag, int di_left, int di_above, int di_diag, int dj_diag) {
+            int v = e.sc - __builtin_popcount(mask & e.pv) + __builtin_popcount(mask & e.mv);
+            v     = special ? spv : (inr ? v : 0);
+            const int above = uni(__builtin_amdgcn_readlane(v, 0));
+            const int dg    = uni(__builtin_amdgcn_readlane(v, 1));
+            const int left  = uni(__builtin_amdgcn_readlane(v, 2));
             int8_t r;
             if (left + 1 == s)
             {
                 r = kInsertion;
                 s = left;
-                i += di_left;
+                if (phase == 2)
+                    ++i;
                 --j;
             }
             else if (above + 1 == s)
             {
                 r = kDeletion;
                 s = above;
-                i += di_above;
+                --i;
             }
             else
             {
-                r = diag == s ? kMatch : kMismatch;
-                s = diag;
-                i += di_diag;
-                j += dj_diag;
+                r = dg == s ? kMatch : kMismatch;
+                s = dg;
+                if (phase != 2)
+                    --i;
+                --j;
             }
             pw.put(r, lane);
-        };
-        while (j >= de)
-        {
-            ensure(j);
-            const int above = i <= 1 ? j : gms(i - 1, j);
-            const int dg    = i <= 1 ? j - 1 : gms(i - 1, j - 1);
-            const int left  = gms(i, j - 1);
-            choose(left, above, dg, 0, -1, -1, -1);
-        }
-        while (j >= db)
-        {
-            ensure(j);
-            const int above = i <= 1 ? j : gms(i - 1, j);
-            const int dg    = i <= 0 ? j - 1 : gms(i, j - 1);
-            const int left  = gms(i + 1, j - 1);
-            choose(left, above, dg, +1, -1, 0, -1);
-        }
-        while (i > 0 && j > 0)
-        {
-            ensure(j);
-            const int above = i == 1 ? j : gms(i - 1, j);
-            const int dg    = i == 1 ? j - 1 : gms(i - 1, j - 1);
-            const int left  = gms(i, j - 1);
-            choose(left, above, dg, 0, -1, -1, -1);
         }
         pw.finish(lane);
         pw.fill(kDeletion, max(i, 0), lane);
@@ -550,6 +649,11 @@ __global__ void __launch_bounds__(kWave) ukkonen_kernel(Args a)
         }
         __threadfence_block();
         wave_sync();
+#ifdef GWAMD_ALN_NO_BACKTRACE
+        if (lane == 0)
+            a.path_len[idx] = 0;
+        continue;
+#endif
 
         // backtrace over an LDS tile of the flat matrix
         const int64_t total = int64_t(bw) * cols;
@@ -574,19 +678,23 @@ __global__ void __launch_bounds__(kWave) ukkonen_kernel(Args a)
             if (k < 0 || k >= bw || l < 0 || l >= cols)
                 return M;
             const int64_t o = int64_t(k) + int64_t(bw) * l;
-            return uni(o >= tb && o < te ? int(tile[o - tb]) : int(S[o]));
+            return o >= tb && o < te ? int(tile[o - tb]) : int(S[o]);
         };
         PathWriter pw{a.paths + size_t(idx) * a.max_path_length, a.max_path_length};
         int i = m - 1, j = n - 1;
         refill(i + j);
-        int s = val(i, j);
+        int s = uni(val(i, j));
+        // lane 0: above (i-1, j), lane 1: diagonal (i-1, j-1), lane 2: left (i, j-1)
+        const int di = lane == 2 ? 0 : 1;
+        const int dj = lane == 0 ? 0 : 1;
         while (i > 0 && j > 0)
         {
             if (int64_t(bw) * (i + j - 2) < tb)
                 refill(i + j);
-            const int above = val(i - 1, j);
-            const int dg    = val(i - 1, j - 1);
-            const int left  = val(i, j - 1);
+            const int v     = val(i - di, j - dj);
+            const int above = uni(__builtin_amdgcn_readlane(v, 0));
+            const int dg    = uni(__builtin_amdgcn_readlane(v, 1));
+            const int left  = uni(__builtin_amdgcn_readlane(v, 2));
             int8_t r;
             if (left + 1 == s)
             {

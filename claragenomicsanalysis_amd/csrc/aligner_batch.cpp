@@ -195,16 +195,18 @@ public:
         max_result_ = (max_q_ + max_t_ + 3) / 4 * 4; // calc_max_result_length (aligner_global.cpp:26-31)
         ScopedDevice dev(device_id_);
         plan();
-        auto dalloc = [&](void** p, size_t bytes) {
+        auto dalloc = [&](void** p, size_t bytes, bool zero = true) {
             GWAMD_HIP_CHECK(hipMalloc(p, std::max<size_t>(bytes, 16)));
-            GWAMD_HIP_CHECK(hipMemsetAsync(*p, 0, std::max<size_t>(bytes, 16), stream_));
+            if (zero)
+                GWAMD_HIP_CHECK(hipMemsetAsync(*p, 0, std::max<size_t>(bytes, 16), stream_));
             device_bytes_ += int64_t(bytes);
         };
         dalloc(reinterpret_cast<void**>(&d_seqs_), size_t(2) * stride_ * max_n_ + 16);
         dalloc(reinterpret_cast<void**>(&d_lens_), size_t(2) * max_n_ * 4);
         dalloc(reinterpret_cast<void**>(&d_paths_), size_t(max_result_) * max_n_ + 16);
         dalloc(reinterpret_cast<void**>(&d_plen_), size_t(max_n_) * 4);
-        dalloc(reinterpret_cast<void**>(&d_ws_), size_t(slots_) * size_t(slot_bytes_));
+        // workspace: every slot entry is written before it is read
+        dalloc(reinterpret_cast<void**>(&d_ws_), size_t(slots_) * size_t(slot_bytes_), false);
         h_seqs_.reserve(size_t(2) * stride_ * max_n_ + 16, stream_);
         h_lens_.reserve(size_t(2) * max_n_ * 4, stream_);
         h_paths_.reserve(size_t(max_result_) * max_n_ + 16, stream_);
@@ -345,23 +347,25 @@ private:
     {
         using namespace gwamd::aln;
         const int pat_words = (max_q_ + kWordBits - 1) / kWordBits;
-        const int64_t ws_cap = int64_t(8) << 30; // resident workspace slots within 8 GiB
+        const int64_t ws_cap = int64_t(64) << 30; // resident workspace slots within 64 GiB of the 288 GB HBM
         if (algo_ == GWAMD_ALIGNER_MYERS_BANDED)
         {
+            // target as 2-bit letter codes, letter-major query patterns, and a
+            // 4 KiB chunk-state / backtrace tile
             lds_target_off_  = 0;
-            lds_pat_off_     = int32_t(a16(max_t_ + 16));
-            lds_tile_off_    = int32_t(lds_pat_off_ + a16(int64_t(pat_words) * 32 + 16));
-            tile_bytes_      = 24576; // 2048 (pv, mv, score) entries >= 2 band columns of 256 words
+            lds_pat_off_     = int32_t(a16((max_t_ + 15) / 16 * 4 + 16));
+            lds_tile_off_    = int32_t(lds_pat_off_ + a16(int64_t(pat_words) * 16 + 16));
+            tile_bytes_      = 4096; // 256 16-byte band entries: two columns of 128 words, or 256 chunk words
             lds_bytes_       = lds_tile_off_ + tile_bytes_;
-            // band matrices of the widest band (the whole query): pv, mv, score
-            slot_bytes_ = a16(int64_t(pat_words) * (max_t_ + 1) * 12 + 64);
+            // band entries (pv, mv, score, pad) of the widest band (the whole query)
+            slot_bytes_ = a16(int64_t(pat_words) * (max_t_ + 1) * 16 + 64);
         }
         else
         {
             lds_target_off_  = 0;
             lds_seq2_off_    = int32_t(a16(stride_ + 16));
             lds_tile_off_    = int32_t(lds_seq2_off_ + a16(stride_ + 16));
-            tile_bytes_      = 16384; // >= 3 columns of 512 band rows
+            tile_bytes_      = 8192; // 4096 int16 >= 3 columns of 512 band rows
             lds_bytes_       = lds_tile_off_ + tile_bytes_;
             // int16 (k, l) matrix: band rows x (n + m) columns
             slot_bytes_ = a16(int64_t(ukkonen_band_rows()) * (int64_t(max_q_) + max_t_ + 2) * 2 + 64);
