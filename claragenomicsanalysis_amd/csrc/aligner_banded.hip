@@ -196,19 +196,6 @@ __device__ __forceinline__ uint32_t band_pattern(const GWAMD_LDS uint32_t* patL,
     return sh != 0 ? (lo >> sh) | (hi << (32 - sh)) : lo;
 }
 
-// target letter codes ("ACTG"[(c >> 1) & 3] index), 16 per word
-__device__ void pack_target(GWAMD_LDS uint32_t* tc, const char* t, int T, int lane)
-{
-    for (int k = lane; k * 16 < T; k += kWave)
-    {
-        uint32_t v    = 0;
-        const int lim = min(T - k * 16, 16);
-        for (int i = 0; i < lim; i++)
-            v |= uint32_t(letter(t[k * 16 + i])) << (2 * i);
-        tc[k] = v;
-    }
-}
-
 } // namespace
 
 __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)

@@ -343,6 +343,21 @@ private:
         return (1 + ukkonen_max_difference() + 2 * gwamd::aln::kUkkonenP + 1) / 2;
     }
 
+    // GWAMD_ALIGNER_GRID (diagnostic): resident workgroups per CU instead of
+    // the occupancy query's answer
+    void apply_grid_override()
+    {
+        const char* env = std::getenv("GWAMD_ALIGNER_GRID");
+        if (!env || !*env)
+            return;
+        const int per_cu = std::atoi(env);
+        if (per_cu < 1 || per_cu > 32)
+            throw std::invalid_argument("GWAMD_ALIGNER_GRID must be 1..32 workgroups per CU");
+        int cus = 1;
+        GWAMD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
+        slots_ = per_cu * cus;
+    }
+
     void plan_banded()
     {
         using namespace gwamd::aln;
@@ -378,6 +393,7 @@ private:
         GWAMD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
         slots_ = std::max(1, per_cu * cus);
         slots_ = int32_t(std::max<int64_t>(1, std::min<int64_t>(slots_, ws_cap / slot_bytes_)));
+        apply_grid_override();
         slots_ = std::min(slots_, max_n_);
     }
 
@@ -391,11 +407,13 @@ private:
         }
         const int pat_words = (max_q_ + kWordBits - 1) / kWordBits;
         lds_target_off_     = 0;
-        lds_pat_off_        = int32_t(a16(max_t_ + 16));
+        // Hirschberg-Myers: target as 2-bit letter codes; full Myers: bytes
+        lds_pat_off_        = int32_t(algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS ? a16((max_t_ + 15) / 16 * 4 + 16)
+                                                                              : a16(max_t_ + 16));
         lds_scratch_off_    = int32_t(lds_pat_off_ + a16(int64_t(pat_words) * 32 + 16));
         scratch_bytes_      = 0;
-        if (algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS)
-            scratch_bytes_ = int32_t(a16(std::max<int64_t>(int64_t(max_t_ + 1) * 2, int64_t(kLeafCols) * kLeafColBytes)));
+        if (algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS) // LDS base case + LDS split scores
+            scratch_bytes_ = int32_t(a16(int64_t(kLeafCols) * kLeafColBytes + 2 * kSplitLds * 2));
         lds_stack_off_ = lds_scratch_off_ + scratch_bytes_;
         lds_bytes_     = lds_stack_off_ + (algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS ? kStackSize * 16 : 0);
         if (lds_bytes_ > 65536)
@@ -406,7 +424,8 @@ private:
         GWAMD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
         slots_ = std::max(1, per_cu * cus);
         if (algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS)
-            slot_bytes_ = a16(int64_t(max_t_ + 1) * 20 + 64); // base cases too wide for LDS
+            // base cases too wide for LDS, then the split scores of wide segments
+            slot_bytes_ = a16(a16(int64_t(stride_ + 1) * kLeafColBytes) + int64_t(stride_ + 1) * 4 + 64);
         else
         {
             // full matrix: pv, mv, score per (word, column)
@@ -414,6 +433,7 @@ private:
             const int64_t cap = int64_t(4) << 30; // keep the resident slots within 4 GiB
             slots_            = int32_t(std::max<int64_t>(1, std::min<int64_t>(slots_, cap / slot_bytes_)));
         }
+        apply_grid_override();
         slots_ = std::min(slots_, max_n_);
     }
 

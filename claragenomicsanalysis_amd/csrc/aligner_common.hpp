@@ -19,7 +19,8 @@ constexpr int kWordBits   = 32;  // Myers word (hirschbergmyers::WordType, uint3
 constexpr int kStackSize  = 64;  // hirschberg_myers_stackbuffer_size (aligner_global_hirschberg_myers.cpp:29)
 constexpr int kFullMyers  = 63;  // hirschberg_myers_switch_to_myers_size (:30)
 constexpr int kMaxChunks  = 4;   // Myers block = 64 lanes x 32 bits; up to 4 blocks per sweep
-constexpr int kLeafCols   = 512; // base-case columns kept in LDS (larger leaves use HBM)
+constexpr int kLeafCols   = 128; // base-case columns kept in LDS (larger leaves use HBM)
+constexpr int kSplitLds   = 512; // split segments up to this many columns keep their scores in LDS
 constexpr int kLeafColBytes = 20; // per column: pv u64, mv u64, score i32
 constexpr int kChunkWords  = 32;  // banded Myers: one reference warp of 32 words per step (myers_gpu.cu:35)
 constexpr int kBandChunks  = 8;   // banded Myers: up to 8 chunks (8192 query rows)

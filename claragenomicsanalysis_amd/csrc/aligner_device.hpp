@@ -86,5 +86,23 @@ __device__ __forceinline__ uint32_t seg_pattern(const GWAMD_LDS uint32_t* pat, i
     return r;
 }
 
+// Target letter codes (letter(), 2 bits each, 16 per word) in LDS.
+__device__ inline void pack_target(GWAMD_LDS uint32_t* tc, const char* t, int T, int lane)
+{
+    for (int k = lane; k * 16 < T; k += kWave)
+    {
+        uint32_t v    = 0;
+        const int lim = min(T - k * 16, 16);
+        for (int i = 0; i < lim; i++)
+            v |= uint32_t(letter(t[k * 16 + i])) << (2 * i);
+        tc[k] = v;
+    }
+}
+
+__device__ __forceinline__ int code_at(const GWAMD_LDS uint32_t* tc, int idx)
+{
+    return int((tc[idx >> 4] >> (2 * (idx & 15))) & 3u);
+}
+
 } // namespace aln
 } // namespace gwamd

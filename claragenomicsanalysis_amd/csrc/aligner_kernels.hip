@@ -23,6 +23,18 @@
 
 #include <climits>
 
+#ifdef GWAMD_ALN_PROFILE
+// Diagnostic build only: cycle counters per phase of hm_kernel, summed over
+// waves ([0] reverse sweeps, [1] forward sweeps, [2] base cases, [3] total,
+// [4] sweep columns x blocks, [5] base-case columns, [6] base cases).
+__device__ unsigned long long gwamd_aln_prof[8];
+#define GWAMD_PROF_T0(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define GWAMD_PROF_ADD(acc, v) acc += __builtin_amdgcn_s_memtime() - v
+#else
+#define GWAMD_PROF_T0(v)
+#define GWAMD_PROF_ADD(acc, v)
+#endif
+
 namespace gwamd
 {
 namespace aln
@@ -145,13 +157,152 @@ __device__ void myers_sweep(const GWAMD_LDS uint32_t* pat, int pat_words, int Q,
     }
 }
 
+// Branch-free variant of myers_block_step: no data-dependent branches, so the
+// two independent sweeps of a split interleave in one instruction stream.
+__device__ __forceinline__ int block_step_bf(MyersBlock& B, int code, int hin, bool last, int ll, int hb, int lane,
+                                             uint32_t hisel, uint32_t lane0bit)
+{
+    const uint32_t lo  = (code & 1) ? B.e[1] : B.e[0];
+    const uint32_t hi  = (code & 1) ? B.e[3] : B.e[2];
+    const uint32_t neg = hin < 0 ? lane0bit : 0u;
+    const uint32_t pos = hin > 0 ? lane0bit : 0u;
+    uint32_t eq        = (code & 2) ? hi : lo;
+    const uint32_t xv  = eq | B.mv;
+    eq |= neg;
+    uint32_t s;
+    const bool ov     = __builtin_add_overflow(eq & B.pv, B.pv, &s);
+    const uint64_t G  = __builtin_amdgcn_ballot_w64(ov) & B.act;
+    const uint64_t P  = __builtin_amdgcn_ballot_w64(s == 0xffffffffu) & B.act;
+    const uint64_t GP = G | P;
+    s += mask_bit((GP + G) ^ GP ^ G, hisel, lane);
+    const uint32_t xh  = (s ^ B.pv) | eq;
+    uint32_t ph        = B.mv | ~(xh | B.pv);
+    uint32_t mh        = B.pv & xh;
+    const uint64_t PH  = __builtin_amdgcn_ballot_w64((ph >> 31) != 0u);
+    const uint64_t MH  = __builtin_amdgcn_ballot_w64((mh >> 31) != 0u);
+    const uint32_t phl = uniu(__builtin_amdgcn_readlane(int(ph), ll));
+    const uint32_t mhl = uniu(__builtin_amdgcn_readlane(int(mh), ll));
+    const int h_last   = int((phl >> hb) & 1u) - int((mhl >> hb) & 1u);
+    const int h_full   = int((PH >> 63) & 1u) - int((MH >> 63) & 1u);
+    ph                 = (ph << 1) | mask_bit(PH << 1, hisel, lane) | pos;
+    mh                 = (mh << 1) | mask_bit(MH << 1, hisel, lane) | neg;
+    B.pv               = mh | ~(xv | ph);
+    B.mv               = ph & xv;
+    return last ? h_last : h_full;
+}
+
+// Myers state of one half of a split (rows [qb, qe), forward or reversed)
+template <int N>
+struct HalfSweep
+{
+    MyersBlock B[N];
+    int lc, ll, hb, score;
+    __device__ void init(const GWAMD_LDS uint32_t* pat, int pat_words, int Q, int qb, int qe, bool rev, int lane)
+    {
+        const int m      = qe - qb;
+        const int nwords = (m + kWordBits - 1) / kWordBits;
+        const int off    = rev ? Q - qe : qb;
+        const int pbase  = rev ? 4 : 0;
+        const int lw     = nwords - 1;
+        lc               = lw / kWave;
+        ll               = lw % kWave;
+        hb               = (m - 1) % kWordBits;
+        score            = m;
+#pragma unroll
+        for (int c = 0; c < N; c++)
+        {
+            const int w      = c * kWave + lane;
+            const bool valid = w < nwords;
+#pragma unroll
+            for (int L = 0; L < 4; L++)
+                B[c].e[L] = valid ? seg_pattern(pat, pat_words, off, w, pbase + L) : 0u;
+            B[c].pv  = ~0u;
+            B[c].mv  = 0u;
+            B[c].act = __builtin_amdgcn_ballot_w64(valid);
+        }
+    }
+    __device__ __forceinline__ void step(int code, int lane, uint32_t hisel, uint32_t lane0bit)
+    {
+        int h = 1, hl = 0; // top row 0, 1, 2, ...: +1 into the first block
+#pragma unroll
+        for (int c = 0; c < N; c++)
+        {
+            h  = block_step_bf(B[c], code, h, c == lc, ll, hb, lane, hisel, lane0bit);
+            hl = c == lc ? h : hl;
+        }
+        score += hl;
+    }
+};
+
+// Both sweeps of a Hirschberg split in one pass over the target segment
+// (hirschberg_myers_compute_target_mid_warp, hirschberg_myers_gpu.cu:411-475):
+// fw[t] = D(q[qb, qm), target[tb, tb + t)), rv[t] = D(q[qm, qe) reversed,
+// target[te - t, te) reversed), t = 0..Ts.  N: 64-word blocks of the larger
+// half.
+template <int N, typename Buf>
+__device__ void split_sweep(const GWAMD_LDS uint32_t* pat, int pat_words, int Q, int qb, int qm, int qe,
+                            const GWAMD_LDS uint32_t* tcod, int tb, int te, int lane, Buf fw, Buf rv)
+{
+    const uint32_t hisel    = lane >= 32 ? 1u : 0u;
+    const uint32_t lane0bit = lane == 0 ? 1u : 0u;
+    HalfSweep<N> F, R;
+    F.init(pat, pat_words, Q, qb, qm, false, lane);
+    R.init(pat, pat_words, Q, qm, qe, true, lane);
+    const int Ts = te - tb;
+    for (int t0 = 0; t0 <= Ts; t0 += kWave)
+    {
+        // letter codes of the next 64 columns, one per lane
+        const int tt = t0 + lane;
+        const bool in = tt >= 1 && tt <= Ts;
+        const int cf  = in ? code_at(tcod, tb + tt - 1) : 0;
+        const int cr  = in ? code_at(tcod, te - tt) : 0;
+        const int cnt = min(kWave, Ts + 1 - t0);
+        uint32_t bf = F.score, br = R.score; // lane x: column t0 + x
+        for (int x = t0 == 0 ? 1 : 0; x < cnt; x++)
+        {
+            F.step(uni(__builtin_amdgcn_readlane(cf, x)), lane, hisel, lane0bit);
+            R.step(uni(__builtin_amdgcn_readlane(cr, x)), lane, hisel, lane0bit);
+            bf = lane == x ? uint32_t(F.score) : bf;
+            br = lane == x ? uint32_t(R.score) : br;
+        }
+        if (lane < cnt)
+        {
+            fw[t0 + lane] = uint16_t(bf);
+            rv[t0 + lane] = uint16_t(br);
+        }
+    }
+}
+
+// Split column: minimum of fw[t] + rv[Ts - t]; ties to the smallest 5-bit-
+// reversed t, then the smallest t (the reference's 32-lane striding and
+// shfl_down tree, hirschberg_myers_gpu.cu:450-474).
+template <typename Buf>
+__device__ int split_argmin(Buf fw, Buf rv, int Ts, int lane)
+{
+    uint64_t best = ~uint64_t(0);
+    for (int t = lane; t <= Ts; t += kWave)
+    {
+        const uint32_t sum = uint32_t(fw[t]) + uint32_t(rv[Ts - t]);
+        const uint32_t key = __builtin_bitreverse32(uint32_t(t) & 31u) >> 27;
+        const uint64_t v   = (uint64_t(sum) << 40) | (uint64_t(key) << 32) | uint32_t(t);
+        best               = v < best ? v : best;
+    }
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1)
+    {
+        const uint64_t o = __shfl_xor(best, d);
+        best             = o < best ? o : best;
+    }
+    return uni(int(uint32_t(best)));
+}
+
 // ---------------------------------------------------------------------------
 // Full-Myers base case of a segment shorter than 63 rows (one 64-bit word,
 // wave-uniform): column state into `leaf` (LDS or HBM), then the backtrace
 // (hirschberg_myers_compute_path / append_myers_backtrace, :372-392, :100-160).
 template <typename LeafPtr64, typename LeafPtr32>
 __device__ int leaf_full_myers(const GWAMD_LDS uint32_t* pat, int pat_words, int qb, int qe,
-                               const GWAMD_LDS uint8_t* tgt, int tb, int te, LeafPtr64 lpv, LeafPtr64 lmv,
+                               const GWAMD_LDS uint32_t* tcod, int tb, int te, LeafPtr64 lpv, LeafPtr64 lmv,
                                LeafPtr32 lsc, int8_t* path, int lane)
 {
     const int m          = qe - qb;
@@ -184,7 +335,7 @@ __device__ int leaf_full_myers(const GWAMD_LDS uint32_t* pat, int pat_words, int
     }
     for (int t = 1; t <= T; t++)
     {
-        const int code    = letter(uni(int(tgt[tb + t - 1])));
+        const int code    = uni(code_at(tcod, tb + t - 1));
         const uint64_t lo = (code & 1) ? e[1] : e[0];
         const uint64_t hi = (code & 1) ? e[3] : e[2];
         const uint64_t eq = (code & 2) ? hi : lo;
@@ -255,6 +406,19 @@ __device__ int leaf_full_myers(const GWAMD_LDS uint32_t* pat, int pat_words, int
     return pos;
 }
 
+template <typename Buf>
+__device__ void run_split(int nblk, const GWAMD_LDS uint32_t* pat, int pat_words, int Q, int qb, int qm, int qe,
+                          const GWAMD_LDS uint32_t* tcod, int tb, int te, int lane, Buf fw, Buf rv)
+{
+    switch (nblk)
+    {
+    case 1: split_sweep<1>(pat, pat_words, Q, qb, qm, qe, tcod, tb, te, lane, fw, rv); break;
+    case 2: split_sweep<2>(pat, pat_words, Q, qb, qm, qe, tcod, tb, te, lane, fw, rv); break;
+    case 3: split_sweep<3>(pat, pat_words, Q, qb, qm, qe, tcod, tb, te, lane, fw, rv); break;
+    default: split_sweep<4>(pat, pat_words, Q, qb, qm, qe, tcod, tb, te, lane, fw, rv); break;
+    }
+}
+
 struct Range
 {
     int32_t qb, qe, tb, te;
@@ -275,22 +439,29 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
     extern __shared__ __align__(16) uint8_t lds[];
     const int lane                  = threadIdx.x;
     GWAMD_LDS uint8_t* base         = (GWAMD_LDS uint8_t*)(lds);
-    GWAMD_LDS uint8_t* tgt          = base + a.lds_target_off;
+    GWAMD_LDS uint32_t* tcod        = (GWAMD_LDS uint32_t*)(base + a.lds_target_off);
     GWAMD_LDS uint32_t* pat         = (GWAMD_LDS uint32_t*)(base + a.lds_pat_off);
     GWAMD_LDS uint8_t* scratch      = base + a.lds_scratch_off;
-    GWAMD_LDS uint16_t* revs        = (GWAMD_LDS uint16_t*)(scratch);
+    // split scores of segments up to kSplitLds columns (wider ones in HBM)
+    GWAMD_LDS uint16_t* fwl         = (GWAMD_LDS uint16_t*)(scratch + kLeafCols * kLeafColBytes);
+    GWAMD_LDS uint16_t* rvl         = fwl + kSplitLds;
     GWAMD_LDS Range* stack          = (GWAMD_LDS Range*)(base + a.lds_stack_off);
     uint8_t* ws                     = a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes);
+    uint16_t* fwg = reinterpret_cast<uint16_t*>(ws + ((int64_t(a.stride + 1) * kLeafColBytes + 15) & ~int64_t(15)));
+    uint16_t* rvg = fwg + (a.stride + 1);
+#ifdef GWAMD_ALN_PROFILE
+    uint64_t pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
 
     for (int idx = blockIdx.x; idx < a.n; idx += gridDim.x)
     {
+        GWAMD_PROF_T0(t_all);
         const char* q  = a.seqs + size_t(2 * idx) * a.stride;
         const char* tg = a.seqs + size_t(2 * idx + 1) * a.stride;
         const int Q    = uni(a.lens[2 * idx]);
         const int T    = uni(a.lens[2 * idx + 1]);
         int8_t* path   = a.paths + size_t(idx) * a.max_path_length;
-        for (int k = lane; k < T; k += kWave)
-            tgt[k] = uint8_t(tg[k]);
+        pack_target(tcod, tg, T, lane);
         build_patterns(pat, q, Q, lane);
         const int pat_words = (Q + kWordBits - 1) / kWordBits;
         wave_sync();
@@ -329,7 +500,7 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
                 for (int k0 = 0; k0 < Ts && found < 0; k0 += kWave)
                 {
                     const int k       = k0 + lane;
-                    const bool hit    = k < Ts && char(tgt[e.te - 1 - k]) == c;
+                    const bool hit    = k < Ts && tg[e.te - 1 - k] == c; // raw characters
                     const uint64_t hm = __builtin_amdgcn_ballot_w64(hit);
                     if (hm != 0)
                         found = k0 + __builtin_ctzll(hm);
@@ -348,12 +519,17 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
                 const int nw = (m + kWordBits - 1) / kWordBits;
                 if (m < kFullMyers && int64_t(Ts + 1) * nw <= a.max_matrix_elems)
                 {
+                    GWAMD_PROF_T0(t_leaf);
+#ifdef GWAMD_ALN_PROFILE
+                    pr[5] += Ts;
+                    pr[6] += 1;
+#endif
                     if (Ts + 1 <= kLeafCols)
                     {
                         GWAMD_LDS uint64_t* lpv = (GWAMD_LDS uint64_t*)(scratch);
                         GWAMD_LDS uint64_t* lmv = lpv + kLeafCols;
                         GWAMD_LDS int32_t* lsc  = (GWAMD_LDS int32_t*)(lmv + kLeafCols);
-                        len += leaf_full_myers(pat, pat_words, e.qb, e.qe, tgt, e.tb, e.te, lpv, lmv, lsc, path + len,
+                        len += leaf_full_myers(pat, pat_words, e.qb, e.qe, tcod, e.tb, e.te, lpv, lmv, lsc, path + len,
                                                lane);
                     }
                     else
@@ -361,46 +537,41 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
                         uint64_t* lpv = reinterpret_cast<uint64_t*>(ws);
                         uint64_t* lmv = lpv + (a.stride + 1);
                         int32_t* lsc  = reinterpret_cast<int32_t*>(lmv + (a.stride + 1));
-                        len += leaf_full_myers(pat, pat_words, e.qb, e.qe, tgt, e.tb, e.te, lpv, lmv, lsc, path + len,
+                        len += leaf_full_myers(pat, pat_words, e.qb, e.qe, tcod, e.tb, e.te, lpv, lmv, lsc, path + len,
                                                lane);
                     }
                     wave_sync();
+                    GWAMD_PROF_ADD(pr[2], t_leaf);
                     continue;
                 }
-                // split the query at its middle, the target at the best column
-                const int qm = e.qb + m / 2;
-                // reverse half: rev[t] = D(q[qm, qe), target suffix of length t)
-                uint32_t acc = 0;
-                myers_sweep(pat, pat_words, Q, qm, e.qe, true, tgt, e.tb, e.te, lane, [&](int t, int sc) {
-                    const int tl = t & (kWave - 1);
-                    if (lane == tl)
-                        acc = uint32_t(sc);
-                    if (tl == kWave - 1 || t == Ts)
-                    {
-                        const int t0 = t - tl;
-                        if (lane <= tl)
-                            revs[t0 + lane] = uint16_t(acc);
-                    }
-                });
-                wave_sync();
-                int best = INT_MAX, bkey = INT_MAX, bt = 0;
-                int rv   = 0;
-                myers_sweep(pat, pat_words, Q, e.qb, qm, false, tgt, e.tb, e.te, lane, [&](int t, int sc) {
-                    const int tl = t & (kWave - 1);
-                    if (tl == 0)
-                    {
-                        const int x = t + lane;
-                        rv          = x <= Ts ? int(revs[Ts - x]) : 0;
-                    }
-                    const int sum = sc + uni(__builtin_amdgcn_readlane(rv, tl));
-                    const int key = int(__builtin_bitreverse32(uint32_t(t) & 31u) >> 27);
-                    if (sum < best || (sum == best && key < bkey))
-                    {
-                        best = sum;
-                        bkey = key;
-                        bt   = t;
-                    }
-                });
+                // split the query at its middle, the target at the best column:
+                // both halves swept together, then the minimum of fwd + rev
+                const int qm   = e.qb + m / 2;
+                const int nblk = uni(((max(qm - e.qb, e.qe - qm) + kWordBits - 1) / kWordBits + kWave - 1) / kWave);
+#ifdef GWAMD_ALN_PROFILE
+                pr[4] += uint64_t(Ts) * nblk;
+#endif
+                GWAMD_PROF_T0(t_rev);
+                int bt;
+                if (Ts + 1 <= kSplitLds)
+                {
+                    run_split(nblk, pat, pat_words, Q, e.qb, qm, e.qe, tcod, e.tb, e.te, lane, fwl, rvl);
+                    wave_sync();
+                    GWAMD_PROF_ADD(pr[0], t_rev);
+                    GWAMD_PROF_T0(t_fwd);
+                    bt = split_argmin(fwl, rvl, Ts, lane);
+                    GWAMD_PROF_ADD(pr[1], t_fwd);
+                }
+                else
+                {
+                    run_split(nblk, pat, pat_words, Q, e.qb, qm, e.qe, tcod, e.tb, e.te, lane, fwg, rvg);
+                    __threadfence_block();
+                    wave_sync();
+                    GWAMD_PROF_ADD(pr[0], t_rev);
+                    GWAMD_PROF_T0(t_fwd);
+                    bt = split_argmin(fwg, rvg, Ts, lane);
+                    GWAMD_PROF_ADD(pr[1], t_fwd);
+                }
                 const int tm = e.tb + bt;
                 wave_sync();
                 if (sp < kStackSize)
@@ -427,7 +598,13 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
         if (lane == 0)
             a.path_len[idx] = success ? len : 0;
         wave_sync();
+        GWAMD_PROF_ADD(pr[3], t_all);
     }
+#ifdef GWAMD_ALN_PROFILE
+    if (lane == 0)
+        for (int k = 0; k < 8; k++)
+            atomicAdd(&gwamd_aln_prof[k], (unsigned long long)pr[k]);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -599,3 +776,19 @@ extern "C" hipError_t gwamd_internal_align_occupancy(int algo, int lds_bytes, in
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, hm_kernel, kWave, size_t(lds_bytes));
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, myers_kernel, kWave, size_t(lds_bytes));
 }
+
+#ifdef GWAMD_ALN_PROFILE
+// Diagnostic build only: read (and optionally clear) the hm_kernel counters.
+extern "C" int gwamd_internal_aln_prof(unsigned long long* out8, int reset)
+{
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(gwamd_aln_prof), 8 * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    if (reset)
+    {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gwamd_aln_prof), z, sizeof(z)) != hipSuccess)
+            return -1;
+    }
+    return 0;
+}
+#endif
