@@ -88,7 +88,9 @@ def poa_window(reads, weights=None, gap=-8, mismatch=-6, match=8, banded=False, 
         max_consensus = 2 * max_len
     if max_seqs is None:
         max_seqs = len(reads)
-    seqs = np.frombuffer(b"".join(reads) + b"\0" * 16, dtype=np.uint8).copy()
+    # the banded DP reads up to a band width past a read's end (values that
+    # never reach an output, cudapoa_nw_banded.cuh:123-173): pad accordingly
+    seqs = np.frombuffer(b"".join(reads) + b"\0" * (2 * band_width + 64), dtype=np.uint8).copy()
     lens = np.array([len(r) for r in reads], dtype=np.int32)
     if weights is None:
         wts = np.ones(max(len(seqs), 1), dtype=np.int8)
@@ -150,7 +152,7 @@ def poa_batch(windows, nthreads=0, gap=-8, mismatch=-6, match=8, banded=False, b
         max_consensus = 2 * max_len
     if max_seqs is None:
         max_seqs = max(nseq + [1])
-    seqs = np.frombuffer(b"".join(flat) + b"\0" * 16, dtype=np.uint8).copy()
+    seqs = np.frombuffer(b"".join(flat) + b"\0" * (2 * band_width + 64), dtype=np.uint8).copy()
     lens_a = np.array(lens, dtype=np.int32)
     offs = np.zeros(len(lens), dtype=np.int64)
     if len(lens) > 1:

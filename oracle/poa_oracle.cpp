@@ -350,8 +350,12 @@ static int nw_banded(const Graph& g, const uint8_t* read, int L, int bw, int gap
     B.max_column = L + 1;
     // Rows 0..V are used; cells are never read before written except through
     // the layout quirks, whose stale values never reach an output.
-    if (flat.size() < size_t(V + 2) * B.stride)
-        flat.resize(size_t(V + 2) * B.stride, ScoreT(0));
+    // set_score(row, 0) writes at the row's band start (:71-87), which for
+    // late rows lies past the row, up to L + 1 cells past the last row: slack
+    // for those writes (never read back)
+    const size_t need = size_t(V + 2) * B.stride + size_t(L + 2 * B.stride);
+    if (flat.size() < need)
+        flat.resize(need, ScoreT(0));
     B.S = flat.data() + B.stride; // one guard row in front
     // horizontal boundary (:212-216)
     for (int j = 0; j < B.stride; j++)
