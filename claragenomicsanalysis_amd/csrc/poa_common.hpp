@@ -145,6 +145,7 @@ enum Phase
     kPhAdd,
     kPhTopsort,
     kPhOutput,
+    kPhRowProg, // read staging + row program (LDS kernel)
     kPhTotal,
     kPhases
 };

@@ -20,6 +20,8 @@
 
 #include "poa_device.hpp"
 
+#define GWAMD_LDS __attribute__((address_space(3)))
+
 namespace gwamd
 {
 namespace poa
@@ -412,54 +414,88 @@ __device__ __forceinline__ int prog_np(const WinGraph<SizeT>& g, int r, uint32_t
     return np == int(kRecEscape) ? int(g.in_cnt[int(g.sorted[r - 1])]) : np;
 }
 
-// Row program for rows 1..V (built after every topological sort).
+// Row program for rows 1..V (built after every topological sort).  The graph
+// lives in HBM, so the loads are batched for memory-level parallelism: each
+// lane takes kRP rows per pass and every dependent level (node, its counts,
+// its first two predecessors' node ids, their rows) is issued for all of them
+// before the next level waits.  A row spills when a successor reads it from
+// ring_rows or more rows later; that is marked from the successor's side
+// (row s, predecessor row p: s - p >= ring_rows) into byte flags in `flags`
+// (V + 2 bytes of free LDS), so no out-edge lists are read.
 template <typename SizeT>
 __device__ void build_row_program(const WinGraph<SizeT>& g, int V, uint32_t* rec, uint16_t* xl, int xl_cap,
-                                  int ring_rows, int lane)
+                                  int ring_rows, int lane, GWAMD_LDS uint8_t* flags)
 {
+    constexpr int kRP = 4;
+    for (int r = lane; r <= V + 1; r += kWave)
+        flags[r] = 0;
+    wave_sync();
     int xbase = 0;
-    for (int r0 = 1; r0 <= V; r0 += kWave)
+    for (int r0 = 1; r0 <= V; r0 += kRP * kWave)
     {
-        const int r      = r0 + lane;
-        const bool valid = r <= V;
-        int node = 0, np = 0, base = 0, sink = 0, spill = 0;
-        if (valid)
+        int node[kRP], np[kRP], base[kRP], oc[kRP], e0[kRP], e1[kRP], p0[kRP], p1[kRP];
+#pragma unroll
+        for (int u = 0; u < kRP; u++)
         {
-            node         = int(g.sorted[r - 1]);
-            np           = int(g.in_cnt[node]);
-            base         = int(g.base[node]);
-            const int oc = int(g.out_cnt[node]);
-            sink         = oc == 0 ? 1 : 0;
-            // spill: a successor reads this row from >= ring_rows rows later
-            for (int e = 0; e < oc; e++)
-                spill |= (int(g.pos[int(g.out_e[node * kMaxEdges + e])]) + 1 - r) >= ring_rows ? 1 : 0;
+            const int r = min(r0 + u * kWave + lane, V);
+            node[u]     = int(g.sorted[r - 1]);
         }
-        int total      = 0;
-        const int excl = wave_excl_sum(np >= 2 ? np : 0, lane, total);
-        if (valid)
+#pragma unroll
+        for (int u = 0; u < kRP; u++)
         {
-            uint32_t v = uint32_t(base) | (uint32_t(sink) << 14) | (uint32_t(spill) << 15);
-            if (np == 1)
+            np[u]   = int(g.in_cnt[node[u]]);
+            base[u] = int(g.base[node[u]]);
+            oc[u]   = int(g.out_cnt[node[u]]);
+            e0[u]   = int(g.in_e[node[u] * kMaxEdges]);
+            e1[u]   = int(g.in_e[node[u] * kMaxEdges + 1]);
+        }
+#pragma unroll
+        for (int u = 0; u < kRP; u++)
+        {
+            // slots beyond in_cnt hold stale ids: clamp to a valid node
+            p0[u] = int(g.pos[np[u] >= 1 ? e0[u] : 0]) + 1;
+            p1[u] = int(g.pos[np[u] >= 2 ? e1[u] : 0]) + 1;
+        }
+#pragma unroll
+        for (int u = 0; u < kRP; u++)
+        {
+            const int r      = r0 + u * kWave + lane;
+            const bool valid = r <= V;
+            const int n      = valid ? np[u] : 0;
+            int total        = 0;
+            const int excl   = wave_excl_sum(n >= 2 ? n : 0, lane, total);
+            if (valid)
             {
-                const int p = pred_row(g, node, 0);
-                v |= (1u << 8) | (uint32_t(r - p) << 16);
-            }
-            else if (np >= 2)
-            {
-                const int off = xbase + excl;
-                if (off + np <= xl_cap)
+                uint32_t v = uint32_t(base[u]) | (uint32_t(oc[u] == 0 ? 1 : 0) << 14);
+                if (n == 1)
                 {
-                    for (int k = 0; k < np; k++)
-                        xl[off + k] = uint16_t(pred_row(g, node, k));
-                    v |= (uint32_t(np) << 8) | (uint32_t(off) << 16);
+                    v |= (1u << 8) | (uint32_t(r - p0[u]) << 16);
+                    if (r - p0[u] >= ring_rows)
+                        flags[p0[u]] = 1;
                 }
-                else
-                    v |= kRecEscape << 8;
+                else if (n >= 2)
+                {
+                    const int off  = xbase + excl;
+                    const bool fit = off + n <= xl_cap;
+                    for (int k = 0; k < n; k++)
+                    {
+                        const int pk = k == 0 ? p0[u] : (k == 1 ? p1[u] : pred_row(g, node[u], k));
+                        if (fit)
+                            xl[off + k] = uint16_t(pk);
+                        if (r - pk >= ring_rows)
+                            flags[pk] = 1;
+                    }
+                    v |= fit ? (uint32_t(n) << 8) | (uint32_t(off) << 16) : (kRecEscape << 8);
+                }
+                rec[r] = v;
             }
-            rec[r] = v;
+            xbase += total;
         }
-        xbase += total;
     }
+    wave_sync();
+    for (int r = lane + 1; r <= V; r += kWave)
+        if (flags[r])
+            rec[r] |= 1u << 15;
     wave_sync();
 }
 
@@ -469,8 +505,6 @@ __device__ void build_row_program(const WinGraph<SizeT>& g, int V, uint32_t* rec
 // per 32-bit register, so the diagonal/vertical/max work runs on v_pk_*
 // instructions.  Cells beyond the read may wrap; they only feed cells further
 // right, never a cell <= L.
-#define GWAMD_LDS __attribute__((address_space(3)))
-
 typedef short pk_s16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short pk_u16x2 __attribute__((ext_vector_type(2)));
 
@@ -1046,15 +1080,33 @@ __device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V
                 ti0 = max(0, i - (kTileRows - 1));
                 tj0 = max(0, cj - (kTileCols - 16)) & ~15;
                 wave_sync();
-                for (int t = lane; t < kTileRows * (kTileCols / 16); t += kWave)
+                // 16 loads per lane, issued 8 at a time before any is waited for
+                constexpr int kPer = kTileRows * (kTileCols / 16) / kWave;
+                constexpr int kB   = 8;
+#pragma unroll
+                for (int b0 = 0; b0 < kPer; b0 += kB)
                 {
-                    const int tr = t / (kTileCols / 16);
-                    const int tc = (t % (kTileCols / 16)) * 16;
-                    const int rr = ti0 + tr;
-                    uint4 v      = make_uint4(0, 0, 0, 0);
-                    if (rr <= V && tj0 + tc + 16 <= code_stride)
-                        v = *reinterpret_cast<const uint4*>(codes + size_t(rr) * code_stride + tj0 + tc);
-                    *reinterpret_cast<uint4*>(tile + tr * kTileCols + tc) = v;
+                    uint4 v[kB];
+#pragma unroll
+                    for (int u = 0; u < kB; u++)
+                    {
+                        const int t   = (b0 + u) * kWave + lane;
+                        const int tr  = t / (kTileCols / 16);
+                        const int tc  = (t % (kTileCols / 16)) * 16;
+                        const int rr  = ti0 + tr;
+                        const bool ok = rr <= V && tj0 + tc + 16 <= code_stride;
+                        v[u] = *reinterpret_cast<const uint4*>(codes + size_t(ok ? rr : 0) * code_stride +
+                                                               (ok ? tj0 + tc : 0));
+                        v[u] = ok ? v[u] : make_uint4(0, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int u = 0; u < kB; u++)
+                    {
+                        const int t  = (b0 + u) * kWave + lane;
+                        const int tr = t / (kTileCols / 16);
+                        const int tc = (t % (kTileCols / 16)) * 16;
+                        *reinterpret_cast<uint4*>(tile + tr * kTileCols + tc) = v[u];
+                    }
                 }
                 wave_sync();
             }
@@ -1340,40 +1392,62 @@ template <typename SizeT>
 __device__ bool topsort_lds(WinGraph<SizeT>& g, int n, GWAMD_LDS uint8_t* scratch, int scratch_bytes,
                             GWAMD_LDS int* sh, int lane)
 {
-    GWAMD_LDS uint16_t* off   = (GWAMD_LDS uint16_t*)(scratch);
-    GWAMD_LDS uint16_t* queue = (GWAMD_LDS uint16_t*)(scratch + (n + 1) * 2);
-    GWAMD_LDS uint8_t* cnt    = scratch + (n + 1) * 2 + n * 2;
-    const int head_bytes      = ((n + 1) * 2 + n * 2 + n + 15) & ~15;
+    // info[v] = out-degree << 16 | first successor: the FIFO step reads one
+    // word per node; off / edges only for nodes with two or more successors
+    GWAMD_LDS uint32_t* info  = (GWAMD_LDS uint32_t*)(scratch);
+    GWAMD_LDS uint16_t* off   = (GWAMD_LDS uint16_t*)(scratch + n * 4);
+    GWAMD_LDS uint16_t* queue = (GWAMD_LDS uint16_t*)(scratch + n * 4 + (n + 1) * 2);
+    GWAMD_LDS uint8_t* cnt    = scratch + n * 4 + (n + 1) * 2 + n * 2;
+    const int head_bytes      = (n * 4 + (n + 1) * 2 + n * 2 + n + 15) & ~15;
     GWAMD_LDS uint16_t* edges = (GWAMD_LDS uint16_t*)(scratch + head_bytes);
     if (head_bytes > scratch_bytes)
         return false;
-    const int edge_cap = (scratch_bytes - head_bytes) / 2;
-    int ebase          = 0;
-    for (int v0 = 0; v0 < n; v0 += kWave)
+    const int edge_cap = min((scratch_bytes - head_bytes) / 2, 65535);
+    // CSR staging from the HBM graph: counts and the first two out-edges of
+    // kTS nodes per lane are loaded before any of them is used
+    constexpr int kTS = 4;
+    int ebase         = 0;
+    for (int v0 = 0; v0 < n; v0 += kTS * kWave)
     {
-        const int v  = v0 + lane;
-        const int oc = v < n ? int(g.out_cnt[v]) : 0;
-        int total    = 0;
-        const int ex = wave_excl_sum(oc, lane, total);
-        if (v < n)
+        int oc[kTS], ic[kTS], e0[kTS], e1[kTS];
+#pragma unroll
+        for (int u = 0; u < kTS; u++)
         {
-            off[v] = uint16_t(ebase + ex);
-            cnt[v] = uint8_t(g.in_cnt[v]);
+            const int v = min(v0 + u * kWave + lane, n - 1);
+            oc[u]       = int(g.out_cnt[v]);
+            ic[u]       = int(g.in_cnt[v]);
+            e0[u]       = int(g.out_e[v * kMaxEdges]);
+            e1[u]       = int(g.out_e[v * kMaxEdges + 1]);
         }
-        ebase += total;
+#pragma unroll
+        for (int u = 0; u < kTS; u++)
+        {
+            const int v     = v0 + u * kWave + lane;
+            const bool real = v < n;
+            const int c     = real ? oc[u] : 0;
+            int total       = 0;
+            const int ex    = wave_excl_sum(c, lane, total);
+            if (ebase + total > edge_cap)
+                return false;
+            if (real)
+            {
+                const int o = ebase + ex;
+                off[v]      = uint16_t(o);
+                cnt[v]      = uint8_t(ic[u]);
+                info[v]     = (uint32_t(c) << 16) | uint32_t(uint16_t(c >= 1 ? e0[u] : 0));
+                if (c >= 1)
+                    edges[o] = uint16_t(e0[u]);
+                if (c >= 2)
+                    edges[o + 1] = uint16_t(e1[u]);
+                for (int e = 2; e < c; e++)
+                    edges[o + e] = uint16_t(int(g.out_e[v * kMaxEdges + e]));
+            }
+            ebase += total;
+        }
     }
-    if (ebase > edge_cap || ebase > 65535)
-        return false;
     if (lane == 0)
         off[n] = uint16_t(ebase);
     wave_sync();
-    for (int v = lane; v < n; v += kWave)
-    {
-        const int o  = int(off[v]);
-        const int oc = int(off[v + 1]) - o;
-        for (int e = 0; e < oc; e++)
-            edges[o + e] = uint16_t(int(g.out_e[v * kMaxEdges + e]));
-    }
     // sources in id order
     int k = 0;
     for (int v0 = 0; v0 < n; v0 += kWave)
@@ -1389,19 +1463,41 @@ __device__ bool topsort_lds(WinGraph<SizeT>& g, int n, GWAMD_LDS uint8_t* scratc
     wave_sync();
     if (lane == 0)
     {
-        int tail = k;
-        for (int q = 0; q < tail; q++)
+        // FIFO (cudapoa_topsort.cuh:58-85); the next node comes from a register
+        // when it was queued by this step or prefetched with this step's info
+        int tail  = k;
+        int vnext = tail > 0 ? int(queue[0]) : 0;
+        for (int q = 0; q < tail;)
         {
-            const int v  = int(queue[q]);
-            const int e1 = int(off[v + 1]);
-            for (int e = int(off[v]); e < e1; e++)
+            const int v        = vnext;
+            const uint32_t inf = info[v];
+            const int qn       = q + 1 < tail ? int(queue[q + 1]) : -1;
+            const int deg      = int(inf >> 16);
+            int first_pushed   = -1;
+            if (deg >= 1)
             {
-                const int o = int(edges[e]);
+                const int o = int(inf & 0xffffu);
                 const int c = int(cnt[o]) - 1;
                 cnt[o]      = uint8_t(c);
                 if (c == 0)
+                {
                     queue[tail++] = uint16_t(o);
+                    first_pushed  = o;
+                }
+                for (int e = int(off[v]) + 1; e < int(off[v]) + deg; e++)
+                {
+                    const int o2 = int(edges[e]);
+                    const int c2 = int(cnt[o2]) - 1;
+                    cnt[o2]      = uint8_t(c2);
+                    if (c2 == 0)
+                    {
+                        queue[tail++] = uint16_t(o2);
+                        first_pushed  = first_pushed < 0 ? o2 : first_pushed;
+                    }
+                }
             }
+            q++;
+            vnext = qn >= 0 ? qn : first_pushed;
         }
         sh[0] = tail;
     }
@@ -1515,8 +1611,9 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
             for (int j = tid; j < padded; j += kThr)
                 lread[j] = j < L ? read_g[j] : 0;
             const int V = node_count;
-            if (wave == 0)
-                build_row_program<SizeT>(g, V, rec, xl, d.lds_xl_cap, d.lds_ring_rows, lane);
+            if (wave == 0) // spill flags in the ring region (free until the forward pass)
+                build_row_program<SizeT>(g, V, rec, xl, d.lds_xl_cap, d.lds_ring_rows, lane,
+                                         (GWAMD_LDS uint8_t*)(lds) + d.lds_ring_off);
             if (NW > 1)
             {
                 // forward-pass channels and progress words start empty
@@ -1524,6 +1621,7 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
                     reinterpret_cast<GWAMD_LDS int*>(shb + kShProg)[t] = 0;
             }
             __syncthreads();
+            ph.lap<kPhRowProg>();
             cells += int64_t(V + 1) * (L + 1);
             const int end_row = nw_forward_lds_pk<CPL, NW, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride,
                                                                   codes, d.code_stride, sc, shb, carry, tid, fp);

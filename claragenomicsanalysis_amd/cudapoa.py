@@ -269,10 +269,10 @@ class CudaPoaBatch:
                                              fn.ctypes.data_as(C.POINTER(C.c_int32))))
         return cells[:n], fn[:n]
 
-    PHASES = ("backbone", "forward", "traceback", "add", "topsort", "output", "total")
+    PHASES = ("backbone", "forward", "traceback", "add", "topsort", "output", "rowprog", "total")
 
     def get_phase_ticks(self):
-        """Per-window in-kernel phase timers (s_memrealtime ticks at 100 MHz), shape (n, 7)."""
+        """Per-window in-kernel phase timers (s_memrealtime ticks at 100 MHz), shape (n, 8)."""
         n = self.total_poas
         out = np.zeros((max(n, 1), len(self.PHASES)), np.int64)
         _check(self._lib.gwamd_poa_get_phase_ticks(self._handle, out.ctypes.data_as(C.POINTER(C.c_int64))))
