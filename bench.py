@@ -72,6 +72,10 @@ CONFIGS = {
     # name: (backbone, reads, mut, ins, del, max_seq, banded, band_width, windows per GPU)
     "B": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=False, bw=256, windows=1024),
     "B_banded": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=True, bw=256, windows=1024),
+    # MSA mode, 10 kb windows x 16 reads, banded bw 256,
+    # BatchSize(10600, 16, 256) -> int32 scores and node ids
+    "C": dict(backbone=10000, reads=16, err=500, max_seq=10600, banded=True, bw=256, windows=128, msa=True,
+              mem_per_window=400e6),
 }
 
 
@@ -248,9 +252,13 @@ def main():
     gen_s = time.time() - t0
 
     stream = torch.cuda.Stream(device=dev)
-    max_mem = int(nwin * 12.5e6) + (2 << 30)
+    msa = bool(cfg.get("msa", False))
+    max_mem = int(nwin * cfg.get("mem_per_window", 12.5e6)) + (2 << 30)
     batch = CudaPoaBatch(cfg["reads"], cfg["max_seq"], max_mem, device_id=dev, stream=stream,
+                         output_type="msa" if msa else "consensus",
                          cuda_banded_alignment=cfg["banded"], alignment_band_width=cfg["bw"])
+    if batch.get_capacity()[1] < nwin:
+        raise RuntimeError("batch holds %d windows, need %d" % (batch.get_capacity()[1], nwin))
     off = 0
     windows = []
     for w in range(nwin):
@@ -295,7 +303,12 @@ def main():
     wall_max = float(t_max.item())
 
     # outputs + work counters (outside the timed region)
-    cons, cov, status = batch.get_consensus()
+    if msa:
+        msa_rows, status = batch.get_msa()
+        cons = ["".join(rows) for rows in msa_rows]  # gathered / counted as output bytes
+        cov = None
+    else:
+        cons, cov, status = batch.get_consensus()
     cells, final_nodes = batch.get_stats()
     ticks = batch.get_phase_ticks()  # last launch, 100 MHz
     n_ok = int(sum(1 for s in status if s == 0))
@@ -309,7 +322,7 @@ def main():
         from claragenomicsanalysis_amd.shard import gather_consensus
         torch.cuda.synchronize()
         tg = time.perf_counter()
-        allc = gather_consensus(cons, 2 * cfg["max_seq"], device="cuda")
+        allc = gather_consensus(cons, max(len(c) for c in cons) if msa else 2 * cfg["max_seq"], device="cuda")
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
         if rank == 0 and len(allc) != nwin * world:
@@ -325,17 +338,22 @@ def main():
         ok = True
         for i in range(k):
             r = oracle.poa_window(windows[i], banded=cfg["banded"], band_width=cfg["bw"], score_bits=score_bits,
-                                  max_nodes=mn, max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"])
-            ok = ok and (r.status == status[i] and r.consensus == cons[i] and r.coverage == cov[i])
+                                  max_nodes=mn, max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"], msa=msa)
+            if msa:
+                ok = ok and (r.status == status[i] and (r.msa or []) == msa_rows[i])
+            else:
+                ok = ok and (r.status == status[i] and r.consensus == cons[i] and r.coverage == cov[i])
         parity = {"windows_checked": k, "bit_exact_vs_oracle": bool(ok)}
         if not args.no_cpu and world == 1:
             th = cpu_threads()
-            ns = args.cpu_sample or min(nwin, max(th * 48, 64))
+            ns = args.cpu_sample or min(nwin, max(th * (2 if msa else 48), 64 if not msa else 16))
             tc = time.perf_counter()
             ccons, cst, _, used = oracle.poa_batch(windows[:ns], nthreads=th, banded=cfg["banded"],
                                                    band_width=cfg["bw"], score_bits=score_bits, max_nodes=mn,
-                                                   max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"])
+                                                   max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"], msa=msa)
             cpu_s = time.perf_counter() - tc
+            if msa:
+                ccons = ["".join(rows) for rows in ccons]
             cpu = {"value": round(ns / cpu_s, 3), "unit": "windows/s", "cores": int(used), "kind": "port",
                    "nproc": os.cpu_count(), "cpu_model": cpu_model(),
                    "sample": "first %d windows of the same workload, oracle/poa_oracle.cpp (reference-algorithm "
@@ -355,7 +373,7 @@ def main():
                 traffic = None
         total_windows = nwin * world
         out = {
-            "metric": "POA windows/sec (consensus)",
+            "metric": "POA windows/sec (%s)" % ("MSA" if msa else "consensus"),
             "value": round(total_windows * args.steps / wall_max, 3),
             "unit": "windows/s",
             "n_gpus": world,
@@ -367,8 +385,8 @@ def main():
             "vs_baseline": None,
             "dtype": "int16" if score_bits == 16 else "int32",
             "data": "synthetic (reference genomeutils generators, seeds 1..N)",
-            "config": {"workload": "cudapoa consensus, %d windows/GPU x %d reads x ~%d bp synthetic ONT, %s"
-                                   % (nwin, cfg["reads"], cfg["backbone"],
+            "config": {"workload": "cudapoa %s, %d windows/GPU x %d reads x ~%d bp synthetic ONT, %s"
+                                   % ("MSA" if msa else "consensus", nwin, cfg["reads"], cfg["backbone"],
                                       "banded bw=%d" % cfg["bw"] if cfg["banded"] else "full alignment"),
                        "config_key": args.config, "windows_per_gpu": nwin, "batch_size": [cfg["max_seq"],
                                                                                         cfg["reads"]],

@@ -41,7 +41,7 @@ def _declare(L):
                                     vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.oracle_poa_batch.restype = C.c_int
     L.oracle_poa_batch.argtypes = [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
-                                   vp, vp, vp, vp, vp]
+                                   vp, vp, vp, vp, vp, i32, vp]
     L.oracle_topsort.restype = None
     L.oracle_topsort.argtypes = [i32, vp, vp, vp, vp]
     L.oracle_nw.restype = C.c_int
@@ -131,9 +131,10 @@ def poa_window(reads, weights=None, gap=-8, mismatch=-6, match=8, banded=False, 
 
 
 def poa_batch(windows, nthreads=0, gap=-8, mismatch=-6, match=8, banded=False, band_width=256, score_bits=16,
-              max_nodes=None, max_consensus=None, max_seqs=None):
+              max_nodes=None, max_consensus=None, max_seqs=None, msa=False):
     """Run many windows (list of lists of bytes) on all host cores (OpenMP).
-    Returns (consensus list, status array, cells array, threads used)."""
+    Returns (consensus list, status array, cells array, threads used); with
+    msa=True the first element is the list of MSA row lists instead."""
     flat = []
     lens = []
     first = []
@@ -165,9 +166,22 @@ def poa_batch(windows, nthreads=0, gap=-8, mismatch=-6, match=8, banded=False, b
     clen = np.zeros(nw, dtype=np.int32)
     status = np.zeros(nw, dtype=np.uint8)
     cells = np.zeros(nw, dtype=np.int64)
+    msa_buf = np.zeros(nw * max_seqs * max_consensus, dtype=np.uint8) if msa else None
     used = lib().oracle_poa_batch(_p(seqs), _p(offs), _p(lens_a), _p(first_a), _p(nseq_a), nw, gap, mismatch,
                                   match, int(banded), band_width, score_bits, max_nodes, max_consensus, max_seqs,
-                                  nthreads, _p(cons), _p(cov), _p(clen), _p(status), _p(cells))
+                                  nthreads, _p(cons), _p(cov), _p(clen), _p(status), _p(cells), int(msa),
+                                  _p(msa_buf))
+    if msa:
+        rows = []
+        for i in range(nw):
+            base = i * max_seqs * max_consensus
+            win = []
+            if status[i] == 0:
+                for s in range(nseq[i]):
+                    row = bytes(msa_buf[base + s * max_consensus:base + (s + 1) * max_consensus])
+                    win.append(row.split(b"\0", 1)[0].decode())
+            rows.append(win)
+        return rows, status, cells, used
     out = [bytes(cons[i * max_consensus:i * max_consensus + clen[i]]).decode() for i in range(nw)]
     return out, status, cells, used
 

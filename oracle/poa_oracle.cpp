@@ -1086,9 +1086,12 @@ int oracle_poa_window(const uint8_t* seqs, const int32_t* lens, const int8_t* wt
 int oracle_poa_batch(const uint8_t* seqs, const int64_t* seq_offsets, const int32_t* lens, const int32_t* win_first,
                      const int32_t* win_nseq, int32_t nwin, int32_t gap, int32_t mismatch, int32_t match, int32_t banded,
                      int32_t band_width, int32_t score_bits, int32_t max_nodes, int32_t max_consensus, int32_t max_seqs,
-                     int32_t nthreads, uint8_t* cons, uint16_t* covg, int32_t* cons_len, uint8_t* status, int64_t* cells)
+                     int32_t nthreads, uint8_t* cons, uint16_t* covg, int32_t* cons_len, uint8_t* status, int64_t* cells,
+                     int32_t msa, uint8_t* msa_out)
 {
-    WindowParams P{gap, mismatch, match, banded, band_width, score_bits, 0, max_nodes, max_consensus, max_seqs};
+    // msa != 0: MSA output (generateMSAKernel) into msa_out, window wi at
+    // wi * max_seqs * max_consensus (rows NUL terminated)
+    WindowParams P{gap, mismatch, match, banded, band_width, score_bits, msa, max_nodes, max_consensus, max_seqs};
     int used = 1;
 #ifdef _OPENMP
     if (nthreads > 0)
@@ -1114,7 +1117,7 @@ int oracle_poa_batch(const uint8_t* seqs, const int64_t* seq_offsets, const int3
         cons_len[wi] = 0;
         status[wi]   = run_window(P, seqs + seq_offsets[first], lens + first, wts.data(), n,
                                 cons + size_t(wi) * max_consensus, covg + size_t(wi) * max_consensus, &cons_len[wi],
-                                nullptr, g, &st);
+                                msa ? msa_out + size_t(wi) * max_seqs * max_consensus : nullptr, g, &st);
         if (cells)
             cells[wi] = st.cells;
     }

@@ -246,3 +246,16 @@ def test_lds_msa_multiwave(monkeypatch):
     for i, w in enumerate(wins):
         r = run_oracle(w, 1000, 10, msa=True)
         assert st[i] == r.status and msa[i] == r.msa, i
+
+
+def test_config_c_msa_10kb_banded_int32():
+    # SURVEY.md 8(d) config C shape: BatchSize(10600, 16, 256), banded, MSA,
+    # 10 kb backbone with 500/500/500 mutations -> int32 scores and node ids
+    wins = synth.poa_windows(1, 2, 10000, 16, 500, 500, 500)
+    b = run_gpu(wins, 10600, 16, banded=True, bw=256, output_type="msa", mem=16 << 30)
+    assert b.get_types() == (32, 32)
+    msa, st = b.get_msa()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 10600, 16, banded=True, bw=256, msa=True, score_bits=32)
+        assert st[i] == r.status == 0
+        assert msa[i] == r.msa, i
