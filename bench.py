@@ -392,7 +392,7 @@ def main():
                                                                                         cfg["reads"]],
                        "scores": [-8, -6, 8], "parallelism": "dp%d (windows sharded, RCCL gather)" % world,
                        "score_bits": score_bits, "size_bits": size_bits,
-                       "kernel_variant": ["", "global", "lds"][batch.kernel_variant()],
+                       "kernel_variant": ["", "global", "lds", "band"][batch.kernel_variant()],
                        "windows_ok": n_ok, "dp_cells_per_step": cells_total,
                        "gcups": round(cells_total / kernel_s / 1e9, 3),
                        "mean_final_nodes": round(float(np.mean(final_nodes)), 1),

@@ -144,6 +144,7 @@ public:
         dims_.aln_cap       = dims_.max_nodes + bs_.max_sequence_size + 4;
         dims_.want_consensus = (output_mask_ & OutputType::consensus) ? 1 : 0;
         plan_lds_kernel();
+        plan_band_kernel();
         const int64_t own = own_bytes_per_window(sz, sbytes, msa);
         if (own > 0)
             max_poas = std::min<int64_t>(max_poas, int64_t(max_mem) / own);
@@ -409,7 +410,7 @@ public:
     int32_t window_num_seqs(int32_t w) const { return h_win_.as<const gwamd::poa::WindowDesc>()[w].num_seqs; }
     int8_t output_mask() const { return output_mask_; }
     int64_t device_bytes() const { return int64_t(d_slab_.n + d_codes_.n + d_seqs_.n + d_wts_.n + d_len_.n + d_off_.n + d_win_.n); }
-    int32_t kernel_kind() const { return dims_.lds_kernel ? 2 : 1; }
+    int32_t kernel_kind() const { return dims_.lds_kernel == 3 ? 3 : (dims_.lds_kernel ? 2 : 1); }
     int32_t max_poas() const { return max_poas_; }
 
     void get_phases(int64_t* out)
@@ -520,6 +521,75 @@ private:
         const int64_t cr_b   = a16(int64_t(dims_.max_nodes + 2) * 2);
         dims_.aux_carry_off  = int32_t(code_b);
         dims_.aux_stride     = code_b + cr_b;
+    }
+
+    // Banded kernel (poa_window_kernel_band, poa_band.hip): band widths of 128
+    // or 256 (2 or 4 cells per lane), gap <= 0.  LDS image per window: staged
+    // read | work region (row-program flags, the 16-row ring of band rows, the
+    // traceback tile, the add-alignment scratch; the topological sort also
+    // reuses the read) | shared words.  Windows per CU: 4, 2 or 1, the most
+    // that leave room for the work region at this batch's maximum sizes.
+    void plan_band_kernel()
+    {
+        if (!banded_ || dims_.lds_kernel)
+            return;
+        const char* env = std::getenv("GWAMD_POA_KERNEL");
+        if (env && std::string(env) == "v1")
+            return;
+        const int bw = dims_.band_width;
+        if ((bw != 128 && bw != 256) || gap_ > 0)
+            return;
+        auto a16          = [](int64_t v) { return (v + 15) & ~int64_t(15); };
+        const int cpl     = bw / 64;
+        const int sbytes  = score_bits_ / 8;
+        const int rowsz   = bw + gwamd::poa::kBandPad + cpl;
+        const int64_t ms  = dims_.max_seq_len, mn = dims_.max_nodes;
+        const int64_t read_b  = a16(ms + bw + 48);
+        const int64_t sh_b    = 64;
+        const int64_t ring_b  = a16(int64_t(16) * rowsz * sbytes);
+        const int64_t tile_b  = a16(int64_t(64) * bw + 512);
+        const int64_t flags_b = a16(mn + 2);
+        const int64_t add_b   = 5 * a16(ms + 16) + 2 * (mn + ms + 16) + 16;
+        const int64_t min_w   = std::max({ring_b, tile_b, flags_b});
+        const int64_t want_w  = std::max(min_w, add_b);
+        const int64_t kStatic = 64; // static __shared__ words of the kernel
+        int64_t total         = 0;
+        for (int per_cu : {4, 2, 1})
+        {
+            const int64_t budget = (163840 / per_cu - kStatic) & ~int64_t(15);
+            if (read_b + want_w + sh_b <= budget || per_cu == 1)
+            {
+                total = budget;
+                break;
+            }
+        }
+        const int64_t work = total - read_b - sh_b;
+        if (work < min_w)
+            return;
+        dims_.lds_kernel     = 3;
+        dims_.lds_cpl        = cpl;
+        dims_.lds_waves      = 1;
+        dims_.lds_bytes      = int32_t(total);
+        dims_.lds_ring_off   = int32_t(read_b);
+        dims_.lds_ring_rows  = 16;
+        dims_.lds_work_bytes = int32_t(work);
+        dims_.lds_sh_off     = int32_t(read_b + work);
+        dims_.score_stride   = rowsz; // spill rows: band row at position idx + cpl - 1
+        dims_.code_stride    = bw;
+        const int64_t rows   = dims_.score_rows;
+        int64_t o            = a16(rows * bw); // codes
+        dims_.aux_reca_off   = int32_t(o);
+        o += a16(rows * 4);
+        dims_.aux_recb_off = int32_t(o);
+        o += a16(rows * 4);
+        dims_.aux_col0_off = int32_t(o);
+        o += a16(rows * 4);
+        dims_.aux_flag_off = int32_t(o);
+        o += a16(rows);
+        dims_.aux_xl_off = int32_t(o);
+        dims_.aux_xl_cap = int32_t(2 * mn + 64);
+        o += a16(int64_t(dims_.aux_xl_cap) * 4);
+        dims_.aux_stride = o;
     }
 
     // Non-score bytes of the reference slab for max_poas windows

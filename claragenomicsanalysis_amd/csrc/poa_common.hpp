@@ -72,6 +72,16 @@ struct Dims
     int32_t code_stride;    // bytes per traceback-code row
     int64_t aux_stride;     // bytes per window of the HBM side buffer:
     int32_t aux_carry_off;  //   codes [score_rows x code_stride] | per-row span carries (int16)
+    // banded kernel (lds_kernel == 3): LDS work region size; the HBM side
+    // buffer holds codes [score_rows x band_width] | row records a, b (u32) |
+    // column-0 values (i32) | row flags (u8) | predecessor lists (i32)
+    int32_t lds_work_bytes;
+    int32_t aux_reca_off;
+    int32_t aux_recb_off;
+    int32_t aux_col0_off;
+    int32_t aux_flag_off;
+    int32_t aux_xl_off;
+    int32_t aux_xl_cap;
 };
 
 // Small shared region of the LDS kernel (kShBytes(waves) at Dims::lds_sh_off):

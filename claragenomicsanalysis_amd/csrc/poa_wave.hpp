@@ -1,0 +1,591 @@
+// Wave-level building blocks shared by the POA kernels (poa_kernels.hip: the
+// global-memory and LDS-resident full-alignment kernels; poa_band.hip: the
+// banded kernel): phase timers, the consensus / MSA epilogue, DPP scans, the
+// wave-parallel addAlignmentToGraph and the LDS Kahn topological sort.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "poa_device.hpp"
+
+#define GWAMD_LDS __attribute__((address_space(3)))
+
+namespace gwamd
+{
+namespace poa
+{
+
+// Per-window phase timers (s_memrealtime, 100 MHz) kept in registers.
+struct PhaseTimer
+{
+    uint64_t t0, mark;
+    uint64_t v[kPhases - 1];
+    __device__ PhaseTimer() : t0(now_ticks()), mark(t0)
+    {
+#pragma unroll
+        for (int i = 0; i < kPhases - 1; i++)
+            v[i] = 0;
+    }
+    template <int P>
+    __device__ void lap()
+    {
+        const uint64_t t = now_ticks();
+        v[P] += t - mark;
+        mark = t;
+    }
+    __device__ void store(int64_t* out) const
+    {
+#pragma unroll
+        for (int i = 0; i < kPhases - 1; i++)
+            out[i] = int64_t(v[i]);
+        out[kPhTotal] = int64_t(now_ticks() - t0);
+    }
+};
+
+// Consensus and/or MSA of one finished window (cudapoa_generate_consensus.cuh:
+// 279-347, cudapoa_generate_msa.cuh:121-224).
+template <typename SizeT, bool MSA>
+__device__ void finish_window(const Buffers& b, const Dims& d, int w, int lane, WinGraph<SizeT>& g, int status,
+                              int nseq, int node_count, int32_t* cscore, SizeT* cpred, uint16_t* ecov,
+                              uint16_t* ecovc, SizeT* seq_begin, int& sh_len, int& sh_status)
+{
+    uint8_t* cons_out = b.cons + size_t(w) * d.max_consensus;
+    const int graph_status = status;
+    if (!MSA || d.want_consensus)
+    {
+        uint16_t* cov_out = b.cov + size_t(w) * d.max_consensus;
+        if (lane == 0)
+        {
+            int len = 0;
+            int cst = graph_status;
+            if (cst == kSuccess && nseq > 0)
+            {
+                int r = consensus_raw<SizeT>(g, node_count, cscore, cpred, cons_out, cov_out, d.max_consensus);
+                if (r < 0)
+                    cst = -r;
+                else
+                    len = r;
+            }
+            sh_len    = len;
+            sh_status = cst;
+        }
+        wave_sync();
+        const int len = sh_len;
+        // reverse in place to host order (cudapoa_batch.cuh:241-246 does this on the host)
+        for (int k = lane; k < len / 2; k += kWave)
+        {
+            uint8_t c0  = cons_out[k];
+            uint8_t c1  = cons_out[len - 1 - k];
+            uint16_t v0 = cov_out[k];
+            uint16_t v1 = cov_out[len - 1 - k];
+            cons_out[k] = c1, cons_out[len - 1 - k] = c0;
+            cov_out[k] = v1, cov_out[len - 1 - k] = v0;
+        }
+        if (lane == 0)
+        {
+            b.cons_len[w] = len;
+            b.status[w]   = uint8_t(sh_status);
+            if (len < d.max_consensus)
+                cons_out[len] = 0;
+        }
+        wave_sync();
+    }
+    if (MSA)
+    {
+        uint8_t* msa_out = b.msa + size_t(w) * d.max_seqs * d.max_consensus;
+        if (lane == 0)
+        {
+            int msa_len = 0;
+            int mst     = graph_status;
+            if (mst == kSuccess && nseq > 0)
+            {
+                if (!topsort_racon<SizeT>(g, node_count, cscore, cpred, 4 * d.max_nodes))
+                    mst = kGenericError;
+                else
+                {
+                    // getNodeIDToMSAPosDevice (cudapoa_generate_msa.cuh:27-45); the racon stack
+                    // region is free again and holds node -> column
+                    SizeT* mpos = cpred;
+                    for (int r = 0; r < node_count; r++)
+                    {
+                        const int id = int(g.sorted[r]);
+                        mpos[id]     = SizeT(msa_len);
+                        const int ac = int(g.aln_cnt[id]);
+                        for (int a = 0; a < ac; a++)
+                            mpos[int(g.sorted[++r])] = SizeT(msa_len);
+                        msa_len++;
+                    }
+                    if (msa_len >= d.max_consensus)
+                        mst = kExceededMaxSeqSize;
+                }
+            }
+            sh_len    = msa_len;
+            sh_status = mst;
+        }
+        wave_sync();
+        const int msa_len = sh_len;
+        const int mst     = sh_status;
+        if (mst == kSuccess && nseq > 0)
+        {
+            const SizeT* mpos = cpred;
+            // generateMSADevice (cudapoa_generate_msa.cuh:47-118): one lane per read
+            for (int s = lane; s < nseq; s += kWave)
+            {
+                uint8_t* row = msa_out + size_t(s) * d.max_consensus;
+                int node     = int(seq_begin[s]);
+                int filled   = 0;
+                while (true)
+                {
+                    const int mp = int(mpos[node]);
+                    row[mp]      = g.base[node];
+                    for (int i = filled; i < mp; i++)
+                        row[i] = '-';
+                    filled   = mp + 1;
+                    bool end = true;
+                    for (int e = 0; e < int(g.out_cnt[node]) && end; e++)
+                    {
+                        const int to = int(g.out_e[node * kMaxEdges + e]);
+                        const int cc = int(ecovc[node * kMaxEdges + e]);
+                        for (int m = 0; m < cc; m++)
+                        {
+                            if (int(ecov[size_t(node * kMaxEdges + e) * d.max_seqs + m]) == s)
+                            {
+                                end  = false;
+                                node = to;
+                                break;
+                            }
+                        }
+                    }
+                    if (end)
+                    {
+                        for (int i = filled; i < msa_len; i++)
+                            row[i] = '-';
+                        break;
+                    }
+                }
+                row[msa_len] = 0;
+            }
+        }
+        if (lane == 0)
+        {
+            b.msa_len[w]    = msa_len;
+            b.msa_status[w] = uint8_t(mst);
+        }
+    }
+}
+
+
+__device__ __forceinline__ int dpp_max(int v, int ctrl, int row_mask)
+{
+    // lanes without a source (or masked rows) keep kNeg, the max identity
+    switch (ctrl)
+    {
+    case 0x111: return max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x111, 0xf, 0xf, false));
+    case 0x112: return max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x112, 0xf, 0xf, false));
+    case 0x114: return max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x114, 0xf, 0xf, false));
+    case 0x118: return max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x118, 0xf, 0xf, false));
+    default: return v;
+    }
+}
+
+// Inclusive max-scan over the wave with DPP (row_shr 1/2/4/8, row_bcast 15/31).
+__device__ __forceinline__ int wave_incl_max_dpp(int v)
+{
+    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x111, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x112, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x114, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x118, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x142, 0xa, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+
+// Exclusive wave sum of small non-negative ints (row-program offsets).
+__device__ __forceinline__ int wave_excl_sum(int v, int lane, int& total)
+{
+    int x = v;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1)
+    {
+        int t = __shfl_up(x, d, kWave);
+        if (lane >= d)
+            x += t;
+    }
+    total = __shfl(x, kWave - 1, kWave);
+    return x - v;
+}
+
+// ---------------------------------------------------------------------------
+// Wave-parallel addAlignmentToGraph (cudapoa_add_alignment.cuh:59-279).
+//
+// The traceback visits every read position exactly once, in increasing
+// order, so element rp of the sequential loop is read base rp and its head is
+// element rp-1's node.  When every element's node is distinct and no two
+// elements touch the same aligned-node group, the sequential loop's writes are
+// independent and are done by one lane per element; the new node ids are a
+// prefix sum, and the first error (node or edge limit) is found by a min
+// over positions.  Otherwise nothing is written and -1 is returned so the
+// caller runs the sequential restatement.
+struct AddScratch
+{
+    GWAMD_LDS uint16_t* gid;   // [max_seq] aligned graph node per read position (0xffff = none)
+    GWAMD_LDS uint16_t* curr;  // [max_seq] node the read base lands on
+    GWAMD_LDS uint8_t* kind;   // [max_seq] 0 same base, 1 aligned hit, 2 new, 3 new + ring; bit 2: edge exists
+    GWAMD_LDS uint16_t* owner; // [max_nodes + max_seq] element that claimed a node (last writer wins)
+    GWAMD_LDS int* sh;         // [0] conflict
+};
+
+template <typename SizeT, bool MSA>
+__device__ int add_alignment_parallel(WinGraph<SizeT>& g, int& node_count, const SizeT* ag, const SizeT* ar,
+                                      int alen, int L, const uint8_t* read, const int8_t* w, int s, uint16_t* ecov,
+                                      uint16_t* ecov_cnt, SizeT* seq_begin, int max_seqs, const AddScratch& X,
+                                      int lane)
+{
+    const int nc0 = node_count;
+    int err       = INT_MAX; // first error in read order: (pos << 8) | status
+    if (lane == 0)
+        X.sh[0] = 0;
+    for (int k = lane; k < alen; k += kWave)
+    {
+        const int rp = int(ar[k]);
+        if (rp >= 0 && rp < L)
+            X.gid[rp] = uint16_t(int(ag[k]) < 0 ? 0xffff : int(ag[k]));
+    }
+    wave_sync();
+    // kinds and existing targets
+    for (int rp = lane; rp < L; rp += kWave)
+    {
+        const int gid    = int(X.gid[rp]);
+        const uint8_t rb = read[rp];
+        int kind = 2, curr = 0;
+        if (gid != 0xffff)
+        {
+            if (g.base[gid] == rb)
+                kind = 0, curr = gid;
+            else
+            {
+                kind         = 3;
+                const int na = int(g.aln_cnt[gid]);
+                for (int n = 0; n < na; n++)
+                {
+                    const int aid = int(g.aln[gid * kMaxAlignments + n]);
+                    if (g.base[aid] == rb)
+                    {
+                        kind = 1, curr = aid;
+                        break;
+                    }
+                }
+            }
+        }
+        X.kind[rp] = uint8_t(kind);
+        X.curr[rp] = uint16_t(curr);
+    }
+    wave_sync();
+    // new node ids: prefix sum over new-node elements in read order
+    int nnew = 0;
+    for (int r0 = 0; r0 < L; r0 += kWave)
+    {
+        const int rp     = r0 + lane;
+        const bool isnew = rp < L && X.kind[rp] >= 2;
+        int total        = 0;
+        const int excl   = wave_excl_sum(isnew ? 1 : 0, lane, total);
+        if (isnew)
+        {
+            const int id = nc0 + nnew + excl;
+            X.curr[rp]   = uint16_t(id);
+            if (id + 1 >= g.max_nodes)
+                err = min(err, (rp << 8) | int(kNodeCountExceeded));
+        }
+        nnew += total;
+    }
+    wave_sync();
+    // independence checks without atomics: every element claims its node (and,
+    // for aligned hits / ring updates, its aligned group); after a barrier an
+    // element that no longer owns a claimed node has a conflicting partner.
+    for (int rp = lane; rp < L; rp += kWave)
+        X.owner[int(X.curr[rp])] = uint16_t(rp);
+    wave_sync();
+    bool conflict = false;
+    for (int rp = lane; rp < L; rp += kWave)
+        conflict |= int(X.owner[int(X.curr[rp])]) != rp;
+    wave_sync();
+    for (int rp = lane; rp < L; rp += kWave)
+    {
+        const int kind = X.kind[rp];
+        if (kind == 1 || kind == 3)
+        {
+            const int gid = int(X.gid[rp]);
+            X.owner[gid]  = uint16_t(rp);
+            const int na  = int(g.aln_cnt[gid]);
+            for (int n = 0; n < na; n++)
+                X.owner[int(g.aln[gid * kMaxAlignments + n])] = uint16_t(rp);
+        }
+    }
+    wave_sync();
+    for (int rp = lane; rp < L; rp += kWave)
+    {
+        const int kind = X.kind[rp];
+        if (kind == 1 || kind == 3)
+        {
+            const int gid = int(X.gid[rp]);
+            conflict |= int(X.owner[gid]) != rp;
+            const int na = int(g.aln_cnt[gid]);
+            for (int n = 0; n < na; n++)
+                conflict |= int(X.owner[int(g.aln[gid * kMaxAlignments + n])]) != rp;
+        }
+    }
+    if (conflict)
+        X.sh[0] = 1;
+    wave_sync();
+    if (X.sh[0])
+        return -1;
+    // edge existence and edge-limit errors
+    for (int rp = lane + 1; rp < L; rp += kWave)
+    {
+        const int head = int(X.curr[rp - 1]);
+        const int curr = int(X.curr[rp]);
+        const int kind = X.kind[rp];
+        bool exists    = false;
+        int ic         = 0;
+        if (kind < 2)
+        {
+            ic = int(g.in_cnt[curr]);
+            for (int e = 0; e < ic; e++)
+                exists |= int(g.in_e[curr * kMaxEdges + e]) == head;
+        }
+        if (!exists)
+        {
+            const int oc = X.kind[rp - 1] >= 2 ? 0 : int(g.out_cnt[head]);
+            if (oc + 1 >= kMaxEdges || ic + 1 >= kMaxEdges)
+                err = min(err, (rp << 8) | int(kEdgeCountExceeded));
+        }
+        else
+            X.kind[rp] = uint8_t(kind | 4);
+    }
+    err = -wave_max(-err); // wave-wide minimum
+    if (err != INT_MAX)
+        return err & 0xff;
+    wave_sync();
+    // writes 1: new nodes and aligned rings (one lane per element)
+    for (int rp = lane; rp < L; rp += kWave)
+    {
+        const int kind = X.kind[rp] & 3;
+        if (kind < 2)
+            continue;
+        const int curr  = int(X.curr[rp]);
+        g.base[curr]    = read[rp];
+        g.out_cnt[curr] = 0;
+        g.in_cnt[curr]  = 0;
+        g.aln_cnt[curr] = 0;
+        g.cov[curr]     = 0;
+        if (kind == 3)
+        {
+            const int gid = int(X.gid[rp]);
+            const int na  = int(g.aln_cnt[gid]);
+            int cnt       = 0;
+            for (int n = 0; n < na; n++)
+            {
+                const int aid                      = int(g.aln[gid * kMaxAlignments + n]);
+                const int ac                       = int(g.aln_cnt[aid]);
+                g.aln[aid * kMaxAlignments + ac]   = SizeT(curr);
+                g.aln_cnt[aid]                     = uint16_t(ac + 1);
+                g.aln[curr * kMaxAlignments + cnt] = SizeT(aid);
+                cnt++;
+            }
+            g.aln[gid * kMaxAlignments + na]   = SizeT(curr);
+            g.aln_cnt[gid]                     = uint16_t(na + 1);
+            g.aln[curr * kMaxAlignments + cnt] = SizeT(gid);
+            g.aln_cnt[curr]                    = uint16_t(cnt + 1);
+        }
+    }
+    wave_sync();
+    // writes 2: the edge head -> curr and the coverage of curr
+    for (int rp = lane; rp < L; rp += kWave)
+    {
+        const int curr = int(X.curr[rp]);
+        if (MSA && rp == 0)
+            seq_begin[s] = SizeT(curr);
+        if (rp > 0)
+        {
+            const int head = int(X.curr[rp - 1]);
+            const int wsum = int(uint16_t(int(w[rp - 1]))) + int(w[rp]);
+            if (X.kind[rp] & 4)
+            {
+                const int ic = int(g.in_cnt[curr]);
+                for (int e = 0; e < ic; e++)
+                    if (int(g.in_e[curr * kMaxEdges + e]) == head)
+                        g.in_w[curr * kMaxEdges + e] = uint16_t(int(g.in_w[curr * kMaxEdges + e]) + wsum);
+                if (MSA)
+                {
+                    const int oc = int(g.out_cnt[head]);
+                    for (int e = 0; e < oc; e++)
+                    {
+                        if (int(g.out_e[head * kMaxEdges + e]) == curr)
+                        {
+                            const int c                                       = int(ecov_cnt[head * kMaxEdges + e]);
+                            ecov[size_t(head * kMaxEdges + e) * max_seqs + c] = uint16_t(s);
+                            ecov_cnt[head * kMaxEdges + e]                    = uint16_t(c + 1);
+                            break;
+                        }
+                    }
+                }
+            }
+            else
+            {
+                const int ic                   = int(g.in_cnt[curr]);
+                g.in_e[curr * kMaxEdges + ic]  = SizeT(head);
+                g.in_w[curr * kMaxEdges + ic]  = uint16_t(wsum);
+                g.in_cnt[curr]                 = uint16_t(ic + 1);
+                const int oc                   = int(g.out_cnt[head]);
+                g.out_e[head * kMaxEdges + oc] = SizeT(curr);
+                if (MSA)
+                {
+                    ecov_cnt[head * kMaxEdges + oc]                = 1;
+                    ecov[size_t(head * kMaxEdges + oc) * max_seqs] = uint16_t(s);
+                }
+                g.out_cnt[head] = uint16_t(oc + 1);
+            }
+        }
+        g.cov[curr]++;
+    }
+    node_count = nc0 + nnew;
+    wave_sync();
+    return kSuccess;
+}
+
+// ---------------------------------------------------------------------------
+// Kahn topological sort (cudapoa_topsort.cuh:38-88) over an LDS copy of the
+// out-edge lists (CSR): the adjacency is staged wave-parallel, the sources
+// are compacted in id order in parallel, and lane 0 runs the FIFO on LDS.
+// Returns false (nothing written) when the scratch is too small.
+template <typename SizeT>
+__device__ bool topsort_lds(WinGraph<SizeT>& g, int n, GWAMD_LDS uint8_t* scratch, int scratch_bytes,
+                            GWAMD_LDS int* sh, int lane)
+{
+    // info[v] = out-degree << 16 | first successor: the FIFO step reads one
+    // word per node; off / edges only for nodes with two or more successors
+    GWAMD_LDS uint32_t* info  = (GWAMD_LDS uint32_t*)(scratch);
+    GWAMD_LDS uint16_t* off   = (GWAMD_LDS uint16_t*)(scratch + n * 4);
+    GWAMD_LDS uint16_t* queue = (GWAMD_LDS uint16_t*)(scratch + n * 4 + (n + 1) * 2);
+    GWAMD_LDS uint8_t* cnt    = scratch + n * 4 + (n + 1) * 2 + n * 2;
+    const int head_bytes      = (n * 4 + (n + 1) * 2 + n * 2 + n + 15) & ~15;
+    GWAMD_LDS uint16_t* edges = (GWAMD_LDS uint16_t*)(scratch + head_bytes);
+    if (head_bytes > scratch_bytes)
+        return false;
+    const int edge_cap = min((scratch_bytes - head_bytes) / 2, 65535);
+    // CSR staging from the HBM graph: counts and the first two out-edges of
+    // kTS nodes per lane are loaded before any of them is used
+    constexpr int kTS = 4;
+    int ebase         = 0;
+    for (int v0 = 0; v0 < n; v0 += kTS * kWave)
+    {
+        int oc[kTS], ic[kTS], e0[kTS], e1[kTS];
+#pragma unroll
+        for (int u = 0; u < kTS; u++)
+        {
+            const int v = min(v0 + u * kWave + lane, n - 1);
+            oc[u]       = int(g.out_cnt[v]);
+            ic[u]       = int(g.in_cnt[v]);
+            e0[u]       = int(g.out_e[v * kMaxEdges]);
+            e1[u]       = int(g.out_e[v * kMaxEdges + 1]);
+        }
+#pragma unroll
+        for (int u = 0; u < kTS; u++)
+        {
+            const int v     = v0 + u * kWave + lane;
+            const bool real = v < n;
+            const int c     = real ? oc[u] : 0;
+            int total       = 0;
+            const int ex    = wave_excl_sum(c, lane, total);
+            if (ebase + total > edge_cap)
+                return false;
+            if (real)
+            {
+                const int o = ebase + ex;
+                off[v]      = uint16_t(o);
+                cnt[v]      = uint8_t(ic[u]);
+                info[v]     = (uint32_t(c) << 16) | uint32_t(uint16_t(c >= 1 ? e0[u] : 0));
+                if (c >= 1)
+                    edges[o] = uint16_t(e0[u]);
+                if (c >= 2)
+                    edges[o + 1] = uint16_t(e1[u]);
+                for (int e = 2; e < c; e++)
+                    edges[o + e] = uint16_t(int(g.out_e[v * kMaxEdges + e]));
+            }
+            ebase += total;
+        }
+    }
+    if (lane == 0)
+        off[n] = uint16_t(ebase);
+    wave_sync();
+    // sources in id order
+    int k = 0;
+    for (int v0 = 0; v0 < n; v0 += kWave)
+    {
+        const int v    = v0 + lane;
+        const bool src = v < n && cnt[v] == 0;
+        int total      = 0;
+        const int ex   = wave_excl_sum(src ? 1 : 0, lane, total);
+        if (src)
+            queue[k + ex] = uint16_t(v);
+        k += total;
+    }
+    wave_sync();
+    if (lane == 0)
+    {
+        // FIFO (cudapoa_topsort.cuh:58-85); the next node comes from a register
+        // when it was queued by this step or prefetched with this step's info
+        int tail  = k;
+        int vnext = tail > 0 ? int(queue[0]) : 0;
+        for (int q = 0; q < tail;)
+        {
+            const int v        = vnext;
+            const uint32_t inf = info[v];
+            const int qn       = q + 1 < tail ? int(queue[q + 1]) : -1;
+            const int deg      = int(inf >> 16);
+            int first_pushed   = -1;
+            if (deg >= 1)
+            {
+                const int o = int(inf & 0xffffu);
+                const int c = int(cnt[o]) - 1;
+                cnt[o]      = uint8_t(c);
+                if (c == 0)
+                {
+                    queue[tail++] = uint16_t(o);
+                    first_pushed  = o;
+                }
+                for (int e = int(off[v]) + 1; e < int(off[v]) + deg; e++)
+                {
+                    const int o2 = int(edges[e]);
+                    const int c2 = int(cnt[o2]) - 1;
+                    cnt[o2]      = uint8_t(c2);
+                    if (c2 == 0)
+                    {
+                        queue[tail++] = uint16_t(o2);
+                        first_pushed  = first_pushed < 0 ? o2 : first_pushed;
+                    }
+                }
+            }
+            q++;
+            vnext = qn >= 0 ? qn : first_pushed;
+        }
+        sh[0] = tail;
+    }
+    wave_sync();
+    const int m = sh[0];
+    for (int q = lane; q < m; q += kWave)
+    {
+        const int v = int(queue[q]);
+        g.sorted[q] = SizeT(v);
+        g.pos[v]    = SizeT(q);
+    }
+    wave_sync();
+    return true;
+}
+
+
+} // namespace poa
+} // namespace gwamd

@@ -259,3 +259,39 @@ def test_config_c_msa_10kb_banded_int32():
         r = run_oracle(w, 10600, 16, banded=True, bw=256, msa=True, score_bits=32)
         assert st[i] == r.status == 0
         assert msa[i] == r.msa, i
+
+
+@pytest.mark.parametrize("variant", ["v1", "band"])
+@pytest.mark.parametrize("bw", [128, 256])
+def test_banded_kernel_variants(variant, bw, monkeypatch):
+    # the banded kernel (codes + LDS ring) and the global-memory kernel agree
+    # with the oracle, including reads much shorter than the band (every row
+    # starts at column 0), reads longer than the graph (gradient > 1), empty
+    # and single-base reads
+    if variant == "v1":
+        monkeypatch.setenv("GWAMD_POA_KERNEL", "v1")
+    else:
+        monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    wins = synth.poa_windows(501, 6, 700, 10, 35, 35, 35)
+    wins += synth.poa_windows(601, 3, 90, 8, 6, 6, 6)
+    wins.append([b"ACGTTGCA" * 20, b"ACGTTGCA" * 80, b"", b"A", b"ACGTTGCA" * 40 + b"T" * 100,
+                 b"GGGG" * 100, b"ACGTTGCA" * 20])
+    wins.append([b"A" * 600, b"C" * 600, b"A" * 300 + b"C" * 300, b"ACGT"])
+    b = run_gpu(wins, 800, 10, banded=True, bw=bw)
+    assert b.kernel_variant() == (1 if variant == "v1" else 3)
+    sbits = b.get_types()[0]
+    cons, cov, st = b.get_consensus()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 800, 10, banded=True, bw=bw, score_bits=sbits)
+        assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), (variant, bw, i)
+
+
+def test_banded_kernel_msa_graph_int32(monkeypatch):
+    monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    wins = synth.poa_windows(701, 5, 900, 9, 45, 45, 45)
+    b = run_gpu(wins, 4200, 9, banded=True, bw=256, output_type="msa")
+    assert b.kernel_variant() == 3 and b.get_types()[0] == 32
+    msa, st = b.get_msa()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 4200, 9, banded=True, bw=256, msa=True, score_bits=32)
+        assert (st[i], msa[i]) == (r.status, r.msa), i
