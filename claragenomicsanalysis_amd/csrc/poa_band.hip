@@ -28,6 +28,7 @@
 
 #include <climits>
 #include <cstdint>
+#include <type_traits>
 
 #include "poa_wave.hpp"
 
@@ -42,12 +43,19 @@ constexpr uint32_t kNpEsc = 63;
 
 // rec_a: base (8) | np (6; 63 = escape: read the graph) | sink (1) | spill (1) | band_start/4 (16)
 // rec_b: bit 31 clear: distance to pred 0 | distance to pred 1 << 16 (both < 32768);
-//        bit 31 set: offset of the row's predecessor list in xl (np >= 3 or far predecessors)
+//        bit 31 set: offset of the row's predecessor list in xl (np >= 5 or far predecessors)
+// rec_c: distance to pred 2 | distance to pred 3 << 16 (np 3-4, inline)
 __device__ __forceinline__ int ra_base(uint32_t a) { return int(a & 0xffu); }
 __device__ __forceinline__ int ra_np(uint32_t a) { return int((a >> 8) & 63u); }
 __device__ __forceinline__ bool ra_sink(uint32_t a) { return (a >> 14) & 1u; }
 __device__ __forceinline__ bool ra_spill(uint32_t a) { return (a >> 15) & 1u; }
 __device__ __forceinline__ int ra_bs(uint32_t a) { return int(a >> 16) << 2; }
+
+// s_waitcnt vmcnt(0) (gfx9 encoding: expcnt and lgkmcnt left at their maxima)
+__device__ __forceinline__ void vm_drain()
+{
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+}
 
 template <typename ScoreT>
 __device__ __forceinline__ int trunc_score(int v)
@@ -60,16 +68,46 @@ struct BandAux
     uint8_t* codes;  // [score_rows][bw]
     uint32_t* reca;  // [score_rows]
     uint32_t* recb;  // [score_rows]
+    uint32_t* recc;  // [score_rows] distances to predecessors 2 and 3 (rows with 3-4 inline predecessors)
     int32_t* col0;   // [score_rows] F(r, 0) of rows with band_start 0
     uint8_t* flags;  // [score_rows] bit 0: row stored in the spill rows
     int32_t* xl;     // [xl_cap] predecessor rows of rows with np >= 3 (or far)
+    int32_t* bx;     // [score_rows / 256 + 2] xl offset of the first listed row of each 256-row block
     int xl_cap;
 };
+
+// Diagnostic counters (-DGWAMD_BAND_PROFILE builds only; stored over the
+// phase slots, see the kernel epilogue).
+struct BandProf
+{
+    uint64_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef GWAMD_BAND_PROFILE
+    __device__ void add(int i, uint64_t x) { v[i] += x; }
+    __device__ static uint64_t now() { return __builtin_amdgcn_s_memtime(); }
+#else
+    __device__ void add(int, uint64_t) {}
+    __device__ static uint64_t now() { return 0; }
+#endif
+};
+enum
+{
+    kBpRows = 0,     // forward rows
+    kBpMulti,        // forward rows with two or more predecessors
+    kBpStageCyc,     // forward cycles spent staging blocks
+    kBpFwdCyc,       // forward cycles
+    kBpSteps,        // traceback steps
+    kBpTileCyc,      // traceback cycles spent staging tiles
+    kBpTbCyc,        // traceback cycles
+    kBpFlushCyc,     // traceback cycles in path flushes
+};
+
+constexpr int kStageRows = 256;  // forward pass: row records staged in LDS per block
+constexpr int kStageXl   = 1024; // predecessor-list entries staged per block
 
 // k-th predecessor row of row r (0 = the virtual row 0) and the predecessor count
 template <typename SizeT>
 __device__ __forceinline__ int band_pred2(const WinGraph<SizeT>& g, const BandAux& X, int r, uint32_t a, uint32_t b,
-                                          int k)
+                                          uint32_t c, int k)
 {
     const int np = ra_np(a);
     if (np == 0)
@@ -78,7 +116,8 @@ __device__ __forceinline__ int band_pred2(const WinGraph<SizeT>& g, const BandAu
         return pred_row(g, int(g.sorted[r - 1]), k);
     if (b >> 31)
         return int(X.xl[(b & 0x7fffffffu) + uint32_t(k)]);
-    return r - int(k == 0 ? (b & 0xffffu) : (b >> 16));
+    const uint32_t w = k < 2 ? b : c;
+    return r - int((k & 1) ? (w >> 16) : (w & 0xffffu));
 }
 
 template <typename SizeT>
@@ -101,8 +140,11 @@ __device__ void band_row_program(const WinGraph<SizeT>& g, int V, const Band& B,
         flags[r] = 0;
     wave_sync();
     int xbase = 0;
+    static_assert(kRP * kWave == kStageRows, "one row-program pass per staged block");
     for (int r0 = 1; r0 <= V; r0 += kRP * kWave)
     {
+        if (lane == 0)
+            X.bx[(r0 - 1) / kStageRows] = xbase;
         int node[kRP], np[kRP], base[kRP], oc[kRP], e0[kRP], e1[kRP], p0[kRP], p1[kRP];
 #pragma unroll
         for (int u = 0; u < kRP; u++)
@@ -131,7 +173,14 @@ __device__ void band_row_program(const WinGraph<SizeT>& g, int V, const Band& B,
             const int r      = r0 + u * kWave + lane;
             const bool valid = r <= V;
             const int n      = valid ? np[u] : 0;
-            const bool near2 = n <= 2 && (n < 1 || r - p0[u] < 32768) && (n < 2 || r - p1[u] < 32768);
+            int p2 = 0, p3 = 0;
+            if (n >= 3 && n <= 4)
+            {
+                p2 = pred_row(g, node[u], 2);
+                p3 = n == 4 ? pred_row(g, node[u], 3) : r;
+            }
+            const bool near2 = n <= 4 && (n < 1 || r - p0[u] < 32768) && (n < 2 || r - p1[u] < 32768) &&
+                               (n < 3 || (r - p2 < 32768 && r - p3 < 32768));
             const int listed = near2 ? 0 : n;
             int total        = 0;
             const int excl   = wave_excl_sum(listed, lane, total);
@@ -155,6 +204,14 @@ __device__ void band_row_program(const WinGraph<SizeT>& g, int V, const Band& B,
                         if (r - p1[u] >= kBandRing)
                             flags[p1[u]] = 1;
                     }
+                    if (n >= 3)
+                    {
+                        X.recc[r] = uint32_t(r - p2) | (uint32_t(r - p3) << 16);
+                        if (r - p2 >= kBandRing)
+                            flags[p2] = 1;
+                        if (n == 4 && r - p3 >= kBandRing)
+                            flags[p3] = 1;
+                    }
                 }
                 else
                 {
@@ -171,12 +228,15 @@ __device__ void band_row_program(const WinGraph<SizeT>& g, int V, const Band& B,
                     a |= (fit ? uint32_t(n) : kNpEsc) << 8;
                     bw = 0x80000000u | uint32_t(off);
                 }
-                X.reca[r] = a;
-                X.recb[r] = bw;
+                X.reca[r]  = a;
+                X.recb[r]  = bw;
+                X.flags[r] = 0; // set by the forward pass for rows it spills
             }
             xbase += total;
         }
     }
+    if (lane == 0)
+        X.bx[(V + kStageRows - 1) / kStageRows] = xbase;
     wave_sync();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     for (int r = lane + 1; r <= V; r += kWave)
@@ -189,10 +249,39 @@ __device__ void band_row_program(const WinGraph<SizeT>& g, int V, const Band& B,
 
 // Predecessor values F(p, d + CPL*lane + c), c = 0..CPL (flat get_scores()
 // reads, :123-173).  Lanes whose groups are cut read clamped garbage.
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int v2i_t __attribute__((ext_vector_type(2)));
+
+// q points at an aligned group of CPL cells; F[0] is the element before it
+#define GWAMD_BAND_LOAD_ROW(NAME, AS)                                                                        \
+    template <typename ScoreT, int CPL>                                                                      \
+    __device__ __forceinline__ void NAME(AS const ScoreT* q, int(&F)[CPL + 1])                               \
+    {                                                                                                        \
+        F[0] = int(q[-1]);                                                                                   \
+        if constexpr (sizeof(ScoreT) == 4 && CPL == 4)                                                       \
+        {                                                                                                    \
+            const v4i_t v = *reinterpret_cast<AS const v4i_t*>(q);                                          \
+            F[1] = v.x, F[2] = v.y, F[3] = v.z, F[4] = v.w;                                         \
+        }                                                                                                    \
+        else if constexpr (sizeof(ScoreT) == 2 && CPL == 4)                                                  \
+        {                                                                                                    \
+            const v2i_t v = *reinterpret_cast<AS const v2i_t*>(q);                                          \
+            F[1] = int(int16_t(v.x & 0xffff)), F[2] = v.x >> 16;                                             \
+            F[3] = int(int16_t(v.y & 0xffff)), F[4] = v.y >> 16;                             \
+        }                                                                                                    \
+        else                                                                                                 \
+        {                                                                                                    \
+            _Pragma("unroll") for (int c = 0; c < CPL; c++) F[c + 1] = int(q[c]);                            \
+        }                                                                                                    \
+    }
+GWAMD_BAND_LOAD_ROW(band_load_lds, GWAMD_LDS)
+GWAMD_BAND_LOAD_ROW(band_load_glb, )
+#undef GWAMD_BAND_LOAD_ROW
+
 template <typename ScoreT, int CPL>
-__device__ __forceinline__ void band_fetch(int p, int d, int r, const int (&Hp)[CPL], int prevF0, const ScoreT* ring,
-                                           const ScoreT* spill, int rowsz, int gap, int minv, int lane,
-                                           int (&F)[CPL + 1])
+__device__ __forceinline__ void band_fetch(int p, int d, int r, const int (&Hp)[CPL], int prevF0,
+                                           GWAMD_LDS ScoreT* ring, const ScoreT* spill, int rowsz, int gap, int minv,
+                                           int lane, int (&F)[CPL + 1])
 {
     if (p == 0)
     {
@@ -217,26 +306,47 @@ __device__ __forceinline__ void band_fetch(int p, int d, int r, const int (&Hp)[
             F[c] = __builtin_amdgcn_update_dpp(minv, Hp[c - 1], 0x130, 0xf, 0xf, false); // wave_shl:1
         return;
     }
-    const ScoreT* row = (r - p < kBandRing) ? ring + (p & (kBandRing - 1)) * rowsz : spill + size_t(p) * rowsz;
-    const int gmax    = rowsz / CPL - 1;
-    const int gi      = min(d / CPL + lane + 1, gmax);
-    const ScoreT* q   = row + gi * CPL;
-    F[0]              = int(q[-1]);
-#pragma unroll
-    for (int c = 0; c < CPL; c++)
-        F[c + 1] = int(q[c]);
+    const int gmax = rowsz / CPL - 1;
+    const int gi   = min(d / CPL + lane + 1, gmax);
+    if (r - p < kBandRing)
+        band_load_lds<ScoreT, CPL>(ring + (p & (kBandRing - 1)) * rowsz + gi * CPL, F);
+    else
+    {
+        band_load_glb<ScoreT, CPL>(spill + size_t(p) * rowsz + gi * CPL, F);
+        vm_drain(); // rare path: keep its loads from forcing waits where the paths join
+    }
 }
 
 // Forward pass over rows 1..V.  Returns the end row (first sink with the
 // strictly greatest get_score(row, L), :349-365).
-template <typename ScoreT, typename SizeT, int CPL>
-__device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, const uint8_t* read, int L,
-                            const Band& B, const Scores sc, ScoreT* ring, ScoreT* spill, int rowsz, int lane)
+//
+// Rows with at most one predecessor that is not listed (the common case) take
+// a straight path: one predecessor fetch, the closure and the codes without
+// predecessor loops.  Row records and read bytes are software-pipelined: the
+// record of row r+2 and the read bytes of row r+1 are requested while row r is
+// computed.
+template <typename ScoreT, int CPL>
+__device__ __forceinline__ uint32_t band_read_bytes(GWAMD_LDS const uint8_t* read, int bs, int lane)
 {
+    if constexpr (CPL == 4)
+        return *reinterpret_cast<GWAMD_LDS const uint32_t*>(read + bs + 4 * lane);
+    else
+        return uint32_t(*reinterpret_cast<GWAMD_LDS const uint16_t*>(read + bs + 2 * lane));
+}
+
+template <typename ScoreT, typename SizeT, int CPL>
+__device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, GWAMD_LDS const uint8_t* read, int L,
+                            const Band& B, const Scores sc, GWAMD_LDS ScoreT* ring, GWAMD_LDS uint32_t* stage,
+                            ScoreT* spill, int rowsz, int lane, BandProf& bp)
+{
+    const uint64_t f_t0 = BandProf::now();
     const int gap  = sc.gap;
     const int bw   = B.bw;
     const int minv = int(band_min_value<ScoreT>(sc));
-    const int T0 = minv - sc.match, T1 = minv - sc.mismatch, T2 = minv - gap;
+    // an out-of-band traceback comparison matches only values minv - match,
+    // minv - mismatch, minv - gap: rows holding a value <= the largest of them
+    // are spilled so the slow path can read them
+    const int Tmax = max(max(minv - sc.match, minv - sc.mismatch), minv - gap);
     // ring padding (idx bw+1 ..) is never overwritten by row stores
     for (int k = lane; k < kBandRing * rowsz; k += kWave)
         if (k % rowsz >= bw + CPL)
@@ -250,168 +360,97 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, c
 #pragma unroll
     for (int c = 0; c < CPL; c++)
         Hp[c] = (CPL * lane + c + 1) * gap;
-    int prevF0 = 0, prev_bs = 0;
+    int prevF0 = 0;
+    int bsv    = 0; // lane k < kBandRing: band start of the row in ring slot k
     int best = INT_MIN, end_row = 0;
-    const int minv_s = minv;
     wave_sync();
 
-    uint32_t ca = 0, cb = 0, na = 0, nb = 0;
-    if (1 + lane <= V)
-        ca = X.reca[1 + lane], cb = X.recb[1 + lane];
-    if (65 + lane <= V)
-        na = X.reca[65 + lane], nb = X.recb[65 + lane];
-    for (int r0 = 1; r0 <= V; r0 += kWave)
+    GWAMD_LDS uint32_t* srec = stage;
+    GWAMD_LDS int32_t* sxl   = (GWAMD_LDS int32_t*)(stage + 3 * kStageRows);
+    for (int r0 = 1; r0 <= V; r0 += kStageRows)
     {
-        const int rend = min(V, r0 + kWave - 1);
+        const int rend = min(V, r0 + kStageRows - 1);
+        const uint64_t st0 = BandProf::now();
+        // one wait per block: records and the block's predecessor lists
+        uint32_t av[kStageRows / kWave], bv[kStageRows / kWave], cv[kStageRows / kWave];
+#pragma unroll
+        for (int u = 0; u < kStageRows / kWave; u++)
+        {
+            const int rr = r0 + u * kWave + lane;
+            av[u]        = rr <= V ? X.reca[rr] : 0u;
+            bv[u]        = rr <= V ? X.recb[rr] : 0u;
+            cv[u]        = rr <= V ? X.recc[rr] : 0u;
+        }
+        const int xs  = uniform(X.bx[(r0 - 1) / kStageRows]);
+        const int xe  = uniform(X.bx[(r0 - 1) / kStageRows + 1]);
+        const int nxs = min(xe - xs, kStageXl);
+        int xv[kStageXl / kWave];
+#pragma unroll
+        for (int u = 0; u < kStageXl / kWave; u++)
+        {
+            const int k = u * kWave + lane;
+            xv[u]       = k < nxs ? X.xl[xs + k] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kStageRows / kWave; u++)
+        {
+            srec[3 * (u * kWave + lane)]     = av[u];
+            srec[3 * (u * kWave + lane) + 1] = bv[u];
+            srec[3 * (u * kWave + lane) + 2] = cv[u];
+        }
+#pragma unroll
+        for (int u = 0; u < kStageXl / kWave; u++)
+            sxl[u * kWave + lane] = xv[u];
+        wave_sync();
+
+        uint32_t a   = uint32_t(uniform(int(srec[0])));
+        uint32_t b   = uint32_t(uniform(int(srec[1])));
+        uint32_t c2  = uint32_t(uniform(int(srec[2])));
+        const int q1 = min(1, rend - r0);
+        uint32_t a1  = uint32_t(uniform(int(srec[3 * q1])));
+        uint32_t b1  = uint32_t(uniform(int(srec[3 * q1 + 1])));
+        uint32_t c1  = uint32_t(uniform(int(srec[3 * q1 + 2])));
+        uint32_t rbw = band_read_bytes<ScoreT, CPL>(read, ra_bs(a), lane);
+        bp.add(kBpStageCyc, BandProf::now() - st0);
+        bp.add(kBpRows, uint64_t(rend - r0 + 1));
         for (int r = r0; r <= rend; r++)
         {
-            const uint32_t a = __builtin_amdgcn_readlane(ca, r - r0);
-            const uint32_t b = __builtin_amdgcn_readlane(cb, r - r0);
-            const int bs     = ra_bs(a);
-            const int gb     = ra_base(a);
-            const int np  = band_np2<SizeT>(g, r, a, b);
-            const int npp = np == 0 ? 1 : np;
-            // read bases of this lane's cells: columns bs+1+t read read[bs+t]
+            // prefetch: record of row r+2, read bytes of row r+1
+            const int q2       = min(r + 2, rend) - r0;
+            const uint32_t va2 = srec[3 * q2];
+            const uint32_t vb2 = srec[3 * q2 + 1];
+            const uint32_t vc2 = srec[3 * q2 + 2];
+            const uint32_t rbn = band_read_bytes<ScoreT, CPL>(read, ra_bs(a1), lane);
+
+            const int bs = ra_bs(a);
+            const int gb = ra_base(a);
+            const int f  = ra_np(a);
             int sig[CPL];
-            {
-                const uint8_t* rp = read + bs + CPL * lane;
 #pragma unroll
-                for (int c = 0; c < CPL; c++)
-                    sig[c] = (int(rp[c]) == gb) ? sc.match : sc.mismatch;
-            }
-            int F0[CPL + 1], F1[CPL + 1];
-            int d0 = 0, d1 = 0, p0 = 0, p1 = 0;
+            for (int c = 0; c < CPL; c++)
+                sig[c] = (int((rbw >> (8 * c)) & 0xffu) == gb) ? sc.match : sc.mismatch;
+
             int v[CPL];
-#pragma unroll
-            for (int c = 0; c < CPL; c++)
-                v[c] = kNeg;
-            int c0max = INT_MIN;
-            for (int k = 0; k < npp; k++)
-            {
-                const int p  = np == 0 ? 0 : uniform(band_pred2<SizeT>(g, X, r, a, b, k));
-                const int pb = (p == r - 1) ? prev_bs : (p == 0 ? 0 : B.start(p));
-                const int d  = bs - pb;
-                int Fk[CPL + 1];
-                band_fetch<ScoreT, CPL>(p, d, r, Hp, prevF0, ring, spill, rowsz, gap, minv, lane, Fk);
-#pragma unroll
-                for (int c = 0; c < CPL; c++)
-                {
-                    const int t    = CPL * lane + c;
-                    const bool cut = (t & ~3) + d >= bw + 4;
-                    const int val  = cut ? minv : trunc_score<ScoreT>(max(Fk[c] + sig[c], Fk[c + 1] + gap));
-                    v[c]           = max(v[c], val);
-                }
-                c0max = max(c0max, __builtin_amdgcn_readlane(Fk[0], 0));
-                if (k == 0)
-                {
-#pragma unroll
-                    for (int c = 0; c <= CPL; c++)
-                        F0[c] = Fk[c];
-                    d0 = d, p0 = p;
-                }
-                else if (k == 1)
-                {
-#pragma unroll
-                    for (int c = 0; c <= CPL; c++)
-                        F1[c] = Fk[c];
-                    d1 = d, p1 = p;
-                }
-            }
-            // column 0 (:219-245): F(r, 0) is the column-0 value when the band
-            // starts at 0, else the minv initialize_band writes at index 0
-            const int col0 = np == 0 ? gap : trunc_score<ScoreT>(c0max + gap);
-            const int carry = bs == 0 ? col0 : minv;
-            // horizontal closure, E domain: E(t) = H(t) - (t+1)*gap, E(-1) = carry
-            int m[CPL];
-            int run = lane == 0 ? carry : kNeg;
-#pragma unroll
-            for (int c = 0; c < CPL; c++)
-            {
-                run  = max(run, v[c] - egap[c]);
-                m[c] = run;
-            }
-            const int incl = wave_incl_max_dpp(run);
-            const int excl = __builtin_amdgcn_update_dpp(kNeg, incl, 0x138, 0xf, 0xf, false);
+            int carry;
             int H[CPL];
-#pragma unroll
-            for (int c = 0; c < CPL; c++)
-                H[c] = trunc_score<ScoreT>(max(m[c], excl) + egap[c]);
-            // traceback codes (:367-477 with get_score(): minv beyond idx bw)
-            const int vlim = L - bs - 1; // cells t <= vlim are columns <= L
             int code[CPL];
-            bool found[CPL];
-#pragma unroll
-            for (int c = 0; c < CPL; c++)
-                code[c] = 3, found[c] = false;
-            for (int k = 0; k < npp; k++)
-            {
-                int Fk[CPL + 1];
-                int d;
-                if (k == 0)
-                {
-#pragma unroll
-                    for (int c = 0; c <= CPL; c++)
-                        Fk[c] = F0[c];
-                    d = d0;
-                }
-                else if (k == 1)
-                {
-#pragma unroll
-                    for (int c = 0; c <= CPL; c++)
-                        Fk[c] = F1[c];
-                    d = d1;
-                }
-                else
-                {
-                    const int p  = uniform(band_pred2<SizeT>(g, X, r, a, b, k));
-                    const int pb = (p == r - 1) ? prev_bs : (p == 0 ? 0 : B.start(p));
-                    d            = bs - pb;
-                    band_fetch<ScoreT, CPL>(p, d, r, Hp, prevF0, ring, spill, rowsz, gap, minv, lane, Fk);
-                }
+            auto closure = [&]() {
+                // E domain: E(t) = H(t) - (t+1)*gap, E(-1) = carry
+                int m[CPL];
+                int run = lane == 0 ? carry : kNeg;
 #pragma unroll
                 for (int c = 0; c < CPL; c++)
                 {
-                    const int t  = CPL * lane + c;
-                    const int gA = (d + t > bw) ? minv : Fk[c];
-                    if (!found[c] && gA + sig[c] == H[c])
-                        code[c] = k << 2, found[c] = true;
+                    run  = max(run, v[c] - egap[c]);
+                    m[c] = run;
                 }
-            }
-            for (int k = 0; k < npp; k++)
-            {
-                int Fk[CPL + 1];
-                int d;
-                if (k == 0)
-                {
-#pragma unroll
-                    for (int c = 0; c <= CPL; c++)
-                        Fk[c] = F0[c];
-                    d = d0;
-                }
-                else if (k == 1)
-                {
-#pragma unroll
-                    for (int c = 0; c <= CPL; c++)
-                        Fk[c] = F1[c];
-                    d = d1;
-                }
-                else
-                {
-                    const int p  = uniform(band_pred2<SizeT>(g, X, r, a, b, k));
-                    const int pb = (p == r - 1) ? prev_bs : (p == 0 ? 0 : B.start(p));
-                    d            = bs - pb;
-                    band_fetch<ScoreT, CPL>(p, d, r, Hp, prevF0, ring, spill, rowsz, gap, minv, lane, Fk);
-                }
+                const int incl = wave_incl_max_dpp(run);
+                const int excl = __builtin_amdgcn_update_dpp(kNeg, incl, 0x138, 0xf, 0xf, false);
 #pragma unroll
                 for (int c = 0; c < CPL; c++)
-                {
-                    const int t  = CPL * lane + c;
-                    const int gB = (d + t + 1 > bw) ? minv : Fk[c + 1];
-                    if (!found[c] && gB + gap == H[c])
-                        code[c] = (k << 2) | 1, found[c] = true;
-                }
-            }
-            {
+                    H[c] = trunc_score<ScoreT>(max(m[c], excl) + egap[c]);
+            };
+            auto horiz = [&](bool (&found)[CPL]) {
                 int left = __builtin_amdgcn_update_dpp(carry, H[CPL - 1], 0x138, 0xf, 0xf, false);
 #pragma unroll
                 for (int c = 0; c < CPL; c++)
@@ -420,21 +459,222 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, c
                         code[c] = 2, found[c] = true;
                     left = H[c];
                 }
+            };
+
+            // rows with 1..4 inline predecessors (distances in rec_b, rec_c) and
+            // sources: predecessor values stay in registers, one pass each
+            auto rowk = [&](auto npc) {
+                constexpr int NP = decltype(npc)::value;
+                int d[NP];
+                int F[NP][CPL + 1];
+#pragma unroll
+                for (int k = 0; k < NP; k++)
+                {
+                    int p = 0, dk = bs;
+                    if (f != 0)
+                    {
+                        const uint32_t w    = k < 2 ? b : c2;
+                        const int dist      = int((k & 1) ? (w >> 16) : (w & 0xffffu));
+                        p                   = r - dist;
+                        const int pb        = dist < kBandRing ? __builtin_amdgcn_readlane(bsv, p & (kBandRing - 1))
+                                                               : B.start(p);
+                        dk                  = bs - pb;
+                    }
+                    d[k] = dk;
+                    band_fetch<ScoreT, CPL>(p, dk, r, Hp, prevF0, ring, spill, rowsz, gap, minv, lane, F[k]);
+                }
+                int c0max = INT_MIN;
+#pragma unroll
+                for (int c = 0; c < CPL; c++)
+                {
+                    const int t = CPL * lane + c;
+                    int vv      = kNeg;
+#pragma unroll
+                    for (int k = 0; k < NP; k++)
+                    {
+                        const bool cut = (t & ~3) + d[k] >= bw + 4;
+                        const int val  = trunc_score<ScoreT>(max(F[k][c] + sig[c], F[k][c + 1] + gap));
+                        vv             = max(vv, cut ? minv : val);
+                    }
+                    v[c] = vv;
+                }
+                // column 0 (:219-245): F(r, 0) is the column-0 value when the
+                // band starts at 0, else the minv initialize_band writes at idx 0
+                carry = minv;
+                if (bs == 0)
+                {
+#pragma unroll
+                    for (int k = 0; k < NP; k++)
+                        c0max = max(c0max, __builtin_amdgcn_readlane(F[k][0], 0));
+                    carry = f == 0 ? gap : trunc_score<ScoreT>(c0max + gap);
+                }
+                closure();
+                // first diagonal slot, else first vertical slot (:367-477)
+                bool found[CPL];
+#pragma unroll
+                for (int c = 0; c < CPL; c++)
+                {
+                    const int t = CPL * lane + c;
+                    int dsl = -1, vsl = -1;
+#pragma unroll
+                    for (int k = NP - 1; k >= 0; k--)
+                    {
+                        const int gA = (d[k] + t > bw) ? minv : F[k][c];
+                        const int gB = (d[k] + t + 1 > bw) ? minv : F[k][c + 1];
+                        dsl          = (gA + sig[c] == H[c]) ? k : dsl;
+                        vsl          = (gB + gap == H[c]) ? k : vsl;
+                    }
+                    code[c]  = dsl >= 0 ? (dsl << 2) : (vsl >= 0 ? ((vsl << 2) | 1) : 3);
+                    found[c] = dsl >= 0 || vsl >= 0;
+                }
+                horiz(found);
+            };
+            const bool inl = f <= 4 && !(b >> 31);
+            bp.add(kBpMulti, f >= 2 ? 1 : 0);
+            if (inl && f <= 1)
+                rowk(std::integral_constant<int, 1>{});
+            else if (inl && f == 2)
+                rowk(std::integral_constant<int, 2>{});
+            else if (inl && f == 3)
+                rowk(std::integral_constant<int, 3>{});
+            else if (inl && f == 4)
+                rowk(std::integral_constant<int, 4>{});
+            else
+            {
+                const int np  = band_np2<SizeT>(g, r, a, b);
+                const int npp = np == 0 ? 1 : np;
+                // k-th predecessor row, predecessor lists from the staged block
+                auto pred = [&](int k) -> int {
+                    if (f == 0)
+                        return 0;
+                    if (f == int(kNpEsc))
+                    {
+                        const int pr = uniform(pred_row(g, int(g.sorted[r - 1]), k));
+                        vm_drain();
+                        return pr;
+                    }
+                    if (b >> 31)
+                    {
+                        const int rel = int(b & 0x7fffffffu) - xs + k;
+                        if (rel < nxs)
+                            return uniform(int(sxl[rel]));
+                        const int pr = uniform(int(X.xl[int(b & 0x7fffffffu) + k]));
+                        vm_drain();
+                        return pr;
+                    }
+                    const uint32_t w = k < 2 ? b : c2;
+                    return r - int((k & 1) ? (w >> 16) : (w & 0xffffu));
+                };
+                auto pbs = [&](int p) -> int {
+                    return p == 0 ? 0
+                                  : (r - p < kBandRing ? __builtin_amdgcn_readlane(bsv, p & (kBandRing - 1))
+                                                       : B.start(p));
+                };
+                int F0[CPL + 1], F1[CPL + 1];
+                int d0 = 0, d1 = 0;
+#pragma unroll
+                for (int c = 0; c < CPL; c++)
+                    v[c] = kNeg;
+                int c0max = INT_MIN;
+                for (int k = 0; k < npp; k++)
+                {
+                    const int p = pred(k);
+                    const int d = bs - pbs(p);
+                    int Fk[CPL + 1];
+                    band_fetch<ScoreT, CPL>(p, d, r, Hp, prevF0, ring, spill, rowsz, gap, minv, lane, Fk);
+#pragma unroll
+                    for (int c = 0; c < CPL; c++)
+                    {
+                        const int t    = CPL * lane + c;
+                        const bool cut = (t & ~3) + d >= bw + 4;
+                        const int val  = cut ? minv : trunc_score<ScoreT>(max(Fk[c] + sig[c], Fk[c + 1] + gap));
+                        v[c]           = max(v[c], val);
+                    }
+                    c0max = max(c0max, __builtin_amdgcn_readlane(Fk[0], 0));
+                    if (k == 0)
+                    {
+#pragma unroll
+                        for (int c = 0; c <= CPL; c++)
+                            F0[c] = Fk[c];
+                        d0 = d;
+                    }
+                    else if (k == 1)
+                    {
+#pragma unroll
+                        for (int c = 0; c <= CPL; c++)
+                            F1[c] = Fk[c];
+                        d1 = d;
+                    }
+                }
+                const int col0 = np == 0 ? gap : trunc_score<ScoreT>(c0max + gap);
+                carry          = bs == 0 ? col0 : minv;
+                closure();
+                // codes (:367-477 with get_score(): minv beyond idx bw)
+                bool found[CPL];
+#pragma unroll
+                for (int c = 0; c < CPL; c++)
+                    code[c] = 3, found[c] = false;
+                for (int pass = 0; pass < 2; pass++)
+                {
+                    for (int k = 0; k < npp; k++)
+                    {
+                        int Fk[CPL + 1];
+                        int d;
+                        if (k == 0)
+                        {
+#pragma unroll
+                            for (int c = 0; c <= CPL; c++)
+                                Fk[c] = F0[c];
+                            d = d0;
+                        }
+                        else if (k == 1)
+                        {
+#pragma unroll
+                            for (int c = 0; c <= CPL; c++)
+                                Fk[c] = F1[c];
+                            d = d1;
+                        }
+                        else
+                        {
+                            const int p = pred(k);
+                            d           = bs - pbs(p);
+                            band_fetch<ScoreT, CPL>(p, d, r, Hp, prevF0, ring, spill, rowsz, gap, minv, lane, Fk);
+                        }
+#pragma unroll
+                        for (int c = 0; c < CPL; c++)
+                        {
+                            const int t = CPL * lane + c;
+                            if (pass == 0)
+                            {
+                                const int gA = (d + t > bw) ? minv : Fk[c];
+                                if (!found[c] && gA + sig[c] == H[c])
+                                    code[c] = k << 2, found[c] = true;
+                            }
+                            else
+                            {
+                                const int gB = (d + t + 1 > bw) ? minv : Fk[c + 1];
+                                if (!found[c] && gB + gap == H[c])
+                                    code[c] = (k << 2) | 1, found[c] = true;
+                            }
+                        }
+                    }
+                }
+                horiz(found);
             }
+
             // store codes (one byte per cell)
             {
                 uint8_t* crow = X.codes + size_t(r) * bw + CPL * lane;
-                if (CPL == 4)
+                if constexpr (CPL == 4)
                 {
-                    const uint32_t w4 = uint32_t(code[0]) | (uint32_t(code[1 % CPL]) << 8) |
-                                        (uint32_t(code[2 % CPL]) << 16) | (uint32_t(code[3 % CPL]) << 24);
+                    const uint32_t w4 = uint32_t(code[0]) | (uint32_t(code[1]) << 8) | (uint32_t(code[2]) << 16) |
+                                        (uint32_t(code[3]) << 24);
                     *reinterpret_cast<uint32_t*>(crow) = w4;
                 }
                 else
                 {
-#pragma unroll
-                    for (int c = 0; c < CPL; c++)
-                        crow[c] = uint8_t(code[c]);
+                    const uint16_t w2 = uint16_t(code[0] | (code[1 % CPL] << 8));
+                    *reinterpret_cast<uint16_t*>(crow) = w2;
                 }
             }
             // end cell candidates (sinks in topological order, strict >)
@@ -443,8 +683,8 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, c
                 int sval;
                 if (L >= bs + 1 && L <= bs + bw)
                 {
-                    const int t  = L - bs - 1;
-                    int hv       = H[0];
+                    const int t = L - bs - 1;
+                    int hv      = H[0];
 #pragma unroll
                     for (int c = 1; c < CPL; c++)
                         hv = (t % CPL == c) ? H[c] : hv;
@@ -453,24 +693,27 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, c
                 else if (L == bs)
                     sval = carry;
                 else
-                    sval = minv_s;
+                    sval = minv;
                 if (best < sval)
                     best = sval, end_row = r;
             }
-            // rows an out-of-band traceback comparison could match (T values)
-            bool tv = false;
+            const int vlim = L - bs - 1; // cells t <= vlim are columns <= L
+            bool tv        = false;
 #pragma unroll
             for (int c = 0; c < CPL; c++)
-            {
-                const int t = CPL * lane + c;
-                tv |= t <= vlim && (H[c] == T0 || H[c] == T1 || H[c] == T2);
-            }
+                tv |= (CPL * lane + c <= vlim) && H[c] <= Tmax;
             const bool tflag = __builtin_amdgcn_ballot_w64(tv) != 0;
             // ring row: position idx + CPL - 1
-            ScoreT* rrow = ring + (r & (kBandRing - 1)) * rowsz;
-            if (CPL == 4 && sizeof(ScoreT) == 4)
+            GWAMD_LDS ScoreT* rrow = ring + (r & (kBandRing - 1)) * rowsz;
+            if constexpr (CPL == 4 && sizeof(ScoreT) == 4)
             {
-                *reinterpret_cast<int4*>(rrow + CPL * (lane + 1)) = make_int4(H[0], H[1 % CPL], H[2 % CPL], H[3 % CPL]);
+                v4i_t q = {H[0], H[1 % CPL], H[2 % CPL], H[3 % CPL]};
+                *reinterpret_cast<GWAMD_LDS v4i_t*>(rrow + CPL * (lane + 1)) = q;
+            }
+            else if constexpr (CPL == 4 && sizeof(ScoreT) == 2)
+            {
+                v2i_t q = {int((H[0] & 0xffff) | (H[1 % CPL] << 16)), int((H[2 % CPL] & 0xffff) | (H[3 % CPL] << 16))};
+                *reinterpret_cast<GWAMD_LDS v2i_t*>(rrow + CPL * (lane + 1)) = q;
             }
             else
             {
@@ -480,14 +723,13 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, c
             }
             if (lane == 0)
                 rrow[CPL - 1] = ScoreT(carry);
+            bsv = lane == (r & (kBandRing - 1)) ? bs : bsv;
             if (ra_spill(a) || tflag)
             {
                 ScoreT* srow = spill + size_t(r) * rowsz;
 #pragma unroll
                 for (int c = 0; c < CPL; c++)
                     srow[CPL * (lane + 1) + c] = ScoreT(H[c]);
-                if (lane == 0)
-                    srow[CPL - 1] = ScoreT(carry);
                 const int pg = rowsz / CPL - (kWave + 1); // padding groups
                 if (lane < pg)
                 {
@@ -495,27 +737,30 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, c
                     for (int c = 0; c < CPL; c++)
                         srow[CPL * (kWave + 1 + lane) + c] = ScoreT(minv);
                 }
+                if (lane == 0)
+                {
+                    srow[CPL - 1] = ScoreT(carry);
+                    X.flags[r]    = 1;
+                }
             }
-            if (lane == 0)
-            {
-                X.flags[r] = uint8_t(tflag ? 1 : 0);
-                if (bs == 0)
-                    X.col0[r] = carry;
-            }
+            if (bs == 0 && lane == 0)
+                X.col0[r] = carry;
             wave_sync();
 #pragma unroll
             for (int c = 0; c < CPL; c++)
                 Hp[c] = H[c];
-            prevF0  = carry;
-            prev_bs = bs;
+            prevF0 = carry;
+            a      = a1;
+            b      = b1;
+            c2     = c1;
+            rbw    = rbn;
+            a1     = uint32_t(uniform(int(va2)));
+            b1     = uint32_t(uniform(int(vb2)));
+            c1     = uint32_t(uniform(int(vc2)));
         }
-        ca = na, cb = nb;
-        na = nb = 0;
-        if (r0 + 2 * kWave + lane <= V)
-            na = X.reca[r0 + 2 * kWave + lane], nb = X.recb[r0 + 2 * kWave + lane];
+        wave_sync(); // the staging buffers are rewritten by the next block
     }
-
-
+    bp.add(kBpFwdCyc, BandProf::now() - f_t0);
     return end_row;
 }
 
@@ -548,9 +793,10 @@ __device__ int band_get_slow(int p, int col, const Band& B, const BandAux& X, co
 template <typename ScoreT, typename SizeT, int CPL>
 __device__ int band_traceback(const WinGraph<SizeT>& g, const BandAux& X, int V, const uint8_t* read, int L,
                               int end_row, const Band& B, const Scores sc, const ScoreT* spill, int rowsz,
-                              uint8_t* tile, uint32_t* trec, SizeT* ag, SizeT* ar, int aln_cap,
-                              int lane)
+                              GWAMD_LDS uint8_t* tile, SizeT* ag, SizeT* ar, int aln_cap,
+                              int lane, BandProf& bp)
 {
+    const uint64_t t_t0 = BandProf::now();
     const int bw    = B.bw;
     const int gap   = sc.gap;
     const int minv  = int(band_min_value<ScoreT>(sc));
@@ -559,6 +805,8 @@ __device__ int band_traceback(const WinGraph<SizeT>& g, const BandAux& X, int V,
     int i           = uniform(end_row), j = L;
     int prev_i = 0, prev_j = 0;
     int ti0 = INT_MIN / 2;
+    uint32_t ta = 0, tb = 0, tcw = 0; // row records of the tile rows, lane k: row ti0 + k
+    static_assert(kBandTile == kWave, "tile records are held one per lane");
     int n = 0, loops = 0;
     const int bound = L + V + 2;
     int eg = 0, er = 0;
@@ -588,6 +836,7 @@ __device__ int band_traceback(const WinGraph<SizeT>& g, const BandAux& X, int V,
         {
             if (i < ti0 || i >= ti0 + kBandTile)
             {
+                const uint64_t tt0 = BandProf::now();
                 ti0 = max(1, i - (kBandTile - 1));
                 wave_sync();
                 constexpr int kPer = kBandTile * 256 / 16 / kWave; // bw <= 256
@@ -600,23 +849,24 @@ __device__ int band_traceback(const WinGraph<SizeT>& g, const BandAux& X, int V,
                     const int tc  = (t % per_row) * 16;
                     const int rr  = ti0 + tr;
                     const bool ok = tr < kBandTile && rr <= V;
-                    uint4 q       = ok ? *reinterpret_cast<const uint4*>(X.codes + size_t(rr) * bw + tc)
-                                       : make_uint4(0, 0, 0, 0);
+                    v4i_t q       = {0, 0, 0, 0};
+                    if (ok)
+                        q = *reinterpret_cast<const v4i_t*>(X.codes + size_t(rr) * bw + tc);
                     if (tr < kBandTile)
-                        *reinterpret_cast<uint4*>(tile + tr * bw + tc) = q;
+                        *reinterpret_cast<GWAMD_LDS v4i_t*>(tile + tr * bw + tc) = q;
                 }
                 {
-                    const int rr = ti0 + lane;
-                    if (lane < kBandTile)
-                    {
-                        trec[2 * lane]     = rr <= V ? X.reca[rr] : 0u;
-                        trec[2 * lane + 1] = rr <= V ? X.recb[rr] : 0u;
-                    }
+                    const int rr = ti0 + lane; // kBandTile == kWave: one record per lane
+                    ta           = rr <= V ? X.reca[rr] : 0u;
+                    tb           = rr <= V ? X.recb[rr] : 0u;
+                    tcw          = rr <= V ? X.recc[rr] : 0u;
                 }
                 wave_sync();
+                bp.add(kBpTileCyc, BandProf::now() - tt0);
             }
-            const uint32_t a = uint32_t(uniform(int(trec[2 * (i - ti0)])));
-            const uint32_t b = uint32_t(uniform(int(trec[2 * (i - ti0) + 1])));
+            const uint32_t a = __builtin_amdgcn_readlane(ta, i - ti0);
+            const uint32_t b = __builtin_amdgcn_readlane(tb, i - ti0);
+            const uint32_t c = __builtin_amdgcn_readlane(tcw, i - ti0);
             const int bs     = ra_bs(a);
             if (j == 0)
             {
@@ -626,7 +876,7 @@ __device__ int band_traceback(const WinGraph<SizeT>& g, const BandAux& X, int V,
                 const int npp = np == 0 ? 1 : np;
                 for (int k = 0; k < npp && !found; k++)
                 {
-                    const int p   = np == 0 ? 0 : band_pred2<SizeT>(g, X, i, a, b, k);
+                    const int p   = np == 0 ? 0 : band_pred2<SizeT>(g, X, i, a, b, c, k);
                     const int f0  = p == 0 ? 0 : (B.start(p) == 0 ? int(X.col0[p]) : minv);
                     if (sij == f0 + gap)
                         pi = p, pj = 0, found = true;
@@ -645,8 +895,20 @@ __device__ int band_traceback(const WinGraph<SizeT>& g, const BandAux& X, int V,
                     pi = i, pj = j - 1, found = true;
                 else if (dir != 3)
                 {
-                    const int np = band_np2<SizeT>(g, i, a, b);
-                    pi           = np == 0 ? 0 : uniform(band_pred2<SizeT>(g, X, i, a, b, code >> 2));
+                    const int f = ra_np(a);
+                    if (f == 0)
+                        pi = 0;
+                    else if (f != int(kNpEsc) && !(b >> 31))
+                    {
+                        const int k      = code >> 2;
+                        const uint32_t w = k < 2 ? b : c;
+                        pi               = i - int((k & 1) ? (w >> 16) : (w & 0xffffu));
+                    }
+                    else
+                    {
+                        pi = uniform(band_pred2<SizeT>(g, X, i, a, b, c, code >> 2));
+                        vm_drain();
+                    }
                     pj           = dir == 0 ? j - 1 : j;
                     found        = true;
                 }
@@ -660,7 +922,7 @@ __device__ int band_traceback(const WinGraph<SizeT>& g, const BandAux& X, int V,
                 const int npp  = np == 0 ? 1 : np;
                 for (int k = 0; k < npp && !found; k++)
                 {
-                    const int p = np == 0 ? 0 : band_pred2<SizeT>(g, X, i, a, b, k);
+                    const int p = np == 0 ? 0 : band_pred2<SizeT>(g, X, i, a, b, c, k);
                     bool kn;
                     const int gv = band_get_slow<ScoreT, CPL>(p, j - 1, B, X, spill, rowsz, gap, minv, kn);
                     if (kn && sij == gv + cost)
@@ -668,7 +930,7 @@ __device__ int band_traceback(const WinGraph<SizeT>& g, const BandAux& X, int V,
                 }
                 for (int k = 0; k < npp && !found; k++)
                 {
-                    const int p = np == 0 ? 0 : band_pred2<SizeT>(g, X, i, a, b, k);
+                    const int p = np == 0 ? 0 : band_pred2<SizeT>(g, X, i, a, b, c, k);
                     bool kn;
                     const int gv = band_get_slow<ScoreT, CPL>(p, j, B, X, spill, rowsz, gap, minv, kn);
                     if (kn && sij == gv + gap)
@@ -692,10 +954,16 @@ __device__ int band_traceback(const WinGraph<SizeT>& g, const BandAux& X, int V,
         }
         n++;
         if ((n & (kWave - 1)) == 0)
+        {
+            const uint64_t ft0 = BandProf::now();
             flush(n);
+            bp.add(kBpFlushCyc, BandProf::now() - ft0);
+        }
         i = prev_i;
         j = prev_j;
     }
+    bp.add(kBpSteps, uint64_t(n));
+    bp.add(kBpTbCyc, BandProf::now() - t_t0);
     if ((n & (kWave - 1)) != 0)
         flush(n);
     wave_sync();
@@ -718,11 +986,12 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
 
     uint8_t* lread          = lds;
     GWAMD_LDS uint8_t* work = (GWAMD_LDS uint8_t*)(lds) + d.lds_ring_off;
-    ScoreT* ring            = reinterpret_cast<ScoreT*>(lds + d.lds_ring_off);
+    GWAMD_LDS ScoreT* ring  = (GWAMD_LDS ScoreT*)(work);
     GWAMD_LDS uint8_t* shb  = (GWAMD_LDS uint8_t*)(lds) + d.lds_sh_off;
-    uint8_t* tile           = lds + d.lds_ring_off;
-    uint32_t* trec          = reinterpret_cast<uint32_t*>(tile + kBandTile * d.band_width);
+    GWAMD_LDS uint8_t* tile = work;
     const int rowsz          = d.score_stride;
+    // row-record staging after the ring (planned by poa_batch.cpp)
+    GWAMD_LDS uint32_t* stage = (GWAMD_LDS uint32_t*)(work + ((kBandRing * rowsz * int(sizeof(ScoreT)) + 15) & ~15));
 
     const size_t mn = size_t(d.max_nodes);
     WinGraph<SizeT> g;
@@ -747,9 +1016,11 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
     X.codes          = aux;
     X.reca           = reinterpret_cast<uint32_t*>(aux + d.aux_reca_off);
     X.recb           = reinterpret_cast<uint32_t*>(aux + d.aux_recb_off);
+    X.recc           = reinterpret_cast<uint32_t*>(aux + d.aux_recc_off);
     X.col0           = reinterpret_cast<int32_t*>(aux + d.aux_col0_off);
     X.flags          = aux + d.aux_flag_off;
     X.xl             = reinterpret_cast<int32_t*>(aux + d.aux_xl_off);
+    X.bx             = reinterpret_cast<int32_t*>(aux + d.aux_bx_off);
     X.xl_cap         = d.aux_xl_cap;
     int32_t* cscore  = b.cscore + w * mn;
     SizeT* cpred     = static_cast<SizeT*>(b.cpred) + w * mn * 4;
@@ -758,6 +1029,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
     SizeT* seq_begin = MSA ? static_cast<SizeT*>(b.seq_begin) + size_t(w) * d.max_seqs : nullptr;
 
     PhaseTimer ph;
+    BandProf bp;
     const WindowDesc wd = b.windows[w];
     const int nseq      = wd.num_seqs;
     int status          = kSuccess;
@@ -798,13 +1070,14 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
             ph.lap<kPhRowProg>();
             cells += int64_t(V + 1) * (d.band_width + kBandPad);
             const int end_row =
-                band_forward<ScoreT, SizeT, CPL>(g, X, V, lread, L, B, sc, ring, spill, rowsz, lane);
+                band_forward<ScoreT, SizeT, CPL>(g, X, V, (GWAMD_LDS const uint8_t*)(lds), L, B, sc, ring, stage,
+                                                 spill, rowsz, lane, bp);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             wave_sync();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             ph.lap<kPhForward>();
             const int alen = band_traceback<ScoreT, SizeT, CPL>(g, X, V, lread, L, end_row, B, sc, spill, rowsz, tile,
-                                                                trec, ag, ar, d.aln_cap, lane);
+                                                                ag, ar, d.aln_cap, lane, bp);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             wave_sync();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -873,7 +1146,15 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
     if (lane == 0)
     {
         if (b.phase)
+        {
             ph.store(b.phase + size_t(w) * kPhases);
+#ifdef GWAMD_BAND_PROFILE
+            // counters over the phase slots (read raw: value = phase_ms * 1e5)
+            const int slot[8] = {kPhBackbone, kPhAdd, kPhTopsort, kPhOutput, kPhRowProg, kPhTotal, -1, -1};
+            for (int i = 0; i < 6; i++)
+                b.phase[size_t(w) * kPhases + slot[i]] = int64_t(bp.v[i == 5 ? kBpTbCyc : (i == 4 ? kBpSteps : i)]);
+#endif
+        }
         b.final_nodes[w] = node_count;
         b.cells[w]       = cells;
     }

@@ -82,6 +82,8 @@ struct Dims
     int32_t aux_flag_off;
     int32_t aux_xl_off;
     int32_t aux_xl_cap;
+    int32_t aux_bx_off;     //   | per-256-row-block predecessor-list offsets (i32)
+    int32_t aux_recc_off;   //   | row records c (u32)
 };
 
 // Small shared region of the LDS kernel (kShBytes(waves) at Dims::lds_sh_off):
