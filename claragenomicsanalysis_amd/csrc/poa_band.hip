@@ -57,6 +57,20 @@ __device__ __forceinline__ void vm_drain()
     __builtin_amdgcn_s_waitcnt(0x0F70);
 }
 
+// Inclusive max-scan over the wave on sign-flipped values (x ^ 0x80000000
+// orders like x and 0 is the identity), so every step is one v_max_u32 with a
+// DPP source (row_shr 1/2/4/8, row_bcast 15/31; missing sources read 0).
+__device__ __forceinline__ uint32_t wave_incl_maxu_dpp(uint32_t v)
+{
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xf, 0xf, true)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xf, 0xf, true)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xf, 0xf, true)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xf, 0xf, true)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xa, 0xf, false)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xc, 0xf, false)));
+    return v;
+}
+
 template <typename ScoreT>
 __device__ __forceinline__ int trunc_score(int v)
 {
@@ -69,6 +83,7 @@ struct BandAux
     uint32_t* reca;  // [score_rows]
     uint32_t* recb;  // [score_rows]
     uint32_t* recc;  // [score_rows] distances to predecessors 2 and 3 (rows with 3-4 inline predecessors)
+    uint32_t* rece;  // [score_rows] band shifts / 4 of inline predecessors 0-3 (bytes; clamped to 255)
     int32_t* col0;   // [score_rows] F(r, 0) of rows with band_start 0
     uint8_t* flags;  // [score_rows] bit 0: row stored in the spill rows
     int32_t* xl;     // [xl_cap] predecessor rows of rows with np >= 3 (or far)
@@ -101,14 +116,30 @@ enum
     kBpFlushCyc,     // traceback cycles in path flushes
 };
 
+__device__ __forceinline__ BandAux as_global(BandAux X)
+{
+    X.codes = glb(X.codes);
+    X.reca  = glb(X.reca);
+    X.recb  = glb(X.recb);
+    X.recc  = glb(X.recc);
+    X.rece  = glb(X.rece);
+    X.col0  = glb(X.col0);
+    X.flags = glb(X.flags);
+    X.xl    = glb(X.xl);
+    X.bx    = glb(X.bx);
+    return X;
+}
+
 constexpr int kStageRows = 256;  // forward pass: row records staged in LDS per block
 constexpr int kStageXl   = 1024; // predecessor-list entries staged per block
 
 // k-th predecessor row of row r (0 = the virtual row 0) and the predecessor count
 template <typename SizeT>
-__device__ __forceinline__ int band_pred2(const WinGraph<SizeT>& g, const BandAux& X, int r, uint32_t a, uint32_t b,
+__device__ __forceinline__ int band_pred2(WinGraph<SizeT> g, BandAux X, int r, uint32_t a, uint32_t b,
                                           uint32_t c, int k)
 {
+    X = as_global(X);
+    g = as_global(g);
     const int np = ra_np(a);
     if (np == 0)
         return 0;
@@ -121,8 +152,9 @@ __device__ __forceinline__ int band_pred2(const WinGraph<SizeT>& g, const BandAu
 }
 
 template <typename SizeT>
-__device__ __forceinline__ int band_np2(const WinGraph<SizeT>& g, int r, uint32_t a, uint32_t b)
+__device__ __forceinline__ int band_np2(WinGraph<SizeT> g, int r, uint32_t a, uint32_t b)
 {
+    g = as_global(g);
     const int np = ra_np(a);
     return np == int(kNpEsc) ? int(g.in_cnt[int(g.sorted[r - 1])]) : np;
 }
@@ -132,9 +164,11 @@ __device__ __forceinline__ int band_np2(const WinGraph<SizeT>& g, int r, uint32_
 // reads the row from kBandRing or more rows later) are collected as LDS bytes
 // from the successor's side and folded into rec_a in a second pass.
 template <typename SizeT>
-__device__ void band_row_program(const WinGraph<SizeT>& g, int V, const Band& B, const BandAux& X, int lane,
+__device__ __forceinline__ void band_row_program(WinGraph<SizeT> g, int V, const Band& B, BandAux X, int lane,
                                  GWAMD_LDS uint8_t* flags)
 {
+    X = as_global(X);
+    g = as_global(g);
     constexpr int kRP = 4;
     for (int r = lane; r <= V + 1; r += kWave)
         flags[r] = 0;
@@ -227,6 +261,22 @@ __device__ void band_row_program(const WinGraph<SizeT>& g, int V, const Band& B,
                     }
                     a |= (fit ? uint32_t(n) : kNpEsc) << 8;
                     bw = 0x80000000u | uint32_t(off);
+                }
+                if (near2)
+                {
+                    // band shifts of the inline predecessors (/4, clamped: >= bw+4 cuts every group)
+                    const int bsr = B.start(r);
+                    auto sh4      = [&](int pk) { return uint32_t(min((bsr - (pk == 0 ? 0 : B.start(pk))) >> 2, 255)); };
+                    uint32_t ew   = n == 0 ? sh4(0) : 0u;
+                    if (n >= 1)
+                        ew |= sh4(p0[u]);
+                    if (n >= 2)
+                        ew |= sh4(p1[u]) << 8;
+                    if (n >= 3)
+                        ew |= sh4(p2) << 16;
+                    if (n >= 4)
+                        ew |= sh4(p3) << 24;
+                    X.rece[r] = ew;
                 }
                 X.reca[r]  = a;
                 X.recb[r]  = bw;
@@ -335,10 +385,12 @@ __device__ __forceinline__ uint32_t band_read_bytes(GWAMD_LDS const uint8_t* rea
 }
 
 template <typename ScoreT, typename SizeT, int CPL>
-__device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, GWAMD_LDS const uint8_t* read, int L,
+__device__ __forceinline__ int band_forward(WinGraph<SizeT> g, BandAux X, int V, GWAMD_LDS const uint8_t* read, int L,
                             const Band& B, const Scores sc, GWAMD_LDS ScoreT* ring, GWAMD_LDS uint32_t* stage,
                             ScoreT* spill, int rowsz, int lane, BandProf& bp)
 {
+    X = as_global(X);
+    g = as_global(g);
     const uint64_t f_t0 = BandProf::now();
     const int gap  = sc.gap;
     const int bw   = B.bw;
@@ -366,13 +418,14 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, G
     wave_sync();
 
     GWAMD_LDS uint32_t* srec = stage;
-    GWAMD_LDS int32_t* sxl   = (GWAMD_LDS int32_t*)(stage + 3 * kStageRows);
+    GWAMD_LDS int32_t* sxl   = (GWAMD_LDS int32_t*)(stage + 4 * kStageRows);
     for (int r0 = 1; r0 <= V; r0 += kStageRows)
     {
         const int rend = min(V, r0 + kStageRows - 1);
         const uint64_t st0 = BandProf::now();
         // one wait per block: records and the block's predecessor lists
-        uint32_t av[kStageRows / kWave], bv[kStageRows / kWave], cv[kStageRows / kWave];
+        uint32_t av[kStageRows / kWave], bv[kStageRows / kWave], cv[kStageRows / kWave],
+            ev[kStageRows / kWave];
 #pragma unroll
         for (int u = 0; u < kStageRows / kWave; u++)
         {
@@ -380,6 +433,7 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, G
             av[u]        = rr <= V ? X.reca[rr] : 0u;
             bv[u]        = rr <= V ? X.recb[rr] : 0u;
             cv[u]        = rr <= V ? X.recc[rr] : 0u;
+            ev[u]        = rr <= V ? X.rece[rr] : 0u;
         }
         const int xs  = uniform(X.bx[(r0 - 1) / kStageRows]);
         const int xe  = uniform(X.bx[(r0 - 1) / kStageRows + 1]);
@@ -394,9 +448,10 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, G
 #pragma unroll
         for (int u = 0; u < kStageRows / kWave; u++)
         {
-            srec[3 * (u * kWave + lane)]     = av[u];
-            srec[3 * (u * kWave + lane) + 1] = bv[u];
-            srec[3 * (u * kWave + lane) + 2] = cv[u];
+            srec[4 * (u * kWave + lane)]     = av[u];
+            srec[4 * (u * kWave + lane) + 1] = bv[u];
+            srec[4 * (u * kWave + lane) + 2] = cv[u];
+            srec[4 * (u * kWave + lane) + 3] = ev[u];
         }
 #pragma unroll
         for (int u = 0; u < kStageXl / kWave; u++)
@@ -406,10 +461,12 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, G
         uint32_t a   = uint32_t(uniform(int(srec[0])));
         uint32_t b   = uint32_t(uniform(int(srec[1])));
         uint32_t c2  = uint32_t(uniform(int(srec[2])));
+        uint32_t e2  = uint32_t(uniform(int(srec[3])));
         const int q1 = min(1, rend - r0);
-        uint32_t a1  = uint32_t(uniform(int(srec[3 * q1])));
-        uint32_t b1  = uint32_t(uniform(int(srec[3 * q1 + 1])));
-        uint32_t c1  = uint32_t(uniform(int(srec[3 * q1 + 2])));
+        uint32_t a1  = uint32_t(uniform(int(srec[4 * q1])));
+        uint32_t b1  = uint32_t(uniform(int(srec[4 * q1 + 1])));
+        uint32_t c1  = uint32_t(uniform(int(srec[4 * q1 + 2])));
+        uint32_t e1  = uint32_t(uniform(int(srec[4 * q1 + 3])));
         uint32_t rbw = band_read_bytes<ScoreT, CPL>(read, ra_bs(a), lane);
         bp.add(kBpStageCyc, BandProf::now() - st0);
         bp.add(kBpRows, uint64_t(rend - r0 + 1));
@@ -417,9 +474,10 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, G
         {
             // prefetch: record of row r+2, read bytes of row r+1
             const int q2       = min(r + 2, rend) - r0;
-            const uint32_t va2 = srec[3 * q2];
-            const uint32_t vb2 = srec[3 * q2 + 1];
-            const uint32_t vc2 = srec[3 * q2 + 2];
+            const uint32_t va2 = srec[4 * q2];
+            const uint32_t vb2 = srec[4 * q2 + 1];
+            const uint32_t vc2 = srec[4 * q2 + 2];
+            const uint32_t ve2 = srec[4 * q2 + 3];
             const uint32_t rbn = band_read_bytes<ScoreT, CPL>(read, ra_bs(a1), lane);
 
             const int bs = ra_bs(a);
@@ -435,20 +493,22 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, G
             int H[CPL];
             int code[CPL];
             auto closure = [&]() {
-                // E domain: E(t) = H(t) - (t+1)*gap, E(-1) = carry
-                int m[CPL];
-                int run = lane == 0 ? carry : kNeg;
+                // E domain: E(t) = H(t) - (t+1)*gap, E(-1) = carry; the
+                // prefix maximum runs on sign-flipped values
+                constexpr uint32_t kFlip = 0x80000000u;
+                uint32_t m[CPL];
+                uint32_t run = lane == 0 ? (uint32_t(carry) ^ kFlip) : 0u;
 #pragma unroll
                 for (int c = 0; c < CPL; c++)
                 {
-                    run  = max(run, v[c] - egap[c]);
+                    run  = max(run, uint32_t(v[c] - egap[c]) ^ kFlip);
                     m[c] = run;
                 }
-                const int incl = wave_incl_max_dpp(run);
-                const int excl = __builtin_amdgcn_update_dpp(kNeg, incl, 0x138, 0xf, 0xf, false);
+                const uint32_t incl = wave_incl_maxu_dpp(run);
+                const uint32_t excl = uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x138, 0xf, 0xf, true));
 #pragma unroll
                 for (int c = 0; c < CPL; c++)
-                    H[c] = trunc_score<ScoreT>(max(m[c], excl) + egap[c]);
+                    H[c] = trunc_score<ScoreT>(int(max(m[c], excl) ^ kFlip) + egap[c]);
             };
             auto horiz = [&](bool (&found)[CPL]) {
                 int left = __builtin_amdgcn_update_dpp(carry, H[CPL - 1], 0x138, 0xf, 0xf, false);
@@ -470,39 +530,52 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, G
 #pragma unroll
                 for (int k = 0; k < NP; k++)
                 {
-                    int p = 0, dk = bs;
-                    if (f != 0)
-                    {
-                        const uint32_t w    = k < 2 ? b : c2;
-                        const int dist      = int((k & 1) ? (w >> 16) : (w & 0xffffu));
-                        p                   = r - dist;
-                        const int pb        = dist < kBandRing ? __builtin_amdgcn_readlane(bsv, p & (kBandRing - 1))
-                                                               : B.start(p);
-                        dk                  = bs - pb;
-                    }
-                    d[k] = dk;
+                    // distance (rec_b / rec_c) and band shift / 4 (rec_e, byte k)
+                    const uint32_t w = k < 2 ? b : c2;
+                    const int p      = f == 0 ? 0 : r - int((k & 1) ? (w >> 16) : (w & 0xffffu));
+                    const int dk     = int((e2 >> (8 * k)) & 0xffu) << 2;
+                    d[k]             = dk;
                     band_fetch<ScoreT, CPL>(p, dk, r, Hp, prevF0, ring, spill, rowsz, gap, minv, lane, F[k]);
-                }
-                int c0max = INT_MIN;
-#pragma unroll
-                for (int c = 0; c < CPL; c++)
-                {
-                    const int t = CPL * lane + c;
-                    int vv      = kNeg;
-#pragma unroll
-                    for (int k = 0; k < NP; k++)
+                    // get_scores() reads the padding up to idx bw+7 (minv, except
+                    // row 0) and cut groups read minv; get_score() sees minv
+                    // beyond idx bw.  Rows >= 1 shifted by <= 4 need neither.
+                    if (p == 0 || dk > 4)
                     {
-                        const bool cut = (t & ~3) + d[k] >= bw + 4;
-                        const int val  = trunc_score<ScoreT>(max(F[k][c] + sig[c], F[k][c + 1] + gap));
-                        vv             = max(vv, cut ? minv : val);
+                        int val[CPL];
+#pragma unroll
+                        for (int c = 0; c < CPL; c++)
+                        {
+                            const int t    = CPL * lane + c;
+                            const bool cut = (t & ~3) + dk >= bw + 4;
+                            const int vl   = trunc_score<ScoreT>(max(F[k][c] + sig[c], F[k][c + 1] + gap));
+                            val[c]         = cut ? minv : vl;
+                        }
+#pragma unroll
+                        for (int i = 0; i <= CPL; i++)
+                            F[k][i] = (dk + CPL * lane + i > bw) ? minv : F[k][i];
+                        // fold the cut values in through a sentinel pair: the
+                        // value pass below recomputes from G, so keep val here
+#pragma unroll
+                        for (int c = 0; c < CPL; c++)
+                            v[c] = k == 0 ? val[c] : max(v[c], val[c]);
                     }
-                    v[c] = vv;
+                    else
+                    {
+#pragma unroll
+                        for (int c = 0; c < CPL; c++)
+                        {
+                            const int vl = trunc_score<ScoreT>(max(F[k][c] + sig[c], F[k][c + 1] + gap));
+                            v[c]         = k == 0 ? vl : max(v[c], vl);
+                        }
+                    }
                 }
                 // column 0 (:219-245): F(r, 0) is the column-0 value when the
                 // band starts at 0, else the minv initialize_band writes at idx 0
+                // (with band start 0 every shift is 0, so G(p, 0) = F(p, 0))
                 carry = minv;
                 if (bs == 0)
                 {
+                    int c0max = INT_MIN;
 #pragma unroll
                     for (int k = 0; k < NP; k++)
                         c0max = max(c0max, __builtin_amdgcn_readlane(F[k][0], 0));
@@ -514,15 +587,12 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, G
 #pragma unroll
                 for (int c = 0; c < CPL; c++)
                 {
-                    const int t = CPL * lane + c;
                     int dsl = -1, vsl = -1;
 #pragma unroll
                     for (int k = NP - 1; k >= 0; k--)
                     {
-                        const int gA = (d[k] + t > bw) ? minv : F[k][c];
-                        const int gB = (d[k] + t + 1 > bw) ? minv : F[k][c + 1];
-                        dsl          = (gA + sig[c] == H[c]) ? k : dsl;
-                        vsl          = (gB + gap == H[c]) ? k : vsl;
+                        dsl = (F[k][c] + sig[c] == H[c]) ? k : dsl;
+                        vsl = (F[k][c + 1] + gap == H[c]) ? k : vsl;
                     }
                     code[c]  = dsl >= 0 ? (dsl << 2) : (vsl >= 0 ? ((vsl << 2) | 1) : 3);
                     found[c] = dsl >= 0 || vsl >= 0;
@@ -697,12 +767,12 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, G
                 if (best < sval)
                     best = sval, end_row = r;
             }
-            const int vlim = L - bs - 1; // cells t <= vlim are columns <= L
-            bool tv        = false;
+            // (columns past L included: spilling more rows only costs stores)
+            int hmin = H[0];
 #pragma unroll
-            for (int c = 0; c < CPL; c++)
-                tv |= (CPL * lane + c <= vlim) && H[c] <= Tmax;
-            const bool tflag = __builtin_amdgcn_ballot_w64(tv) != 0;
+            for (int c = 1; c < CPL; c++)
+                hmin = min(hmin, H[c]);
+            const bool tflag = __builtin_amdgcn_ballot_w64(hmin <= Tmax) != 0;
             // ring row: position idx + CPL - 1
             GWAMD_LDS ScoreT* rrow = ring + (r & (kBandRing - 1)) * rowsz;
             if constexpr (CPL == 4 && sizeof(ScoreT) == 4)
@@ -753,10 +823,12 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, G
             a      = a1;
             b      = b1;
             c2     = c1;
+            e2     = e1;
             rbw    = rbn;
             a1     = uint32_t(uniform(int(va2)));
             b1     = uint32_t(uniform(int(vb2)));
             c1     = uint32_t(uniform(int(vc2)));
+            e1     = uint32_t(uniform(int(ve2)));
         }
         wave_sync(); // the staging buffers are rewritten by the next block
     }
@@ -768,9 +840,10 @@ __device__ int band_forward(const WinGraph<SizeT>& g, const BandAux& X, int V, G
 // known = false for an in-band value that was not stored: such a value is
 // not one of the T values, so no comparison with minv can match it.
 template <typename ScoreT, int CPL>
-__device__ int band_get_slow(int p, int col, const Band& B, const BandAux& X, const ScoreT* spill, int rowsz,
+__device__ int band_get_slow(int p, int col, const Band& B, BandAux X, const ScoreT* spill, int rowsz,
                              int gap, int minv, bool& known)
 {
+    X = as_global(X);
     known = true;
     if (p == 0)
         return (col >= 0 && col <= B.bw) ? col * gap : minv;
@@ -791,11 +864,16 @@ __device__ int band_get_slow(int p, int col, const Band& B, const BandAux& X, co
 // Traceback from (end_row, L) over the codes (:367-477).  Writes the reversed
 // alignment into ag / ar and returns its length, -1 at the loop bound.
 template <typename ScoreT, typename SizeT, int CPL>
-__device__ int band_traceback(const WinGraph<SizeT>& g, const BandAux& X, int V, const uint8_t* read, int L,
+__device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int V, const uint8_t* read, int L,
                               int end_row, const Band& B, const Scores sc, const ScoreT* spill, int rowsz,
                               GWAMD_LDS uint8_t* tile, SizeT* ag, SizeT* ar, int aln_cap,
                               int lane, BandProf& bp)
 {
+    X = as_global(X);
+    spill = glb(spill);
+    ag    = glb(ag);
+    ar    = glb(ar);
+    g = as_global(g);
     const uint64_t t_t0 = BandProf::now();
     const int bw    = B.bw;
     const int gap   = sc.gap;
@@ -822,7 +900,12 @@ __device__ int band_traceback(const WinGraph<SizeT>& g, const BandAux& X, int V,
     bool bad = false;
     while (!(i == 0 && j == 0) && loops < bound)
     {
-        loops++;
+        i      = uniform(i);
+        j      = uniform(j);
+        prev_i = uniform(prev_i);
+        prev_j = uniform(prev_j);
+        ti0    = uniform(ti0);
+        loops  = uniform(loops) + 1;
         bool found = false;
         int pi = 0, pj = 0;
         if (i == 0)
@@ -839,27 +922,29 @@ __device__ int band_traceback(const WinGraph<SizeT>& g, const BandAux& X, int V,
                 const uint64_t tt0 = BandProf::now();
                 ti0 = max(1, i - (kBandTile - 1));
                 wave_sync();
-                constexpr int kPer = kBandTile * 256 / 16 / kWave; // bw <= 256
-                const int per_row  = bw / 16;
+                // kBandTile rows of bw = 64*CPL code bytes: 4*CPL 16-B pieces
+                // per lane, all loads issued before the first store waits
+                constexpr int kPer    = 4 * CPL;
+                constexpr int kPerRow = 4 * CPL; // 16-B pieces per code row
+                v4i_t q[kPer];
 #pragma unroll
                 for (int u = 0; u < kPer; u++)
                 {
-                    const int t   = u * kWave + lane;
-                    const int tr  = t / per_row;
-                    const int tc  = (t % per_row) * 16;
-                    const int rr  = ti0 + tr;
-                    const bool ok = tr < kBandTile && rr <= V;
-                    v4i_t q       = {0, 0, 0, 0};
-                    if (ok)
-                        q = *reinterpret_cast<const v4i_t*>(X.codes + size_t(rr) * bw + tc);
-                    if (tr < kBandTile)
-                        *reinterpret_cast<GWAMD_LDS v4i_t*>(tile + tr * bw + tc) = q;
+                    const int t  = u * kWave + lane;
+                    const int rr = min(ti0 + t / kPerRow, V); // rows past V: never read
+                    q[u]         = *reinterpret_cast<const v4i_t*>(X.codes + size_t(rr) * bw + (t % kPerRow) * 16);
                 }
                 {
-                    const int rr = ti0 + lane; // kBandTile == kWave: one record per lane
-                    ta           = rr <= V ? X.reca[rr] : 0u;
-                    tb           = rr <= V ? X.recb[rr] : 0u;
-                    tcw          = rr <= V ? X.recc[rr] : 0u;
+                    const int rr = min(ti0 + lane, V); // kBandTile == kWave: one record per lane
+                    ta           = X.reca[rr];
+                    tb           = X.recb[rr];
+                    tcw          = X.recc[rr];
+                }
+#pragma unroll
+                for (int u = 0; u < kPer; u++)
+                {
+                    const int t = u * kWave + lane;
+                    *reinterpret_cast<GWAMD_LDS v4i_t*>(tile + (t / kPerRow) * bw + (t % kPerRow) * 16) = q[u];
                 }
                 wave_sync();
                 bp.add(kBpTileCyc, BandProf::now() - tt0);
@@ -1017,6 +1102,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
     X.reca           = reinterpret_cast<uint32_t*>(aux + d.aux_reca_off);
     X.recb           = reinterpret_cast<uint32_t*>(aux + d.aux_recb_off);
     X.recc           = reinterpret_cast<uint32_t*>(aux + d.aux_recc_off);
+    X.rece           = reinterpret_cast<uint32_t*>(aux + d.aux_rece_off);
     X.col0           = reinterpret_cast<int32_t*>(aux + d.aux_col0_off);
     X.flags          = aux + d.aux_flag_off;
     X.xl             = reinterpret_cast<int32_t*>(aux + d.aux_xl_off);
@@ -1030,6 +1116,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
 
     PhaseTimer ph;
     BandProf bp;
+    uint64_t tsprof[4] = {0, 0, 0, 0}; // topsort sections (GWAMD_TOPSORT_PROFILE builds)
     const WindowDesc wd = b.windows[w];
     const int nseq      = wd.num_seqs;
     int status          = kSuccess;
@@ -1122,7 +1209,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
             if (rc == kSuccess)
             {
                 if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, (GWAMD_LDS int*)(shb),
-                                        lane))
+                                        lane, tsprof))
                 {
                     if (lane == 0)
                         topsort_kahn<SizeT>(g, nc, cscore);
@@ -1148,11 +1235,23 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
         if (b.phase)
         {
             ph.store(b.phase + size_t(w) * kPhases);
+#ifdef GWAMD_TOPSORT_PROFILE
+            b.phase[size_t(w) * kPhases + kPhBackbone] = int64_t(tsprof[0] / 1000);
+            b.phase[size_t(w) * kPhases + kPhAdd]      = int64_t(tsprof[1] / 1000);
+            b.phase[size_t(w) * kPhases + kPhOutput]   = int64_t(tsprof[2] / 1000);
+            b.phase[size_t(w) * kPhases + kPhRowProg]  = int64_t(tsprof[3]);
+#endif
 #ifdef GWAMD_BAND_PROFILE
             // counters over the phase slots (read raw: value = phase_ms * 1e5)
-            const int slot[8] = {kPhBackbone, kPhAdd, kPhTopsort, kPhOutput, kPhRowProg, kPhTotal, -1, -1};
-            for (int i = 0; i < 6; i++)
-                b.phase[size_t(w) * kPhases + slot[i]] = int64_t(bp.v[i == 5 ? kBpTbCyc : (i == 4 ? kBpSteps : i)]);
+            // backbone: rows, add: traceback tile cycles, topsort: flush cycles,
+            // output: forward cycles, rowprog: traceback steps, total: traceback cycles
+            int64_t* ph8 = b.phase + size_t(w) * kPhases;
+            ph8[kPhBackbone] = int64_t(bp.v[kBpRows]);
+            ph8[kPhAdd]      = int64_t(bp.v[kBpTileCyc]);
+            ph8[kPhTopsort]  = int64_t(bp.v[kBpFlushCyc]);
+            ph8[kPhOutput]   = int64_t(bp.v[kBpFwdCyc]);
+            ph8[kPhRowProg]  = int64_t(bp.v[kBpSteps]);
+            ph8[kPhTotal]    = int64_t(bp.v[kBpTbCyc]);
 #endif
         }
         b.final_nodes[w] = node_count;

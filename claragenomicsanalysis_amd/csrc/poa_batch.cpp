@@ -546,7 +546,7 @@ private:
         const int64_t ms  = dims_.max_seq_len, mn = dims_.max_nodes;
         const int64_t read_b  = a16(ms + bw + 48);
         const int64_t sh_b    = 64;
-        const int64_t ring_b  = a16(int64_t(16) * rowsz * sbytes) + 3 * 256 * 4 + 1024 * 4; // + record staging
+        const int64_t ring_b  = a16(int64_t(16) * rowsz * sbytes) + 4 * 256 * 4 + 1024 * 4; // + record staging
         const int64_t tile_b  = a16(int64_t(64) * bw + 512);
         const int64_t flags_b = a16(mn + 2);
         const int64_t add_b   = 5 * a16(ms + 16) + 2 * (mn + ms + 16) + 16;
@@ -592,6 +592,8 @@ private:
         dims_.aux_bx_off = int32_t(o);
         o += a16((rows / 256 + 2) * 4);
         dims_.aux_recc_off = int32_t(o);
+        o += a16(rows * 4);
+        dims_.aux_rece_off = int32_t(o);
         o += a16(rows * 4);
         dims_.aux_stride = o;
     }

@@ -84,6 +84,7 @@ struct Dims
     int32_t aux_xl_cap;
     int32_t aux_bx_off;     //   | per-256-row-block predecessor-list offsets (i32)
     int32_t aux_recc_off;   //   | row records c (u32)
+    int32_t aux_rece_off;   //   | row records e (u32)
 };
 
 // Small shared region of the LDS kernel (kShBytes(waves) at Dims::lds_sh_off):

@@ -33,6 +33,34 @@ struct WinGraph
     int32_t max_nodes;
 };
 
+// Pointers reached through structs (WinGraph, Buffers fields copied into
+// locals) lose their address space when a struct is passed to a call that is
+// not inlined; flat accesses then count in both vmcnt and lgkmcnt, so every
+// LDS wait also waits for outstanding global stores.  as_global() re-asserts
+// the global space (an addrspacecast the compiler propagates).
+template <typename T>
+__device__ __forceinline__ T* glb(T* p)
+{
+    return (T*)((__attribute__((address_space(1))) T*)(p));
+}
+
+template <typename SizeT>
+__device__ __forceinline__ WinGraph<SizeT> as_global(WinGraph<SizeT> g)
+{
+    g.base    = glb(g.base);
+    g.in_cnt  = glb(g.in_cnt);
+    g.out_cnt = glb(g.out_cnt);
+    g.aln_cnt = glb(g.aln_cnt);
+    g.cov     = glb(g.cov);
+    g.in_w    = glb(g.in_w);
+    g.in_e    = glb(g.in_e);
+    g.out_e   = glb(g.out_e);
+    g.aln     = glb(g.aln);
+    g.sorted  = glb(g.sorted);
+    g.pos     = glb(g.pos);
+    return g;
+}
+
 __device__ __forceinline__ uint64_t now_ticks()
 {
     return __builtin_amdgcn_s_memrealtime();
@@ -77,17 +105,19 @@ __device__ __forceinline__ int wave_max(int v)
 
 // Row of the score matrix for predecessor slot p of node (cudapoa_nw.cuh:103).
 template <typename SizeT>
-__device__ __forceinline__ int pred_row(const WinGraph<SizeT>& g, int node, int p)
+__device__ __forceinline__ int pred_row(WinGraph<SizeT> g, int node, int p)
 {
+    g = as_global(g);
     return int(g.pos[int(g.in_e[node * kMaxEdges + p])]) + 1;
 }
 
 // ---------------------------------------------------------------------------
 // Backbone from read 0 (cudapoa_kernels.cuh:171-209), lane-parallel.
 template <typename SizeT, bool MSA>
-__device__ void build_backbone(WinGraph<SizeT>& g, const uint8_t* seq, const int8_t* w, int len, int lane,
+__device__ void build_backbone(WinGraph<SizeT> g, const uint8_t* seq, const int8_t* w, int len, int lane,
                                uint16_t* ecov, uint16_t* ecov_cnt, SizeT* seq_begin, int max_seqs)
 {
+    g = as_global(g);
     if (lane == 0)
     {
         g.base[0]    = seq[0];
@@ -173,9 +203,10 @@ struct Pack8<int32_t>
 };
 
 template <typename ScoreT, typename SizeT>
-__device__ void nw_forward_full(const WinGraph<SizeT>& g, int V, const uint8_t* read, int L, ScoreT* S, int stride,
+__device__ void nw_forward_full(WinGraph<SizeT> g, int V, const uint8_t* read, int L, ScoreT* S, int stride,
                                 const Scores sc, int lane)
 {
+    g = as_global(g);
     const int gap = sc.gap;
     // row 0: H[0][j] = j * gap (cudapoa_nw.cuh:176-179)
     for (int j = lane; j <= L; j += kWave)
@@ -266,9 +297,10 @@ __device__ void nw_forward_full(const WinGraph<SizeT>& g, int V, const uint8_t* 
 // Traceback (cudapoa_nw.cuh:329-462), lane 0 only.  Writes the reversed
 // alignment and returns its length, or -1 at the loop bound.
 template <typename ScoreT, typename SizeT>
-__device__ int traceback_full(const WinGraph<SizeT>& g, int V, const uint8_t* read, int L, const ScoreT* S,
+__device__ int traceback_full(WinGraph<SizeT> g, int V, const uint8_t* read, int L, const ScoreT* S,
                               int stride, const Scores sc, SizeT* ag, SizeT* ar, int aln_cap)
 {
+    g = as_global(g);
     auto H = [&](int i, int j) { return int(S[size_t(i) * stride + kColShift + j]); };
     int i = 0, j = L;
     int best = INT_MIN;
@@ -392,9 +424,10 @@ __device__ __forceinline__ ScoreT band_min_value(const Scores sc)
 }
 
 template <typename ScoreT, typename SizeT>
-__device__ void nw_forward_banded(const WinGraph<SizeT>& g, int V, const uint8_t* read, int L, ScoreT* S,
+__device__ void nw_forward_banded(WinGraph<SizeT> g, int V, const uint8_t* read, int L, ScoreT* S,
                                   const Band& B, const Scores sc, int lane)
 {
+    g = as_global(g);
     const ScoreT minv = band_min_value<ScoreT>(sc);
     const int gap     = sc.gap;
     // horizontal boundary (:212-216)
@@ -520,9 +553,10 @@ __device__ void nw_forward_banded(const WinGraph<SizeT>& g, int V, const uint8_t
 }
 
 template <typename ScoreT, typename SizeT>
-__device__ int traceback_banded(const WinGraph<SizeT>& g, int V, const uint8_t* read, int L, const ScoreT* S,
+__device__ int traceback_banded(WinGraph<SizeT> g, int V, const uint8_t* read, int L, const ScoreT* S,
                                 const Band& B, const Scores sc, SizeT* ag, SizeT* ar, int aln_cap)
 {
+    g = as_global(g);
     const ScoreT minv = band_min_value<ScoreT>(sc);
     auto H            = [&](int i, int j) { return int(band_get(S, B, i, j, minv)); };
     int i = 0, j = L;
@@ -593,10 +627,11 @@ __device__ int traceback_banded(const WinGraph<SizeT>& g, int V, const uint8_t* 
 // ---------------------------------------------------------------------------
 // addAlignmentToGraph (cudapoa_add_alignment.cuh:59-279), lane 0.
 template <typename SizeT, bool MSA>
-__device__ uint8_t add_alignment(WinGraph<SizeT>& g, int& node_count, const SizeT* ag, const SizeT* ar, int alen,
+__device__ uint8_t add_alignment(WinGraph<SizeT> g, int& node_count, const SizeT* ag, const SizeT* ar, int alen,
                                  const uint8_t* read, const int8_t* w, int s, uint16_t* ecov, uint16_t* ecov_cnt,
                                  SizeT* seq_begin, int max_seqs)
 {
+    g = as_global(g);
     int head = -1, curr = -1;
     uint16_t prev_w = 0;
     int nc          = node_count;
@@ -735,8 +770,9 @@ __device__ uint8_t add_alignment(WinGraph<SizeT>& g, int& node_count, const Size
 
 // Kahn topological sort (cudapoa_topsort.cuh:38-88), lane 0.
 template <typename SizeT>
-__device__ void topsort_kahn(WinGraph<SizeT>& g, int n, int32_t* local)
+__device__ void topsort_kahn(WinGraph<SizeT> g, int n, int32_t* local)
 {
+    g = as_global(g);
     int k = 0;
     for (int v = 0; v < n; v++)
     {
@@ -766,8 +802,9 @@ __device__ void topsort_kahn(WinGraph<SizeT>& g, int n, int32_t* local)
 // racon/SPOA DFS sort (cudapoa_topsort.cuh:94-189), lane 0.  marks packs
 // node_marks (bits 0-1) and check_aligned_nodes (bit 2).
 template <typename SizeT>
-__device__ bool topsort_racon(WinGraph<SizeT>& g, int n, int32_t* marks, SizeT* stack, int stack_cap)
+__device__ bool topsort_racon(WinGraph<SizeT> g, int n, int32_t* marks, SizeT* stack, int stack_cap)
 {
+    g = as_global(g);
     for (int i = 0; i < g.max_nodes; i++)
         marks[i] = 4; // mark 0, check = true
     int top = -1, k = 0;
@@ -838,8 +875,9 @@ __device__ bool topsort_racon(WinGraph<SizeT>& g, int n, int32_t* marks, SizeT* 
 // Heaviest bundle (cudapoa_generate_consensus.cuh:28-276), lane 0.  Writes the
 // consensus backwards (as the reference kernel) and returns its length or -status.
 template <typename SizeT>
-__device__ int branch_completion(const WinGraph<SizeT>& g, int n, int max_pos, int32_t* score, SizeT* pred)
+__device__ int branch_completion(WinGraph<SizeT> g, int n, int max_pos, int32_t* score, SizeT* pred)
 {
+    g = as_global(g);
     int node = int(g.sorted[max_pos]);
     for (int oe = 0; oe < int(g.out_cnt[node]); oe++)
     {
@@ -879,9 +917,10 @@ __device__ int branch_completion(const WinGraph<SizeT>& g, int n, int max_pos, i
 }
 
 template <typename SizeT>
-__device__ int consensus_raw(const WinGraph<SizeT>& g, int n, int32_t* score, SizeT* pred, uint8_t* cons,
+__device__ int consensus_raw(WinGraph<SizeT> g, int n, int32_t* score, SizeT* pred, uint8_t* cons,
                              uint16_t* cov, int max_cons)
 {
+    g = as_global(g);
     for (int i = 0; i < n; i++)
     {
         pred[i]  = SizeT(-1);

@@ -191,8 +191,9 @@ struct RowProg
 
 // k-th predecessor row of row r (0 = the virtual row 0)
 template <typename SizeT>
-__device__ __forceinline__ int prog_pred(const RowProg& P, const WinGraph<SizeT>& g, int r, uint32_t rec, int k)
+__device__ __forceinline__ int prog_pred(const RowProg& P, WinGraph<SizeT> g, int r, uint32_t rec, int k)
 {
+    g = as_global(g);
     const int np = (rec >> 8) & 63;
     if (np == 0)
         return 0; // source node: the virtual row 0
@@ -208,8 +209,9 @@ __device__ __forceinline__ int prog_pred(const RowProg& P, const WinGraph<SizeT>
 }
 
 template <typename SizeT>
-__device__ __forceinline__ int prog_np(const WinGraph<SizeT>& g, int r, uint32_t rec)
+__device__ __forceinline__ int prog_np(WinGraph<SizeT> g, int r, uint32_t rec)
 {
+    g = as_global(g);
     const int np = (rec >> 8) & 63;
     return np == int(kRecEscape) ? int(g.in_cnt[int(g.sorted[r - 1])]) : np;
 }
@@ -223,9 +225,10 @@ __device__ __forceinline__ int prog_np(const WinGraph<SizeT>& g, int r, uint32_t
 // (row s, predecessor row p: s - p >= ring_rows) into byte flags in `flags`
 // (V + 2 bytes of free LDS), so no out-edge lists are read.
 template <typename SizeT>
-__device__ void build_row_program(const WinGraph<SizeT>& g, int V, uint32_t* rec, uint16_t* xl, int xl_cap,
+__device__ void build_row_program(WinGraph<SizeT> g, int V, uint32_t* rec, uint16_t* xl, int xl_cap,
                                   int ring_rows, int lane, GWAMD_LDS uint8_t* flags)
 {
+    g = as_global(g);
     constexpr int kRP = 4;
     for (int r = lane; r <= V + 1; r += kWave)
         flags[r] = 0;
@@ -431,9 +434,10 @@ struct FwdProf
 // predecessor (n = 1, row 0), which gives the same column-0 value (gap) and
 // the same scores as the reference's source-node case.
 template <typename SizeT>
-__device__ __forceinline__ int row_preds(const RowProg& P, const WinGraph<SizeT>& g, int rr, uint32_t rec, int lane,
+__device__ __forceinline__ int row_preds(const RowProg& P, WinGraph<SizeT> g, int rr, uint32_t rec, int lane,
                                          int& n)
 {
+    g = as_global(g);
     n      = int((rec >> 8) & 63);
     int pv = 0;
     if (n == int(kRecEscape))
@@ -480,11 +484,12 @@ __device__ __forceinline__ void load_row_pk(const int16_t* p, uint32_t (&P)[NR],
 }
 
 template <int CPL, int NW, typename SizeT>
-__device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int V, const uint8_t* read, int L,
+__device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, const uint8_t* read, int L,
                                  int16_t* ring, int ring_stride, int16_t* spill, int stride, uint8_t* codes,
                                  int code_stride, const Scores sc, GWAMD_LDS uint8_t* shb, int16_t* carry_hbm,
                                  int tid, FwdProf& fp)
 {
+    g = as_global(g);
     constexpr int NR    = CPL / 2;
     constexpr int kSpan = kWave * CPL;
     const int lane      = tid & (kWave - 1);
@@ -841,10 +846,11 @@ __device__ int nw_forward_lds_pk(const WinGraph<SizeT>& g, const RowProg& P, int
 // cudapoa_nw.cuh:361-452) are collected one per lane and stored 64 at a time;
 // rows become node ids at the store.
 template <typename SizeT>
-__device__ int traceback_codes(const WinGraph<SizeT>& g, const RowProg& P, int V, int L, int end_row,
+__device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L, int end_row,
                                const uint8_t* codes, int code_stride, uint8_t* tile, SizeT* ag, SizeT* ar,
                                int aln_cap, int lane)
 {
+    g = as_global(g);
 
     V       = uniform(V);
     L       = uniform(L);

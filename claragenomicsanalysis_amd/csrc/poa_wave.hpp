@@ -48,10 +48,11 @@ struct PhaseTimer
 // Consensus and/or MSA of one finished window (cudapoa_generate_consensus.cuh:
 // 279-347, cudapoa_generate_msa.cuh:121-224).
 template <typename SizeT, bool MSA>
-__device__ void finish_window(const Buffers& b, const Dims& d, int w, int lane, WinGraph<SizeT>& g, int status,
+__device__ __forceinline__ void finish_window(const Buffers& b, const Dims& d, int w, int lane, WinGraph<SizeT> g, int status,
                               int nseq, int node_count, int32_t* cscore, SizeT* cpred, uint16_t* ecov,
                               uint16_t* ecovc, SizeT* seq_begin, int& sh_len, int& sh_status)
 {
+    g = as_global(g);
     uint8_t* cons_out = b.cons + size_t(w) * d.max_consensus;
     const int graph_status = status;
     if (!MSA || d.want_consensus)
@@ -203,18 +204,19 @@ __device__ __forceinline__ int wave_incl_max_dpp(int v)
     return v;
 }
 
-// Exclusive wave sum of small non-negative ints (row-program offsets).
+// Exclusive wave sum of small non-negative ints (row-program offsets): DPP
+// inclusive scan (row_shr 1/2/4/8, row_bcast 15/31); the total is uniform.
 __device__ __forceinline__ int wave_excl_sum(int v, int lane, int& total)
 {
     int x = v;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1)
-    {
-        int t = __shfl_up(x, d, kWave);
-        if (lane >= d)
-            x += t;
-    }
-    total = __shfl(x, kWave - 1, kWave);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+    (void)lane;
+    total = __builtin_amdgcn_readlane(x, kWave - 1);
     return x - v;
 }
 
@@ -239,11 +241,12 @@ struct AddScratch
 };
 
 template <typename SizeT, bool MSA>
-__device__ int add_alignment_parallel(WinGraph<SizeT>& g, int& node_count, const SizeT* ag, const SizeT* ar,
+__device__ __forceinline__ int add_alignment_parallel(WinGraph<SizeT> g, int& node_count, const SizeT* ag, const SizeT* ar,
                                       int alen, int L, const uint8_t* read, const int8_t* w, int s, uint16_t* ecov,
                                       uint16_t* ecov_cnt, SizeT* seq_begin, int max_seqs, const AddScratch& X,
                                       int lane)
 {
+    g = as_global(g);
     const int nc0 = node_count;
     int err       = INT_MAX; // first error in read order: (pos << 8) | status
     if (lane == 0)
@@ -458,134 +461,231 @@ __device__ int add_alignment_parallel(WinGraph<SizeT>& g, int& node_count, const
 
 // ---------------------------------------------------------------------------
 // Kahn topological sort (cudapoa_topsort.cuh:38-88) over an LDS copy of the
-// out-edge lists (CSR): the adjacency is staged wave-parallel, the sources
-// are compacted in id order in parallel, and lane 0 runs the FIFO on LDS.
-// Returns false (nothing written) when the scratch is too small.
+// out-edge lists.  One 32-bit word per node holds the remaining in-degree
+// (bits 24-31), the out-degree (16-21) and either the single successor or the
+// offset of the successor list (0-15).  The FIFO is run by the whole wave on
+// uniform values (scalar control flow).  Queue entries keep the node's word
+// next to its id, and the entry after the current one is requested while the
+// current node is processed, so a node costs one dependent LDS round trip per
+// released successor.  The queue is a ring of kTsQueue entries (the frontier
+// of a POA graph is a handful of nodes); node positions are collected one per
+// lane and stored 64 at a time.  Returns false (nothing written) when the
+// scratch is too small, the frontier outgrows the ring or ids exceed 16 bits.
+constexpr int kTsQueue = 1024;
+
 template <typename SizeT>
-__device__ bool topsort_lds(WinGraph<SizeT>& g, int n, GWAMD_LDS uint8_t* scratch, int scratch_bytes,
-                            GWAMD_LDS int* sh, int lane)
+__device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS uint8_t* scratch, int scratch_bytes,
+                            GWAMD_LDS int* sh, int lane, uint64_t* prof = nullptr)
 {
-    // info[v] = out-degree << 16 | first successor: the FIFO step reads one
-    // word per node; off / edges only for nodes with two or more successors
+    g = as_global(g);
+#ifdef GWAMD_TOPSORT_PROFILE
+    const uint64_t tp0 = __builtin_amdgcn_s_memtime();
+#endif
+    // (a non-inlined call passes these in VGPRs: keep the control flow scalar)
+    n             = uniform(n);
+    scratch_bytes = uniform(scratch_bytes);
     GWAMD_LDS uint32_t* info  = (GWAMD_LDS uint32_t*)(scratch);
-    GWAMD_LDS uint16_t* off   = (GWAMD_LDS uint16_t*)(scratch + n * 4);
-    GWAMD_LDS uint16_t* queue = (GWAMD_LDS uint16_t*)(scratch + n * 4 + (n + 1) * 2);
-    GWAMD_LDS uint8_t* cnt    = scratch + n * 4 + (n + 1) * 2 + n * 2;
-    const int head_bytes      = (n * 4 + (n + 1) * 2 + n * 2 + n + 15) & ~15;
+    GWAMD_LDS uint32_t* qinfo = (GWAMD_LDS uint32_t*)(scratch + ((n * 4 + 15) & ~15));
+    GWAMD_LDS uint16_t* qid   = (GWAMD_LDS uint16_t*)(qinfo + kTsQueue);
+    const int head_bytes      = ((n * 4 + 15) & ~15) + kTsQueue * 6 + 512; // + 128 dummy words
     GWAMD_LDS uint16_t* edges = (GWAMD_LDS uint16_t*)(scratch + head_bytes);
-    if (head_bytes > scratch_bytes)
+    if (head_bytes > scratch_bytes || n > 65535 || n <= 0)
         return false;
     const int edge_cap = min((scratch_bytes - head_bytes) / 2, 65535);
-    // CSR staging from the HBM graph: counts and the first two out-edges of
-    // kTS nodes per lane are loaded before any of them is used
+    // staging from the HBM graph (the first kE successor slots of every node
+    // are loaded with the counts; only nodes with more read the rest)
     constexpr int kTS = 4;
+    constexpr int kE  = 8;
     int ebase         = 0;
     for (int v0 = 0; v0 < n; v0 += kTS * kWave)
     {
-        int oc[kTS], ic[kTS], e0[kTS], e1[kTS];
+        int oc[kTS], ic[kTS], ev[kTS][kE];
 #pragma unroll
         for (int u = 0; u < kTS; u++)
         {
             const int v = min(v0 + u * kWave + lane, n - 1);
             oc[u]       = int(g.out_cnt[v]);
             ic[u]       = int(g.in_cnt[v]);
-            e0[u]       = int(g.out_e[v * kMaxEdges]);
-            e1[u]       = int(g.out_e[v * kMaxEdges + 1]);
+#pragma unroll
+            for (int e = 0; e < kE; e++)
+                ev[u][e] = int(g.out_e[v * kMaxEdges + e]);
         }
 #pragma unroll
         for (int u = 0; u < kTS; u++)
         {
-            const int v     = v0 + u * kWave + lane;
-            const bool real = v < n;
-            const int c     = real ? oc[u] : 0;
-            int total       = 0;
-            const int ex    = wave_excl_sum(c, lane, total);
+            const int v      = v0 + u * kWave + lane;
+            const bool real  = v < n;
+            const int c      = real ? oc[u] : 0;
+            const int listed = c >= 2 ? c : 0;
+            int total        = 0;
+            const int ex     = wave_excl_sum(listed, lane, total);
             if (ebase + total > edge_cap)
                 return false;
             if (real)
             {
                 const int o = ebase + ex;
-                off[v]      = uint16_t(o);
-                cnt[v]      = uint8_t(ic[u]);
-                info[v]     = (uint32_t(c) << 16) | uint32_t(uint16_t(c >= 1 ? e0[u] : 0));
-                if (c >= 1)
-                    edges[o] = uint16_t(e0[u]);
+                info[v]     = (uint32_t(ic[u]) << 24) | (uint32_t(c) << 16) |
+                          uint32_t(uint16_t(c == 1 ? ev[u][0] : (c >= 2 ? o : 0)));
                 if (c >= 2)
-                    edges[o + 1] = uint16_t(e1[u]);
-                for (int e = 2; e < c; e++)
-                    edges[o + e] = uint16_t(int(g.out_e[v * kMaxEdges + e]));
+                {
+#pragma unroll
+                    for (int e = 0; e < kE; e++)
+                        if (e < c)
+                            edges[o + e] = uint16_t(ev[u][e]);
+                    for (int e = kE; e < c; e++)
+                        edges[o + e] = uint16_t(int(g.out_e[v * kMaxEdges + e]));
+                }
             }
             ebase += total;
         }
     }
-    if (lane == 0)
-        off[n] = uint16_t(ebase);
     wave_sync();
     // sources in id order
     int k = 0;
     for (int v0 = 0; v0 < n; v0 += kWave)
     {
-        const int v    = v0 + lane;
-        const bool src = v < n && cnt[v] == 0;
-        int total      = 0;
-        const int ex   = wave_excl_sum(src ? 1 : 0, lane, total);
+        const int v      = v0 + lane;
+        const uint32_t w = v < n ? info[v] : 0xff000000u;
+        const bool src   = (w >> 24) == 0;
+        int total        = 0;
+        const int ex     = wave_excl_sum(src ? 1 : 0, lane, total);
+        if (k + total > kTsQueue)
+            return false;
         if (src)
-            queue[k + ex] = uint16_t(v);
+        {
+            qid[k + ex]   = uint16_t(v);
+            qinfo[k + ex] = w;
+        }
         k += total;
     }
     wave_sync();
-    if (lane == 0)
+#ifdef GWAMD_TOPSORT_PROFILE
+    const uint64_t tp1 = __builtin_amdgcn_s_memtime();
+#endif
+    // FIFO (cudapoa_topsort.cuh:58-85) on uniform values; every lane reads the
+    // same word (LDS broadcast) and writes the same value to the same address
+    constexpr int kQm = kTsQueue - 1;
+    // uniform stores: lane 0 writes the word, the other lanes write to their
+    // own dummy word (no same-address write conflict, no exec-mask branch)
+    GWAMD_LDS uint32_t* dummy = (GWAMD_LDS uint32_t*)(qid + kTsQueue) + 64;
+    auto st32 = [&](GWAMD_LDS uint32_t* p, uint32_t v) { *(lane == 0 ? p : dummy + lane) = v; };
+    auto st16 = [&](GWAMD_LDS uint16_t* p, uint16_t v) {
+        *(lane == 0 ? p : (GWAMD_LDS uint16_t*)(dummy + lane)) = v;
+    };
+    int tail          = k;
+    int q             = 0;
+    bool overflow     = false;
+    int ids           = 0; // lane (q & 63): id of entry q until stored
+    uint32_t vinfo    = tail > 0 ? uint32_t(uniform(int(qinfo[0]))) : 0u;
+    int vid           = tail > 0 ? uniform(int(qid[0])) : 0;
+    auto push         = [&](int o, uint32_t oi) {
+        st16(&qid[tail & kQm], uint16_t(o));
+        st32(&qinfo[tail & kQm], oi);
+        tail++;
+    };
+    tail = uniform(tail);
+    while (q < tail)
     {
-        // FIFO (cudapoa_topsort.cuh:58-85); the next node comes from a register
-        // when it was queued by this step or prefetched with this step's info
-        int tail  = k;
-        int vnext = tail > 0 ? int(queue[0]) : 0;
-        for (int q = 0; q < tail;)
+        q     = uniform(q);
+        tail  = uniform(tail);
+        vinfo = uint32_t(uniform(int(vinfo)));
+        vid   = uniform(vid);
+        // entry q+1 is requested now if it is already queued
+        const int qn       = (q + 1) & kQm;
+        const uint32_t nxi = qinfo[qn];
+        const int nxid     = int(qid[qn]);
+        const int qtail    = tail; // entries pushed by this step start here
+        uint32_t first_info = 0;
+        int first_id        = 0;
+        const int deg       = int((vinfo >> 16) & 63u);
+        if (deg == 1)
         {
-            const int v        = vnext;
-            const uint32_t inf = info[v];
-            const int qn       = q + 1 < tail ? int(queue[q + 1]) : -1;
-            const int deg      = int(inf >> 16);
-            int first_pushed   = -1;
-            if (deg >= 1)
+            const int o       = int(vinfo & 0xffffu);
+            const uint32_t oi = uint32_t(uniform(int(info[o]))) - (1u << 24);
+            st32(&info[o], oi);
+            if ((oi >> 24) == 0u)
             {
-                const int o = int(inf & 0xffffu);
-                const int c = int(cnt[o]) - 1;
-                cnt[o]      = uint8_t(c);
-                if (c == 0)
+                first_info = oi, first_id = o;
+                push(o, oi);
+            }
+        }
+        else if (deg >= 2)
+        {
+            const int off = int(vinfo & 0xffffu);
+            for (int e0 = 0; e0 < deg; e0 += 4)
+            {
+                // up to four successors: their ids, then their words, in parallel
+                int o[4];
+                uint32_t w[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    o[u] = e0 + u < deg ? int(edges[off + e0 + u]) : 0;
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    o[u] = uniform(o[u]);
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    w[u] = info[o[u]];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
                 {
-                    queue[tail++] = uint16_t(o);
-                    first_pushed  = o;
-                }
-                for (int e = int(off[v]) + 1; e < int(off[v]) + deg; e++)
-                {
-                    const int o2 = int(edges[e]);
-                    const int c2 = int(cnt[o2]) - 1;
-                    cnt[o2]      = uint8_t(c2);
-                    if (c2 == 0)
+                    if (e0 + u < deg)
                     {
-                        queue[tail++] = uint16_t(o2);
-                        first_pushed  = first_pushed < 0 ? o2 : first_pushed;
+                        const uint32_t oi = uint32_t(uniform(int(w[u]))) - (1u << 24);
+                        st32(&info[o[u]], oi);
+                        if ((oi >> 24) == 0u)
+                        {
+                            if (tail == qtail)
+                                first_info = oi, first_id = o[u];
+                            push(o[u], oi);
+                        }
                     }
                 }
             }
-            q++;
-            vnext = qn >= 0 ? qn : first_pushed;
         }
-        sh[0] = tail;
+        overflow = overflow || uniform(tail - q) > kTsQueue;
+        ids = lane == (q & (kWave - 1)) ? vid : ids;
+        if ((q & (kWave - 1)) == kWave - 1)
+        {
+            const int qq = (q & ~(kWave - 1)) + lane;
+            g.sorted[qq] = SizeT(ids);
+            g.pos[ids]   = SizeT(qq);
+        }
+        q++;
+        if (q < tail)
+        {
+            if (q == qtail)
+                vinfo = first_info, vid = first_id;
+            else
+                vinfo = uint32_t(uniform(int(nxi))), vid = uniform(nxid);
+        }
+        if (overflow)
+            break;
     }
-    wave_sync();
-    const int m = sh[0];
-    for (int q = lane; q < m; q += kWave)
+    if (overflow)
+        return false; // partial HBM writes are rewritten by the fallback sort
+    if ((q & (kWave - 1)) != 0)
     {
-        const int v = int(queue[q]);
-        g.sorted[q] = SizeT(v);
-        g.pos[v]    = SizeT(q);
+        const int qq = (q & ~(kWave - 1)) + lane;
+        if (lane < (q & (kWave - 1)))
+        {
+            g.sorted[qq] = SizeT(ids);
+            g.pos[ids]   = SizeT(qq);
+        }
     }
     wave_sync();
+#ifdef GWAMD_TOPSORT_PROFILE
+    if (prof)
+    {
+        const uint64_t tp3 = __builtin_amdgcn_s_memtime();
+        prof[0] += tp1 - tp0;
+        prof[1] += tp3 - tp1;
+        prof[3] += uint64_t(n);
+    }
+#endif
+    (void)sh;
     return true;
 }
-
 
 } // namespace poa
 } // namespace gwamd
