@@ -464,30 +464,22 @@ __device__ __forceinline__ int add_alignment_parallel(WinGraph<SizeT> g, int& no
 // out-edge lists.  One 32-bit word per node holds the remaining in-degree
 // (bits 24-31), the out-degree (16-21) and either the single successor or the
 // offset of the successor list (0-15).  The FIFO is run by the whole wave on
-// uniform values (scalar control flow).  Queue entries keep the node's word
-// next to its id, and the entry after the current one is requested while the
-// current node is processed, so a node costs one dependent LDS round trip per
-// released successor.  The queue is a ring of kTsQueue entries (the frontier
-// of a POA graph is a handful of nodes); node positions are collected one per
-// lane and stored 64 at a time.  Returns false (nothing written) when the
-// scratch is too small, the frontier outgrows the ring or ids exceed 16 bits.
-constexpr int kTsQueue = 1024;
-
+// uniform values (scalar control flow): every lane reads the same word (LDS
+// broadcast) and writes the same value to the same address.  The next node
+// comes from a register when it was released by the current step.  Returns
+// false (nothing written) when the scratch is too small; node ids and list
+// offsets must fit 16 bits.
 template <typename SizeT>
 __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS uint8_t* scratch, int scratch_bytes,
-                            GWAMD_LDS int* sh, int lane, uint64_t* prof = nullptr)
+                                            GWAMD_LDS int* sh, int lane, uint64_t* prof = nullptr)
 {
     g = as_global(g);
 #ifdef GWAMD_TOPSORT_PROFILE
     const uint64_t tp0 = __builtin_amdgcn_s_memtime();
 #endif
-    // (a non-inlined call passes these in VGPRs: keep the control flow scalar)
-    n             = uniform(n);
-    scratch_bytes = uniform(scratch_bytes);
     GWAMD_LDS uint32_t* info  = (GWAMD_LDS uint32_t*)(scratch);
-    GWAMD_LDS uint32_t* qinfo = (GWAMD_LDS uint32_t*)(scratch + ((n * 4 + 15) & ~15));
-    GWAMD_LDS uint16_t* qid   = (GWAMD_LDS uint16_t*)(qinfo + kTsQueue);
-    const int head_bytes      = ((n * 4 + 15) & ~15) + kTsQueue * 6 + 512; // + 128 dummy words
+    GWAMD_LDS uint16_t* queue = (GWAMD_LDS uint16_t*)(scratch + n * 4);
+    const int head_bytes      = (n * 6 + 15) & ~15;
     GWAMD_LDS uint16_t* edges = (GWAMD_LDS uint16_t*)(scratch + head_bytes);
     if (head_bytes > scratch_bytes || n > 65535 || n <= 0)
         return false;
@@ -544,134 +536,63 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
     int k = 0;
     for (int v0 = 0; v0 < n; v0 += kWave)
     {
-        const int v      = v0 + lane;
-        const uint32_t w = v < n ? info[v] : 0xff000000u;
-        const bool src   = (w >> 24) == 0;
-        int total        = 0;
-        const int ex     = wave_excl_sum(src ? 1 : 0, lane, total);
-        if (k + total > kTsQueue)
-            return false;
+        const int v    = v0 + lane;
+        const bool src = v < n && (info[v] >> 24) == 0;
+        int total      = 0;
+        const int ex   = wave_excl_sum(src ? 1 : 0, lane, total);
         if (src)
-        {
-            qid[k + ex]   = uint16_t(v);
-            qinfo[k + ex] = w;
-        }
+            queue[k + ex] = uint16_t(v);
         k += total;
     }
     wave_sync();
 #ifdef GWAMD_TOPSORT_PROFILE
     const uint64_t tp1 = __builtin_amdgcn_s_memtime();
 #endif
-    // FIFO (cudapoa_topsort.cuh:58-85) on uniform values; every lane reads the
-    // same word (LDS broadcast) and writes the same value to the same address
-    constexpr int kQm = kTsQueue - 1;
-    // uniform stores: lane 0 writes the word, the other lanes write to their
-    // own dummy word (no same-address write conflict, no exec-mask branch)
-    GWAMD_LDS uint32_t* dummy = (GWAMD_LDS uint32_t*)(qid + kTsQueue) + 64;
-    auto st32 = [&](GWAMD_LDS uint32_t* p, uint32_t v) { *(lane == 0 ? p : dummy + lane) = v; };
-    auto st16 = [&](GWAMD_LDS uint16_t* p, uint16_t v) {
-        *(lane == 0 ? p : (GWAMD_LDS uint16_t*)(dummy + lane)) = v;
-    };
-    int tail          = k;
-    int q             = 0;
-    bool overflow     = false;
-    int ids           = 0; // lane (q & 63): id of entry q until stored
-    uint32_t vinfo    = tail > 0 ? uint32_t(uniform(int(qinfo[0]))) : 0u;
-    int vid           = tail > 0 ? uniform(int(qid[0])) : 0;
-    auto push         = [&](int o, uint32_t oi) {
-        st16(&qid[tail & kQm], uint16_t(o));
-        st32(&qinfo[tail & kQm], oi);
-        tail++;
-    };
-    tail = uniform(tail);
-    while (q < tail)
     {
-        q     = uniform(q);
-        tail  = uniform(tail);
-        vinfo = uint32_t(uniform(int(vinfo)));
-        vid   = uniform(vid);
-        // entry q+1 is requested now if it is already queued
-        const int qn       = (q + 1) & kQm;
-        const uint32_t nxi = qinfo[qn];
-        const int nxid     = int(qid[qn]);
-        const int qtail    = tail; // entries pushed by this step start here
-        uint32_t first_info = 0;
-        int first_id        = 0;
-        const int deg       = int((vinfo >> 16) & 63u);
-        if (deg == 1)
+        // FIFO (cudapoa_topsort.cuh:58-85)
+        int tail       = k;
+        int q          = 0;
+        uint32_t vinfo = tail > 0 ? uint32_t(uniform(int(info[int(queue[0])]))) : 0u;
+        while (q < tail)
         {
-            const int o       = int(vinfo & 0xffffu);
-            const uint32_t oi = uint32_t(uniform(int(info[o]))) - (1u << 24);
-            st32(&info[o], oi);
-            if ((oi >> 24) == 0u)
-            {
-                first_info = oi, first_id = o;
-                push(o, oi);
-            }
-        }
-        else if (deg >= 2)
-        {
-            const int off = int(vinfo & 0xffffu);
-            for (int e0 = 0; e0 < deg; e0 += 4)
-            {
-                // up to four successors: their ids, then their words, in parallel
-                int o[4];
-                uint32_t w[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    o[u] = e0 + u < deg ? int(edges[off + e0 + u]) : 0;
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    o[u] = uniform(o[u]);
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    w[u] = info[o[u]];
-#pragma unroll
-                for (int u = 0; u < 4; u++)
+            const int deg       = int((vinfo >> 16) & 63u);
+            const int qtail     = tail; // entries pushed by this step start here
+            uint32_t first_info = 0;
+            auto release        = [&](int o) {
+                const uint32_t oi = uint32_t(uniform(int(info[o]))) - (1u << 24);
+                info[o]           = oi;
+                if ((oi >> 24) == 0u)
                 {
-                    if (e0 + u < deg)
-                    {
-                        const uint32_t oi = uint32_t(uniform(int(w[u]))) - (1u << 24);
-                        st32(&info[o[u]], oi);
-                        if ((oi >> 24) == 0u)
-                        {
-                            if (tail == qtail)
-                                first_info = oi, first_id = o[u];
-                            push(o[u], oi);
-                        }
-                    }
+                    if (tail == qtail)
+                        first_info = oi;
+                    queue[tail++] = uint16_t(o);
                 }
+            };
+            if (deg == 1)
+                release(int(vinfo & 0xffffu));
+            else if (deg >= 2)
+            {
+                const int off = int(vinfo & 0xffffu);
+                for (int e = 0; e < deg; e++)
+                    release(uniform(int(edges[off + e])));
             }
+            q++;
+            if (q < tail)
+                vinfo = (q == qtail) ? first_info : uint32_t(uniform(int(info[int(queue[q])])));
         }
-        overflow = overflow || uniform(tail - q) > kTsQueue;
-        ids = lane == (q & (kWave - 1)) ? vid : ids;
-        if ((q & (kWave - 1)) == kWave - 1)
-        {
-            const int qq = (q & ~(kWave - 1)) + lane;
-            g.sorted[qq] = SizeT(ids);
-            g.pos[ids]   = SizeT(qq);
-        }
-        q++;
-        if (q < tail)
-        {
-            if (q == qtail)
-                vinfo = first_info, vid = first_id;
-            else
-                vinfo = uint32_t(uniform(int(nxi))), vid = uniform(nxid);
-        }
-        if (overflow)
-            break;
+        if (lane == 0)
+            sh[0] = tail;
     }
-    if (overflow)
-        return false; // partial HBM writes are rewritten by the fallback sort
-    if ((q & (kWave - 1)) != 0)
+    wave_sync();
+#ifdef GWAMD_TOPSORT_PROFILE
+    const uint64_t tp2 = __builtin_amdgcn_s_memtime();
+#endif
+    const int m = sh[0];
+    for (int q = lane; q < m; q += kWave)
     {
-        const int qq = (q & ~(kWave - 1)) + lane;
-        if (lane < (q & (kWave - 1)))
-        {
-            g.sorted[qq] = SizeT(ids);
-            g.pos[ids]   = SizeT(qq);
-        }
+        const int v = int(queue[q]);
+        g.sorted[q] = SizeT(v);
+        g.pos[v]    = SizeT(q);
     }
     wave_sync();
 #ifdef GWAMD_TOPSORT_PROFILE
@@ -679,11 +600,11 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
     {
         const uint64_t tp3 = __builtin_amdgcn_s_memtime();
         prof[0] += tp1 - tp0;
-        prof[1] += tp3 - tp1;
+        prof[1] += tp2 - tp1;
+        prof[2] += tp3 - tp2;
         prof[3] += uint64_t(n);
     }
 #endif
-    (void)sh;
     return true;
 }
 
