@@ -132,42 +132,46 @@ __device__ __forceinline__ void finish_window(const Buffers& b, const Dims& d, i
         if (mst == kSuccess && nseq > 0)
         {
             const SizeT* mpos = cpred;
-            // generateMSADevice (cudapoa_generate_msa.cuh:47-118): one lane per read
-            for (int s = lane; s < nseq; s += kWave)
+            // generateMSADevice (cudapoa_generate_msa.cuh:47-118).  Read s walks
+            // from seq_begin[s] along the out-edge whose read list holds s; a
+            // read's path is simple (its positions land on distinct nodes joined
+            // by its own edges), so the walk visits exactly seq_begin[s] and the
+            // ends of the edges listing s.  The rows are filled in parallel:
+            // gaps everywhere, then the base of every visited node in its column.
+            for (int t = lane; t < nseq * (msa_len + 1); t += kWave)
             {
-                uint8_t* row = msa_out + size_t(s) * d.max_consensus;
-                int node     = int(seq_begin[s]);
-                int filled   = 0;
-                while (true)
+                const int sr = t / (msa_len + 1), col = t - sr * (msa_len + 1);
+                msa_out[size_t(sr) * d.max_consensus + col] = col == msa_len ? 0 : '-';
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            wave_sync();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            for (int v = lane; v < node_count; v += kWave)
+            {
+                const int oc = int(g.out_cnt[v]);
+                if (oc == 0)
+                    continue;
+                const int mv     = int(mpos[v]);
+                const uint8_t bv = g.base[v];
+                for (int e = 0; e < oc; e++)
                 {
-                    const int mp = int(mpos[node]);
-                    row[mp]      = g.base[node];
-                    for (int i = filled; i < mp; i++)
-                        row[i] = '-';
-                    filled   = mp + 1;
-                    bool end = true;
-                    for (int e = 0; e < int(g.out_cnt[node]) && end; e++)
+                    const int to     = int(g.out_e[v * kMaxEdges + e]);
+                    const int mt     = int(mpos[to]);
+                    const uint8_t bt = g.base[to];
+                    const int cc     = int(ecovc[v * kMaxEdges + e]);
+                    for (int m = 0; m < cc; m++)
                     {
-                        const int to = int(g.out_e[node * kMaxEdges + e]);
-                        const int cc = int(ecovc[node * kMaxEdges + e]);
-                        for (int m = 0; m < cc; m++)
-                        {
-                            if (int(ecov[size_t(node * kMaxEdges + e) * d.max_seqs + m]) == s)
-                            {
-                                end  = false;
-                                node = to;
-                                break;
-                            }
-                        }
-                    }
-                    if (end)
-                    {
-                        for (int i = filled; i < msa_len; i++)
-                            row[i] = '-';
-                        break;
+                        const int sr = int(ecov[size_t(v * kMaxEdges + e) * d.max_seqs + m]);
+                        uint8_t* row = msa_out + size_t(sr) * d.max_consensus;
+                        row[mv]      = bv;
+                        row[mt]      = bt;
                     }
                 }
-                row[msa_len] = 0;
+            }
+            for (int sr = lane; sr < nseq; sr += kWave)
+            {
+                const int node                                = int(seq_begin[sr]);
+                msa_out[size_t(sr) * d.max_consensus + int(mpos[node])] = g.base[node];
             }
         }
         if (lane == 0)
