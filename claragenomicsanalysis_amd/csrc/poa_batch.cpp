@@ -9,6 +9,7 @@
 // reference throws).  Device memory is laid out for the HIP kernels
 // (poa_kernels.hip), not the reference's slab.
 #include <claraparabricks/genomeworks/cudapoa/batch.hpp>
+#include <claraparabricks/genomeworks/cudapoa/utils.hpp>
 
 #include "gwamd_cudapoa.h"
 #include "host_common.hpp"
@@ -815,6 +816,114 @@ StatusType Init()
     return StatusType::success;
 }
 
+// BatchBlock::estimate_max_poas (allocate_block.hpp:364-401)
+int64_t estimate_max_poas(const BatchSize& batch_size, bool banded_alignment, bool msa_flag,
+                          size_t free_device_memory, float memory_usage_quota, int32_t mismatch_score,
+                          int32_t gap_score, int32_t match_score)
+{
+    const size_t mem_per_batch = size_t(memory_usage_quota * double(free_device_memory));
+    int64_t sizeof_score       = 2;
+    int64_t per_poa            = 0;
+    if (use32bit_score(batch_size, int16_t(gap_score), int16_t(mismatch_score), int16_t(match_score)))
+    {
+        sizeof_score = 4;
+        per_poa      = reference_device_bytes_per_poa(batch_size, banded_alignment, msa_flag,
+                                                 use32bit_size(batch_size, banded_alignment) ? 4 : 2);
+    }
+    else
+        per_poa = reference_device_bytes_per_poa(batch_size, banded_alignment, msa_flag, 2);
+    const int64_t seq_dim = banded_alignment ? batch_size.alignment_band_width + gwamd::poa::kBandPad
+                                             : batch_size.max_matrix_sequence_dimension;
+    const int64_t graph_dim = banded_alignment ? batch_size.max_matrix_graph_dimension_banded
+                                               : batch_size.max_matrix_graph_dimension;
+    return int64_t(mem_per_batch) / (per_poa + seq_dim * graph_dim * sizeof_score);
+}
+
+// get_multi_batch_sizes (utils.cu:24-138): groups are binned by their batch
+// capacity (bins 1, 2, 4, ... 2^19 unless given), each non-empty bin becomes
+// one BatchSize sized by its largest group (max read length x reads), and the
+// following bins are merged into it while their group count fits its capacity.
+void get_multi_batch_sizes_for_memory(std::vector<BatchSize>& list_of_batch_sizes,
+                                      std::vector<std::vector<int32_t>>& list_of_groups_per_batch,
+                                      const std::vector<Group>& poa_groups, size_t free_device_memory,
+                                      bool banded_alignment, bool msa_flag, int32_t band_width,
+                                      std::vector<int32_t>* bins_capacity, float gpu_memory_usage_quota,
+                                      int32_t mismatch_score, int32_t gap_score, int32_t match_score)
+{
+    const int32_t num_groups = int32_t(poa_groups.size());
+    std::vector<int64_t> max_poas(num_groups);
+    std::vector<int32_t> max_lengths(num_groups);
+    for (int32_t i = 0; i < num_groups; i++)
+    {
+        int32_t max_read_length = 0;
+        for (const auto& e : poa_groups[i])
+            max_read_length = std::max(max_read_length, e.length);
+        max_poas[i] = estimate_max_poas(BatchSize(max_read_length, int32_t(poa_groups[i].size()), band_width),
+                                        banded_alignment, msa_flag, free_device_memory, gpu_memory_usage_quota,
+                                        mismatch_score, gap_score, match_score);
+        max_lengths[i] = max_read_length;
+    }
+    std::vector<int32_t> default_bins(20, 1);
+    for (size_t j = 1; j < default_bins.size(); j++)
+        default_bins[j] = default_bins[j - 1] * 2;
+    const std::vector<int32_t>& bins = bins_capacity ? *bins_capacity : default_bins;
+    const int32_t num_bins           = int32_t(bins.size());
+    std::vector<int32_t> freq(num_bins, 0), bin_len(num_bins, 0), bin_reads(num_bins, 0);
+    std::vector<std::vector<int32_t>> bin_groups(num_bins);
+    for (int32_t i = 0; i < num_groups; i++)
+    {
+        const int32_t current = max_lengths[i] * int32_t(poa_groups[i].size());
+        for (int32_t j = 0; j < num_bins; j++)
+        {
+            if (max_poas[i] <= bins[j] || j == num_bins - 1)
+            {
+                freq[j]++;
+                bin_groups[j].push_back(i);
+                if (bin_len[j] * bin_reads[j] < current)
+                {
+                    bin_len[j]   = max_lengths[i];
+                    bin_reads[j] = int32_t(poa_groups[i].size());
+                }
+                break;
+            }
+        }
+    }
+    for (int32_t j = 0; j < num_bins; j++)
+    {
+        if (freq[j] == 0)
+            continue;
+        list_of_batch_sizes.emplace_back(bin_len[j], bin_reads[j], band_width);
+        list_of_groups_per_batch.push_back(bin_groups[j]);
+        for (int32_t k = j + 1; k < num_bins; k++)
+        {
+            if (freq[k] == 0)
+                continue;
+            if (bins[j] >= freq[k])
+            {
+                auto& cur = list_of_groups_per_batch.back();
+                cur.insert(cur.end(), bin_groups[k].begin(), bin_groups[k].end());
+                freq[k] = 0;
+            }
+            else
+                break;
+        }
+    }
+}
+
+void get_multi_batch_sizes(std::vector<BatchSize>& list_of_batch_sizes,
+                           std::vector<std::vector<int32_t>>& list_of_groups_per_batch,
+                           const std::vector<Group>& poa_groups, bool banded_alignment, bool msa_flag,
+                           int32_t band_width, std::vector<int32_t>* bins_capacity, float gpu_memory_usage_quota,
+                           int32_t mismatch_score, int32_t gap_score, int32_t match_score)
+{
+    size_t free_mem = 0, total = 0;
+    if (hipMemGetInfo(&free_mem, &total) != hipSuccess)
+        throw std::runtime_error("get_multi_batch_sizes: hipMemGetInfo failed");
+    get_multi_batch_sizes_for_memory(list_of_batch_sizes, list_of_groups_per_batch, poa_groups, free_mem,
+                                     banded_alignment, msa_flag, band_width, bins_capacity, gpu_memory_usage_quota,
+                                     mismatch_score, gap_score, match_score);
+}
+
 std::unique_ptr<Batch> create_batch(int32_t device_id, hipStream_t stream, size_t max_mem, int8_t output_mask,
                                     const BatchSize& batch_size, int16_t gap_score, int16_t mismatch_score,
                                     int16_t match_score, bool cuda_banded_alignment)
@@ -1092,6 +1201,69 @@ int32_t gwamd_poa_get_capacity(const gwamd_poa_batch* batch, int64_t* device_byt
     *device_bytes = batch->impl->device_bytes();
     *max_poas     = batch->impl->max_poas();
     return 0;
+}
+
+static size_t query_free_memory(uint64_t given)
+{
+    if (given != 0)
+        return size_t(given);
+    size_t free_mem = 0, total = 0;
+    if (hipMemGetInfo(&free_mem, &total) != hipSuccess)
+        throw std::runtime_error("hipMemGetInfo failed");
+    return free_mem;
+}
+
+int64_t gwamd_poa_estimate_max_poas(int32_t max_seq_sz, int32_t max_seq_per_poa, int32_t band_width, int32_t banded,
+                                    int32_t msa, uint64_t free_device_memory, float quota, int32_t mismatch,
+                                    int32_t gap, int32_t match)
+{
+    int64_t r = 0;
+    const int32_t rc = guarded([&]() -> int32_t {
+        r = cp::estimate_max_poas(cp::BatchSize(max_seq_sz, max_seq_per_poa, band_width), banded != 0, msa != 0,
+                                  query_free_memory(free_device_memory), quota, mismatch, gap, match);
+        return 0;
+    });
+    return rc != 0 ? int64_t(rc) : r;
+}
+
+int32_t gwamd_poa_get_multi_batch_sizes(const int32_t* group_max_len, const int32_t* group_num_reads,
+                                        int32_t num_groups, uint64_t free_device_memory, int32_t banded,
+                                        int32_t msa, int32_t band_width, const int32_t* bins, int32_t num_bins,
+                                        float quota, int32_t mismatch, int32_t gap, int32_t match,
+                                        int32_t* num_batches, int32_t* batch_max_seq, int32_t* batch_num_reads,
+                                        int32_t* group_batch, int32_t* group_rank)
+{
+    return guarded([&]() -> int32_t {
+        // groups as Entry lists: only the longest read and the read count matter
+        std::vector<cp::Group> groups(size_t(std::max(num_groups, 0)));
+        for (int32_t i = 0; i < num_groups; i++)
+        {
+            groups[i].resize(size_t(std::max(group_num_reads[i], 1)));
+            for (auto& e : groups[i])
+                e = cp::Entry{nullptr, nullptr, 0};
+            groups[i][0].length = group_max_len[i];
+        }
+        std::vector<int32_t> bin_vec;
+        if (bins && num_bins > 0)
+            bin_vec.assign(bins, bins + num_bins);
+        std::vector<cp::BatchSize> sizes;
+        std::vector<std::vector<int32_t>> per_batch;
+        cp::get_multi_batch_sizes_for_memory(sizes, per_batch, groups, query_free_memory(free_device_memory),
+                                         banded != 0, msa != 0, band_width, bin_vec.empty() ? nullptr : &bin_vec,
+                                         quota, mismatch, gap, match);
+        *num_batches = int32_t(sizes.size());
+        for (size_t b = 0; b < sizes.size(); b++)
+        {
+            batch_max_seq[b]   = sizes[b].max_sequence_size;
+            batch_num_reads[b] = sizes[b].max_sequences_per_poa;
+            for (size_t r = 0; r < per_batch[b].size(); r++)
+            {
+                group_batch[per_batch[b][r]] = int32_t(b);
+                group_rank[per_batch[b][r]]  = int32_t(r);
+            }
+        }
+        return 0;
+    });
 }
 
 } // extern "C"

@@ -296,3 +296,100 @@ class CudaPoaBatch:
 
     def reset(self):
         self._lib.gwamd_poa_reset(self._handle)
+
+
+# --- window batching (cudapoa/include/.../utils.hpp:48-66, cudapoa/src/utils.cu:24-138) ---
+
+def _declare_utils(L):
+    i32, i64, u64, f32, vp = C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_void_p
+    L.gwamd_poa_estimate_max_poas.restype = i64
+    L.gwamd_poa_estimate_max_poas.argtypes = [i32, i32, i32, i32, i32, u64, f32, i32, i32, i32]
+    L.gwamd_poa_get_multi_batch_sizes.restype = i32
+    L.gwamd_poa_get_multi_batch_sizes.argtypes = [vp, vp, i32, u64, i32, i32, i32, vp, i32, f32, i32, i32, i32,
+                                                  vp, vp, vp, vp, vp]
+
+
+def estimate_max_poas(max_sequence_size, max_sequences_per_poa, band_width=256, banded=True, msa=False,
+                      free_device_memory=0, gpu_memory_usage_quota=0.9, mismatch=-6, gap=-8, match=8):
+    """BatchBlock::estimate_max_poas (allocate_block.hpp:364-401); free_device_memory 0
+    queries the current device."""
+    L = load_library()
+    _declare_utils(L)
+    r = L.gwamd_poa_estimate_max_poas(int(max_sequence_size), int(max_sequences_per_poa), int(band_width),
+                                      int(bool(banded)), int(bool(msa)), int(free_device_memory),
+                                      float(gpu_memory_usage_quota), int(mismatch), int(gap), int(match))
+    _check(int(r) if r < 0 else 0)
+    return int(r)
+
+
+def get_multi_batch_sizes(groups, banded_alignment=True, msa_flag=False, band_width=256, bins_capacity=None,
+                          gpu_memory_usage_quota=0.9, mismatch_score=-6, gap_score=-8, match_score=8,
+                          free_device_memory=0):
+    """Bins POA groups (lists of reads) into batch sizes, as the reference's
+    get_multi_batch_sizes.  Returns (list of (max_sequence_size,
+    max_sequences_per_poa), list of group-index lists per batch)."""
+    L = load_library()
+    _declare_utils(L)
+    n = len(groups)
+    ml = np.array([max([len(r) for r in g] + [0]) for g in groups], np.int32)
+    nr = np.array([len(g) for g in groups], np.int32)
+    bins = np.array(bins_capacity, np.int32) if bins_capacity is not None else None
+    nb = np.zeros(1, np.int32)
+    bmax = np.zeros(max(n, 1), np.int32)
+    bnr = np.zeros(max(n, 1), np.int32)
+    gb = np.full(max(n, 1), -1, np.int32)
+    gr = np.zeros(max(n, 1), np.int32)
+    _check(L.gwamd_poa_get_multi_batch_sizes(
+        ml.ctypes.data, nr.ctypes.data, n, int(free_device_memory), int(bool(banded_alignment)), int(bool(msa_flag)),
+        int(band_width), bins.ctypes.data if bins is not None else None, len(bins) if bins is not None else 0,
+        float(gpu_memory_usage_quota), int(mismatch_score), int(gap_score), int(match_score),
+        nb.ctypes.data, bmax.ctypes.data, bnr.ctypes.data, gb.ctypes.data, gr.ctypes.data))
+    k = int(nb[0])
+    sizes = [(int(bmax[b]), int(bnr[b])) for b in range(k)]
+    per_batch = [[] for _ in range(k)]
+    for g in sorted(range(n), key=lambda g: (gb[g], gr[g])):
+        per_batch[int(gb[g])].append(g)
+    return sizes, per_batch
+
+
+def parse_cudapoa_file(filename, total_windows=-1):
+    """cudapoa window format (utils.hpp:88-132): a count line, then that many reads."""
+    windows, left = [], 0
+    with open(filename) as f:
+        for line in f:
+            line = line.rstrip("\n")
+            if left == 0:
+                left = int(line.split()[0]) if line.split() else 0
+                windows.append([])
+            else:
+                windows[-1].append(line)
+                left -= 1
+    return resize_windows(windows, total_windows)
+
+
+def parse_fasta_files(paths, total_windows=-1):
+    """One window per FASTA file, its records in file order (utils.hpp:142-157)."""
+    windows = []
+    for p in paths:
+        recs = []
+        with open(p) as f:
+            for line in f:
+                line = line.rstrip("\r\n")
+                if line.startswith(">"):
+                    recs.append("")
+                elif recs:
+                    recs[-1] += line
+        windows.append(recs)
+    return resize_windows(windows, total_windows)
+
+
+def resize_windows(windows, total_windows):
+    """Truncate or cyclically repeat to total_windows; -1 keeps all (utils.hpp:68-86)."""
+    if total_windows is None or total_windows < 0:
+        return windows
+    if len(windows) > total_windows:
+        return windows[:total_windows]
+    read = len(windows)
+    while len(windows) < total_windows:
+        windows.append(windows[len(windows) - read])
+    return windows

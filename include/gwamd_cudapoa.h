@@ -119,6 +119,27 @@ int32_t gwamd_poa_get_types(const gwamd_poa_batch* batch, int32_t* score_bits, i
 /* Device bytes allocated by the batch and its window capacity (max_poas). */
 int32_t gwamd_poa_get_capacity(const gwamd_poa_batch* batch, int64_t* device_bytes, int32_t* max_poas);
 
+/* BatchBlock::estimate_max_poas (allocate_block.hpp:364-401) for a
+ * BatchSize(max_seq_sz, max_seq_per_poa, band_width); free_device_memory 0
+ * queries the current device. */
+int64_t gwamd_poa_estimate_max_poas(int32_t max_seq_sz, int32_t max_seq_per_poa, int32_t band_width,
+                                    int32_t banded, int32_t msa, uint64_t free_device_memory, float quota,
+                                    int32_t mismatch, int32_t gap, int32_t match);
+
+/* get_multi_batch_sizes (utils.hpp:48-66, utils.cu:24-138) over groups given
+ * by their longest read and read count.  Outputs: *num_batches, per batch its
+ * BatchSize(max_sequence_size, max_sequences_per_poa) in batch_max_seq /
+ * batch_num_reads (capacity num_groups), and per group its batch index and its
+ * rank inside that batch's group list.  bins (num_bins > 0) replaces the
+ * default capacities 1, 2, 4, ... 2^19.  free_device_memory 0 queries the
+ * current device.  Returns 0 or GWAMD_E_INVALID_ARGUMENT. */
+int32_t gwamd_poa_get_multi_batch_sizes(const int32_t* group_max_len, const int32_t* group_num_reads,
+                                        int32_t num_groups, uint64_t free_device_memory, int32_t banded,
+                                        int32_t msa, int32_t band_width, const int32_t* bins, int32_t num_bins,
+                                        float quota, int32_t mismatch, int32_t gap, int32_t match,
+                                        int32_t* num_batches, int32_t* batch_max_seq, int32_t* batch_num_reads,
+                                        int32_t* group_batch, int32_t* group_rank);
+
 #ifdef __cplusplus
 }
 #endif
