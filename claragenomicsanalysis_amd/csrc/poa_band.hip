@@ -1208,8 +1208,10 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
             ph.lap<kPhAdd>();
             if (rc == kSuccess)
             {
-                if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, (GWAMD_LDS int*)(shb),
-                                        lane, tsprof))
+                if (d.spoa_accurate)
+                    rc = topsort_racon_wave<SizeT>(g, nc, cscore, cpred, 4 * d.max_nodes, lane);
+                else if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, (GWAMD_LDS int*)(shb),
+                                             lane, tsprof))
                 {
                     if (lane == 0)
                         topsort_kahn<SizeT>(g, nc, cscore);

@@ -144,6 +144,10 @@ public:
         dims_.score_rows    = dims_.max_nodes + 2;
         dims_.aln_cap       = dims_.max_nodes + bs_.max_sequence_size + 4;
         dims_.want_consensus = (output_mask_ & OutputType::consensus) ? 1 : 0;
+        // the reference's spoa_accurate build option (CMakeLists.txt:23-30) as a
+        // process-wide default; gwamd_poa_set_spoa_accurate switches one batch
+        if (const char* sa = std::getenv("GWAMD_SPOA_ACCURATE"))
+            dims_.spoa_accurate = std::atoi(sa) != 0 ? 1 : 0;
         plan_lds_kernel();
         plan_band_kernel();
         const int64_t own = own_bytes_per_window(sz, sbytes, msa);
@@ -413,6 +417,8 @@ public:
     int64_t device_bytes() const { return int64_t(d_slab_.n + d_codes_.n + d_seqs_.n + d_wts_.n + d_len_.n + d_off_.n + d_win_.n); }
     int32_t kernel_kind() const { return dims_.lds_kernel == 3 ? 3 : (dims_.lds_kernel ? 2 : 1); }
     int32_t max_poas() const { return max_poas_; }
+    void set_spoa_accurate(bool on) { dims_.spoa_accurate = on ? 1 : 0; }
+    bool spoa_accurate() const { return dims_.spoa_accurate != 0; }
 
     void get_phases(int64_t* out)
     {
@@ -1194,6 +1200,13 @@ int32_t gwamd_poa_get_types(const gwamd_poa_batch* batch, int32_t* score_bits, i
     *score_bits = batch->impl->score_bits();
     *size_bits  = batch->impl->size_bits();
     return batch->impl->kernel_kind();
+}
+
+int32_t gwamd_poa_set_spoa_accurate(gwamd_poa_batch* batch, int32_t on)
+{
+    const int32_t was = batch->impl->spoa_accurate() ? 1 : 0;
+    batch->impl->set_spoa_accurate(on != 0);
+    return was;
 }
 
 int32_t gwamd_poa_get_capacity(const gwamd_poa_batch* batch, int64_t* device_bytes, int32_t* max_poas)

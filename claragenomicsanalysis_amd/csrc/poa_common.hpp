@@ -57,6 +57,7 @@ struct Dims
     int32_t aln_cap;       // traceback buffer capacity
     int32_t band_width;    // banded mode only
     int32_t want_consensus; // MSA kernels also emit the consensus when set
+    int32_t spoa_accurate;  // per-read racon DFS sort instead of Kahn (SPOA_ACCURATE builds)
     // LDS-resident kernel (full alignment, 16-bit scores): layout of the
     // per-workgroup LDS image and of the per-window HBM side buffers
     int32_t lds_kernel;     // 1: launch the LDS-resident kernel

@@ -135,7 +135,15 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
                                                        d.max_seqs);
                 ph.lap<kPhAdd>();
                 if (rc == kSuccess)
-                    topsort_kahn<SizeT>(g, nc, cscore);
+                {
+                    if (d.spoa_accurate) // cudapoa_kernels.cuh:324-337
+                    {
+                        if (!topsort_racon<SizeT>(g, nc, cscore, cpred, 4 * d.max_nodes))
+                            rc = kGenericError;
+                    }
+                    else
+                        topsort_kahn<SizeT>(g, nc, cscore);
+                }
                 ph.lap<kPhTopsort>();
                 sh_status = rc;
                 sh_len    = nc;
@@ -1101,8 +1109,10 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
                 ph.lap<kPhAdd>();
                 if (rc == kSuccess)
                 {
+                    if (d.spoa_accurate)
+                        rc = topsort_racon_wave<SizeT>(g, nc, cscore, cpred, 4 * d.max_nodes, lane);
                     // scratch: the read and the ring (both free after the add)
-                    if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, AX.sh, lane))
+                    else if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, AX.sh, lane))
                     {
                         if (lane == 0)
                             topsort_kahn<SizeT>(g, nc, cscore);

@@ -463,6 +463,19 @@ __device__ __forceinline__ int add_alignment_parallel(WinGraph<SizeT> g, int& no
     return kSuccess;
 }
 
+// SPOA_ACCURATE per-read sort (cudapoa_kernels.cuh:324-337): the racon DFS on
+// lane 0 of the window's wave; returns the window status for every lane.
+template <typename SizeT>
+__device__ __forceinline__ int topsort_racon_wave(WinGraph<SizeT> g, int n, int32_t* marks, SizeT* stack, int cap,
+                                                  int lane)
+{
+    int ok = 1;
+    if (lane == 0)
+        ok = topsort_racon<SizeT>(g, n, marks, stack, cap) ? 1 : 0;
+    wave_sync();
+    return __builtin_amdgcn_readfirstlane(ok) ? int(kSuccess) : int(kGenericError);
+}
+
 // ---------------------------------------------------------------------------
 // Kahn topological sort (cudapoa_topsort.cuh:38-88) over an LDS copy of the
 // out-edge lists.  One 32-bit word per node holds the remaining in-degree

@@ -108,7 +108,7 @@ class CudaPoaBatch:
     def __init__(self, max_sequences_per_poa, max_sequence_size, max_gpu_mem, output_type="consensus",
                  device_id=0, stream=None, gap_score=-8, mismatch_score=-6, match_score=8,
                  cuda_banded_alignment=False, alignment_band_width=256, max_consensus_size=None,
-                 max_nodes_per_window=None, max_nodes_per_window_banded=None, *args, **kwargs):
+                 max_nodes_per_window=None, max_nodes_per_window_banded=None, spoa_accurate=None, *args, **kwargs):
         self._lib = load_library()
         self._handle = C.c_void_p()
         if stream is None:
@@ -138,6 +138,8 @@ class CudaPoaBatch:
         _check(self._lib.gwamd_poa_create_batch(C.byref(self._handle), device_id, st, int(max_gpu_mem),
                                                 output_mask, C.byref(self.batch_size), gap_score, mismatch_score,
                                                 match_score, int(bool(cuda_banded_alignment))))
+        if spoa_accurate is not None:  # None: GWAMD_SPOA_ACCURATE decides (reference: build option)
+            self.set_spoa_accurate(spoa_accurate)
 
     def __del__(self):
         h = getattr(self, "_handle", None)
@@ -288,6 +290,11 @@ class CudaPoaBatch:
         """1: global-memory kernel, 2: LDS-resident kernel (full), 3: banded kernel."""
         sb, zb = C.c_int32(), C.c_int32()
         return self._lib.gwamd_poa_get_types(self._handle, C.byref(sb), C.byref(zb))
+
+    def set_spoa_accurate(self, on=True):
+        """SPOA_ACCURATE mode (cudapoa_kernels.cuh:324-337): racon DFS sort after every read.
+        Returns the previous setting."""
+        return bool(self._lib.gwamd_poa_set_spoa_accurate(self._handle, int(bool(on))))
 
     def get_capacity(self):
         nb, mp = C.c_int64(), C.c_int32()

@@ -116,6 +116,13 @@ int32_t gwamd_poa_get_phase_ticks(gwamd_poa_batch* batch, int64_t* ticks);
 /* Score/size types chosen by create_batch (16 or 32 bits each); returns the
  * kernel variant (1: global-memory kernel, 2: LDS-resident kernel). */
 int32_t gwamd_poa_get_types(const gwamd_poa_batch* batch, int32_t* score_bits, int32_t* size_bits);
+/* SPOA_ACCURATE mode (reference build option spoa_accurate, CMakeLists.txt:23-30;
+ * cudapoa_kernels.cuh:324-337): after each read the graph is re-sorted with the
+ * racon/SPOA DFS (cudapoa_topsort.cuh:94-189) instead of Kahn's order, which
+ * matches SPOA's consensus order at a lower speed.  Takes effect at the next
+ * generate_poa; returns the previous setting.  Default: the GWAMD_SPOA_ACCURATE
+ * environment variable at create time (off when unset). */
+int32_t gwamd_poa_set_spoa_accurate(gwamd_poa_batch* batch, int32_t on);
 /* Device bytes allocated by the batch and its window capacity (max_poas). */
 int32_t gwamd_poa_get_capacity(const gwamd_poa_batch* batch, int64_t* device_bytes, int32_t* max_poas);
 

@@ -42,6 +42,8 @@ def _declare(L):
     L.oracle_poa_batch.restype = C.c_int
     L.oracle_poa_batch.argtypes = [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
                                    vp, vp, vp, vp, vp, i32, vp]
+    L.oracle_set_spoa_accurate.restype = None
+    L.oracle_set_spoa_accurate.argtypes = [C.c_int32]
     L.oracle_topsort.restype = None
     L.oracle_topsort.argtypes = [i32, vp, vp, vp, vp]
     L.oracle_nw.restype = C.c_int
@@ -78,8 +80,9 @@ class WindowResult:
 
 def poa_window(reads, weights=None, gap=-8, mismatch=-6, match=8, banded=False, band_width=256,
                score_bits=16, msa=False, max_nodes=None, max_consensus=None, max_seqs=None,
-               want_graph=False):
-    """Run one window through the restatement; reads are bytes/str."""
+               want_graph=False, spoa_accurate=False):
+    """Run one window through the restatement; reads are bytes/str.  spoa_accurate:
+    racon DFS sort after every read (cudapoa_kernels.cuh:324-337)."""
     reads = [r.encode() if isinstance(r, str) else bytes(r) for r in reads]
     max_len = max([len(r) for r in reads] + [1])
     if max_nodes is None:
@@ -108,10 +111,14 @@ def poa_window(reads, weights=None, gap=-8, mismatch=-6, match=8, banded=False, 
         gc = np.zeros(max_nodes, dtype=np.int32)
         ge = np.zeros(max_nodes * MAX_EDGES, dtype=np.int32)
         gw = np.zeros(max_nodes * MAX_EDGES, dtype=np.int32)
-    st = lib().oracle_poa_window(_p(seqs), _p(lens), _p(wts), len(reads), gap, mismatch, match, int(banded),
-                                 band_width, score_bits, int(msa), max_nodes, max_consensus, max_seqs,
-                                 _p(cons), _p(cov), _p(clen), _p(msa_buf), _p(cells), _p(fnodes),
-                                 _p(gb), _p(gc), _p(ge), _p(gw))
+    lib().oracle_set_spoa_accurate(int(bool(spoa_accurate)))
+    try:
+        st = lib().oracle_poa_window(_p(seqs), _p(lens), _p(wts), len(reads), gap, mismatch, match, int(banded),
+                                     band_width, score_bits, int(msa), max_nodes, max_consensus, max_seqs,
+                                     _p(cons), _p(cov), _p(clen), _p(msa_buf), _p(cells), _p(fnodes),
+                                     _p(gb), _p(gc), _p(ge), _p(gw))
+    finally:
+        lib().oracle_set_spoa_accurate(0)
     n = int(clen[0])
     consensus = bytes(cons[:n]).decode() if st == 0 and not msa else ""
     coverage = cov[:n].tolist() if st == 0 and not msa else []
@@ -131,7 +138,7 @@ def poa_window(reads, weights=None, gap=-8, mismatch=-6, match=8, banded=False, 
 
 
 def poa_batch(windows, nthreads=0, gap=-8, mismatch=-6, match=8, banded=False, band_width=256, score_bits=16,
-              max_nodes=None, max_consensus=None, max_seqs=None, msa=False):
+              max_nodes=None, max_consensus=None, max_seqs=None, msa=False, spoa_accurate=False):
     """Run many windows (list of lists of bytes) on all host cores (OpenMP).
     Returns (consensus list, status array, cells array, threads used); with
     msa=True the first element is the list of MSA row lists instead."""
@@ -167,10 +174,14 @@ def poa_batch(windows, nthreads=0, gap=-8, mismatch=-6, match=8, banded=False, b
     status = np.zeros(nw, dtype=np.uint8)
     cells = np.zeros(nw, dtype=np.int64)
     msa_buf = np.zeros(nw * max_seqs * max_consensus, dtype=np.uint8) if msa else None
-    used = lib().oracle_poa_batch(_p(seqs), _p(offs), _p(lens_a), _p(first_a), _p(nseq_a), nw, gap, mismatch,
-                                  match, int(banded), band_width, score_bits, max_nodes, max_consensus, max_seqs,
-                                  nthreads, _p(cons), _p(cov), _p(clen), _p(status), _p(cells), int(msa),
-                                  _p(msa_buf))
+    lib().oracle_set_spoa_accurate(int(bool(spoa_accurate)))
+    try:
+        used = lib().oracle_poa_batch(_p(seqs), _p(offs), _p(lens_a), _p(first_a), _p(nseq_a), nw, gap, mismatch,
+                                      match, int(banded), band_width, score_bits, max_nodes, max_consensus,
+                                      max_seqs, nthreads, _p(cons), _p(cov), _p(clen), _p(status), _p(cells),
+                                      int(msa), _p(msa_buf))
+    finally:
+        lib().oracle_set_spoa_accurate(0)
     if msa:
         rows = []
         for i in range(nw):

@@ -719,12 +719,16 @@ static void topsort_fast(Graph& g, std::vector<uint16_t>& local)
 }
 
 // --- racon/SPOA DFS topological sort: cudapoa_topsort.cuh:94-189 -----------------
-static void topsort_racon(Graph& g)
+// The DFS stack holds at most 4 x max_nodes entries (the kernels' bound; the
+// reference's nodes_to_visit has no bound check): beyond it the window fails
+// with generic_error.
+static bool topsort_racon(Graph& g)
 {
     const int n = g.node_count;
     std::vector<uint8_t> mark(g.max_nodes, 0);
     std::vector<uint8_t> check(g.max_nodes, 1);
-    std::vector<int32_t> stack(g.max_nodes + 1, 0);
+    const int cap = 4 * g.max_nodes;
+    std::vector<int32_t> stack(cap, 0);
     int top = -1, k = 0;
     for (int v = 0; v < n; v++)
     {
@@ -742,6 +746,8 @@ static void topsort_racon(Graph& g)
                     int b = g.in_e[id * kMaxEdges + e];
                     if (mark[b] != 2)
                     {
+                        if (top + 1 >= cap)
+                            return false;
                         stack[++top] = b;
                         valid        = false;
                     }
@@ -753,6 +759,8 @@ static void topsort_racon(Graph& g)
                         int aid = g.aln[id * kMaxAlignments + a];
                         if (mark[aid] != 2)
                         {
+                            if (top + 1 >= cap)
+                                return false;
                             stack[++top] = aid;
                             check[aid]   = 0;
                             valid        = false;
@@ -783,6 +791,7 @@ static void topsort_racon(Graph& g)
                 top--;
         }
     }
+    return true;
 }
 
 // --- heaviest bundle: cudapoa_generate_consensus.cuh:28-276 ----------------------
@@ -897,7 +906,8 @@ static uint8_t consensus_raw(const Graph& g, uint8_t* cons, uint16_t* covg, int 
 // --- MSA: cudapoa_generate_msa.cuh:27-118, kernel :121-224 -----------------------
 static uint8_t generate_msa(Graph& g, int nseq, int max_cons, uint8_t* msa_out /* nseq x max_cons */)
 {
-    topsort_racon(g);
+    if (!topsort_racon(g))
+        return kGenericError;
     const int n = g.node_count;
     std::vector<int32_t> mpos(g.max_nodes, 0);
     int msa_len = 0;
@@ -958,6 +968,7 @@ struct WindowParams
     int score_bits; // 16 or 32, only observable in banded mode
     int msa;
     int max_nodes, max_consensus, max_seqs;
+    int spoa_accurate = 0; // per-read racon DFS sort (SPOA_ACCURATE builds)
 };
 
 struct WindowStats
@@ -1017,7 +1028,13 @@ static uint8_t run_window(const WindowParams& P, const uint8_t* seqs, const int3
         uint8_t err = add_alignment(g, ag, ar, alen, seq, w, s);
         if (err != kSuccess)
             return err;
-        topsort_fast(g, local);
+        if (P.spoa_accurate) // cudapoa_kernels.cuh:324-337 (SPOA_ACCURATE builds)
+        {
+            if (!topsort_racon(g))
+                return kGenericError;
+        }
+        else
+            topsort_fast(g, local);
     }
     if (st)
         st->final_nodes = g.node_count;
@@ -1042,7 +1059,12 @@ static uint8_t run_window(const WindowParams& P, const uint8_t* seqs, const int3
 
 using namespace oracle;
 
+// SPOA_ACCURATE for the calls below (the reference's build option, here a switch)
+static int g_spoa_accurate = 0;
+
 extern "C" {
+
+void oracle_set_spoa_accurate(int32_t on) { g_spoa_accurate = on != 0; }
 
 // One POA window.  Outputs: consensus (host order, length in *cons_len) and
 // coverage, or MSA rows (nseq x max_consensus, NUL terminated), plus the final
@@ -1055,7 +1077,8 @@ int oracle_poa_window(const uint8_t* seqs, const int32_t* lens, const int8_t* wt
                       int64_t* cells, int32_t* final_nodes,
                       uint8_t* g_bases, int32_t* g_in_cnt, int32_t* g_in_e, int32_t* g_in_w)
 {
-    WindowParams P{gap, mismatch, match, banded, band_width, score_bits, msa, max_nodes, max_consensus, max_seqs};
+    WindowParams P{gap, mismatch, match, banded, band_width, score_bits, msa, max_nodes, max_consensus, max_seqs,
+                   g_spoa_accurate};
     Graph g;
     WindowStats st{0, 0, 0};
     *cons_len   = 0;
@@ -1091,7 +1114,8 @@ int oracle_poa_batch(const uint8_t* seqs, const int64_t* seq_offsets, const int3
 {
     // msa != 0: MSA output (generateMSAKernel) into msa_out, window wi at
     // wi * max_seqs * max_consensus (rows NUL terminated)
-    WindowParams P{gap, mismatch, match, banded, band_width, score_bits, msa, max_nodes, max_consensus, max_seqs};
+    WindowParams P{gap, mismatch, match, banded, band_width, score_bits, msa, max_nodes, max_consensus, max_seqs,
+                   g_spoa_accurate};
     int used = 1;
 #ifdef _OPENMP
     if (nthreads > 0)

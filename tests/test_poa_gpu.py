@@ -36,7 +36,7 @@ def run_oracle(w, max_seq, max_seqs, banded=False, bw=256, msa=False, score_bits
     mn = kw.get("max_nodes", ((4 if banded else 3) * max_seq + 3) // 4 * 4)
     return oracle.poa_window(w, banded=banded, band_width=bw, msa=msa, score_bits=score_bits,
                              max_nodes=mn, max_consensus=kw.get("max_consensus", 2 * max_seq), max_seqs=max_seqs,
-                             want_graph=kw.get("want_graph", False))
+                             want_graph=kw.get("want_graph", False), spoa_accurate=kw.get("spoa_accurate", False))
 
 
 def test_kat_all_A():
@@ -295,3 +295,33 @@ def test_banded_kernel_msa_graph_int32(monkeypatch):
     for i, w in enumerate(wins):
         r = run_oracle(w, 4200, 9, banded=True, bw=256, msa=True, score_bits=32)
         assert (st[i], msa[i]) == (r.status, r.msa), i
+
+
+@pytest.mark.parametrize("variant", ["v1", "fast"])
+@pytest.mark.parametrize("banded", [False, True])
+@pytest.mark.parametrize("out", ["consensus", "msa"])
+def test_spoa_accurate(variant, banded, out, monkeypatch):
+    # SPOA_ACCURATE (cudapoa_kernels.cuh:324-337): racon DFS sort after every
+    # read, on every kernel; these windows include ones whose output differs
+    # from the default Kahn-order build, so the mode is observable
+    if variant == "v1":
+        monkeypatch.setenv("GWAMD_POA_KERNEL", "v1")
+    else:
+        monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    wins = synth.poa_windows(100, 16, 300, 20, 60, 60, 60)
+    b = run_gpu(wins, 400, 20, banded=banded, bw=256, output_type=out, spoa_accurate=True)
+    assert b.kernel_variant() == (1 if variant == "v1" else (3 if banded else 2))
+    sbits = b.get_types()[0]
+    if out == "msa":
+        got, st = b.get_msa()
+    else:
+        cons, cov, st = b.get_consensus()
+        got = list(zip(cons, cov))
+    differ = 0
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 400, 20, banded=banded, bw=256, msa=(out == "msa"), score_bits=sbits, spoa_accurate=True)
+        k = run_oracle(w, 400, 20, banded=banded, bw=256, msa=(out == "msa"), score_bits=sbits)
+        want = r.msa if out == "msa" else (r.consensus, r.coverage)
+        assert (st[i], got[i]) == (r.status, want), i
+        differ += (k.msa if out == "msa" else (k.consensus, k.coverage)) != want
+    assert differ > 0
