@@ -71,6 +71,8 @@ def _declare(L):
     if hasattr(L, "gwamd_aligner_create"):
         from . import cudaaligner
         cudaaligner._declare(L)
+    from . import cudamapper
+    cudamapper._declare(L)
 
 
 def last_error():
