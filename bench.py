@@ -89,7 +89,8 @@ def parse():
     p.add_argument("--windows", type=int, default=None, help="override windows per GPU")
     p.add_argument("--cpu-sample", type=int, default=None, help="windows in the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_poa_B.json"))
+    p.add_argument("--traffic-file", default=None,
+                   help="PMC HBM bytes per launch (default profiles/traffic_poa_<config>.json)")
     return p.parse_args()
 
 
@@ -364,6 +365,8 @@ def main():
         kernel_s = kernel_ms / 1e3
         achieved = alg_bytes / kernel_s / 1e9
         traffic = None
+        if args.traffic_file is None:
+            args.traffic_file = os.path.join(ROOT, "profiles", "traffic_poa_%s.json" % args.config)
         if os.path.exists(args.traffic_file):
             try:
                 tf = json.load(open(args.traffic_file))
