@@ -1206,6 +1206,8 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
                 nc = sh_len;
             }
             ph.lap<kPhAdd>();
+            rc = uniform(rc); // wave-uniform: the sort below runs scalar control flow
+            nc = uniform(nc);
             if (rc == kSuccess)
             {
                 if (d.spoa_accurate)

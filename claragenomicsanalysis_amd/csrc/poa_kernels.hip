@@ -134,6 +134,8 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
                 uint8_t rc = add_alignment<SizeT, MSA>(g, nc, ag, ar, alen, read_g, wts_g, s, ecov, ecovc, seq_begin,
                                                        d.max_seqs);
                 ph.lap<kPhAdd>();
+                rc = uniform(rc); // wave-uniform: the sort below runs scalar control flow
+                nc = uniform(nc);
                 if (rc == kSuccess)
                 {
                     if (d.spoa_accurate) // cudapoa_kernels.cuh:324-337

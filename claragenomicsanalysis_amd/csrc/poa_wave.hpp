@@ -549,16 +549,26 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
         }
     }
     wave_sync();
+    // queued nodes' final info words next to the queue when they fit: a pop is
+    // then one LDS read instead of two dependent ones
+    const int qinfo_off          = (head_bytes + ebase * 2 + 15) & ~15;
+    const bool use_q             = qinfo_off + n * 4 <= scratch_bytes;
+    GWAMD_LDS uint32_t* qinfo    = (GWAMD_LDS uint32_t*)(scratch + qinfo_off);
     // sources in id order
     int k = 0;
     for (int v0 = 0; v0 < n; v0 += kWave)
     {
         const int v    = v0 + lane;
-        const bool src = v < n && (info[v] >> 24) == 0;
+        const uint32_t vi = v < n ? info[v] : 1u << 24;
+        const bool src = (vi >> 24) == 0;
         int total      = 0;
         const int ex   = wave_excl_sum(src ? 1 : 0, lane, total);
         if (src)
+        {
             queue[k + ex] = uint16_t(v);
+            if (use_q)
+                qinfo[k + ex] = vi;
+        }
         k += total;
     }
     wave_sync();
@@ -567,35 +577,62 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
 #endif
     {
         // FIFO (cudapoa_topsort.cuh:58-85)
-        int tail       = k;
+        int tail       = uniform(k);
         int q          = 0;
         uint32_t vinfo = tail > 0 ? uint32_t(uniform(int(info[int(queue[0])]))) : 0u;
         while (q < tail)
         {
+            // the loop state is wave-uniform; saying so keeps it in SGPRs with
+            // scalar branches whatever the caller's control flow looks like
+            tail                = uniform(tail);
+            q                   = uniform(q);
+            vinfo               = uint32_t(uniform(int(vinfo)));
             const int deg       = int((vinfo >> 16) & 63u);
             const int qtail     = tail; // entries pushed by this step start here
             uint32_t first_info = 0;
-            auto release        = [&](int o) {
+            if (deg == 1)
+            {
+                const int o       = int(vinfo & 0xffffu);
                 const uint32_t oi = uint32_t(uniform(int(info[o]))) - (1u << 24);
                 info[o]           = oi;
                 if ((oi >> 24) == 0u)
                 {
-                    if (tail == qtail)
-                        first_info = oi;
+                    first_info = oi;
+                    if (use_q)
+                        qinfo[tail] = oi;
                     queue[tail++] = uint16_t(o);
                 }
-            };
-            if (deg == 1)
-                release(int(vinfo & 0xffffu));
+            }
             else if (deg >= 2)
             {
-                const int off = int(vinfo & 0xffffu);
-                for (int e = 0; e < deg; e++)
-                    release(uniform(int(edges[off + e])));
+                // all successors at once, one per lane: children are distinct,
+                // so the decrements are independent; ready ones are queued in
+                // successor-slot order (cudapoa_topsort.cuh:72-83)
+                const int off     = int(vinfo & 0xffffu);
+                const bool act    = lane < deg;
+                const int o       = act ? int(edges[off + lane]) : 0;
+                const uint32_t oi = act ? info[o] - (1u << 24) : 0xffffffffu;
+                if (act)
+                    info[o] = oi;
+                const bool rdy       = act && (oi >> 24) == 0u;
+                const uint64_t ready = __builtin_amdgcn_ballot_w64(rdy);
+                if (ready)
+                {
+                    const int before = __popcll(ready & ((uint64_t(1) << lane) - 1));
+                    if (rdy)
+                    {
+                        queue[tail + before] = uint16_t(o);
+                        if (use_q)
+                            qinfo[tail + before] = oi;
+                    }
+                    first_info = uint32_t(__builtin_amdgcn_readlane(int(oi), __builtin_ctzll(ready)));
+                    tail += __popcll(ready);
+                }
             }
             q++;
             if (q < tail)
-                vinfo = (q == qtail) ? first_info : uint32_t(uniform(int(info[int(queue[q])])));
+                vinfo = (q == qtail) ? first_info
+                                     : uint32_t(uniform(int(use_q ? qinfo[q] : info[int(queue[q])])));
         }
         if (lane == 0)
             sh[0] = tail;
