@@ -552,7 +552,7 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
     // queued nodes' final info words next to the queue when they fit: a pop is
     // then one LDS read instead of two dependent ones
     const int qinfo_off          = (head_bytes + ebase * 2 + 15) & ~15;
-    const bool use_q             = qinfo_off + n * 4 <= scratch_bytes;
+    const bool use_q             = uniform(int(qinfo_off + n * 4 <= scratch_bytes)) != 0;
     GWAMD_LDS uint32_t* qinfo    = (GWAMD_LDS uint32_t*)(scratch + qinfo_off);
     // sources in id order
     int k = 0;
