@@ -898,6 +898,84 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
         }
     };
     bool bad = false;
+    // code tile: kBandTile rows of bw = 64*CPL code bytes from row ti0 on, and
+    // their row records one per lane
+    auto load_tile = [&](int ii) {
+        const uint64_t tt0 = BandProf::now();
+        ti0 = max(1, ii - (kBandTile - 1));
+        wave_sync();
+        // 4*CPL 16-B pieces per lane, all loads issued before the first store waits
+        constexpr int kPer    = 4 * CPL;
+        constexpr int kPerRow = 4 * CPL; // 16-B pieces per code row
+        v4i_t q[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; u++)
+        {
+            const int t  = u * kWave + lane;
+            const int rr = min(ti0 + t / kPerRow, V); // rows past V: never read
+            q[u]         = *reinterpret_cast<const v4i_t*>(X.codes + size_t(rr) * bw + (t % kPerRow) * 16);
+        }
+        {
+            const int rr = min(ti0 + lane, V); // kBandTile == kWave: one record per lane
+            ta           = X.reca[rr];
+            tb           = X.recb[rr];
+            tcw          = X.recc[rr];
+        }
+#pragma unroll
+        for (int u = 0; u < kPer; u++)
+        {
+            const int t = u * kWave + lane;
+            *reinterpret_cast<GWAMD_LDS v4i_t*>(tile + (t / kPerRow) * bw + (t % kPerRow) * 16) = q[u];
+        }
+        wave_sync();
+        bp.add(kBpTileCyc, BandProf::now() - tt0);
+    };
+    // Move window: the moves out of kWinR x kWinC cells (rows wi0-kWinR+1..wi0,
+    // columns wj0-kWinC+1..wj0) decoded in one lane-parallel pass, two cells
+    // per lane, packed (row << 16 | column); the walk then takes them with
+    // readlane instead of one LDS round trip and its decoding per step.  Cells
+    // whose move needs more than the tile and the inline predecessor distances
+    // (row 0, column 0, outside the band, listed or escaped predecessor rows,
+    // no move) are kSlow and go through the general step.
+    constexpr int kWinR     = 16;
+    constexpr int kWinC     = 8;
+    constexpr uint32_t kSlow = 0xffffffffu;
+    const bool win_ok       = V < 65535 && L < 65535;
+    int wi0 = -1, wj0 = -1;
+    uint32_t wpk0 = kSlow, wpk1 = kSlow;
+    auto decode_cell = [&](int t) -> uint32_t {
+        const int r   = wi0 - t / kWinC;
+        const int c   = wj0 - t % kWinC;
+        const int src = min(max(r - ti0, 0), kWave - 1);
+        const uint32_t a  = uint32_t(__builtin_amdgcn_ds_bpermute(src * 4, int(ta)));
+        const uint32_t b  = uint32_t(__builtin_amdgcn_ds_bpermute(src * 4, int(tb)));
+        const uint32_t cw = uint32_t(__builtin_amdgcn_ds_bpermute(src * 4, int(tcw)));
+        uint32_t res = kSlow;
+        const int bs = ra_bs(a);
+        if (r >= 1 && c >= 1 && r >= ti0 && r < ti0 + kBandTile && c >= bs + 1 && c <= bs + bw)
+        {
+            const int code = int(tile[(r - ti0) * bw + (c - bs - 1)]);
+            const int dir  = code & 3;
+            if (dir == 2)
+                res = (uint32_t(r) << 16) | uint32_t(c - 1);
+            else if (dir != 3)
+            {
+                const int f = ra_np(a);
+                int p       = -1;
+                if (f == 0)
+                    p = 0;
+                else if (f != int(kNpEsc) && !(b >> 31))
+                {
+                    const int k      = code >> 2;
+                    const uint32_t w = k < 2 ? b : cw;
+                    p                = r - int((k & 1) ? (w >> 16) : (w & 0xffffu));
+                }
+                if (p >= 0)
+                    res = (uint32_t(p) << 16) | uint32_t(dir == 0 ? c - 1 : c);
+            }
+        }
+        return res;
+    };
     while (!(i == 0 && j == 0) && loops < bound)
     {
         i      = uniform(i);
@@ -905,10 +983,37 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
         prev_i = uniform(prev_i);
         prev_j = uniform(prev_j);
         ti0    = uniform(ti0);
+        wi0    = uniform(wi0);
+        wj0    = uniform(wj0);
         loops  = uniform(loops) + 1;
         bool found = false;
         int pi = 0, pj = 0;
-        if (i == 0)
+        if (win_ok && i >= 1 && j >= 1)
+        {
+            if (!(i <= wi0 && i > wi0 - kWinR && j <= wj0 && j > wj0 - kWinC))
+            {
+                // the tile must hold the window's rows (those >= 1)
+                if (i < ti0 || i >= ti0 + kBandTile || (i - (kWinR - 1) < ti0 && ti0 > 1))
+                    load_tile(i);
+                wi0  = i;
+                wj0  = j;
+                wpk0 = decode_cell(lane);
+                wpk1 = decode_cell(lane + kWave);
+            }
+            const int idx     = (wi0 - i) * kWinC + (wj0 - j);
+            const uint32_t nx = uint32_t(idx < kWave ? __builtin_amdgcn_readlane(int(wpk0), idx)
+                                                     : __builtin_amdgcn_readlane(int(wpk1), idx - kWave));
+            if (nx != kSlow)
+            {
+                pi    = int(nx >> 16);
+                pj    = int(nx & 0xffffu);
+                found = true;
+            }
+        }
+        if (found)
+        {
+        }
+        else if (i == 0)
         {
             const int sij = (j <= bw) ? j * gap : minv;
             const int lft = (j - 1 >= 0 && j - 1 <= bw) ? (j - 1) * gap : minv;
@@ -918,37 +1023,7 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
         else
         {
             if (i < ti0 || i >= ti0 + kBandTile)
-            {
-                const uint64_t tt0 = BandProf::now();
-                ti0 = max(1, i - (kBandTile - 1));
-                wave_sync();
-                // kBandTile rows of bw = 64*CPL code bytes: 4*CPL 16-B pieces
-                // per lane, all loads issued before the first store waits
-                constexpr int kPer    = 4 * CPL;
-                constexpr int kPerRow = 4 * CPL; // 16-B pieces per code row
-                v4i_t q[kPer];
-#pragma unroll
-                for (int u = 0; u < kPer; u++)
-                {
-                    const int t  = u * kWave + lane;
-                    const int rr = min(ti0 + t / kPerRow, V); // rows past V: never read
-                    q[u]         = *reinterpret_cast<const v4i_t*>(X.codes + size_t(rr) * bw + (t % kPerRow) * 16);
-                }
-                {
-                    const int rr = min(ti0 + lane, V); // kBandTile == kWave: one record per lane
-                    ta           = X.reca[rr];
-                    tb           = X.recb[rr];
-                    tcw          = X.recc[rr];
-                }
-#pragma unroll
-                for (int u = 0; u < kPer; u++)
-                {
-                    const int t = u * kWave + lane;
-                    *reinterpret_cast<GWAMD_LDS v4i_t*>(tile + (t / kPerRow) * bw + (t % kPerRow) * 16) = q[u];
-                }
-                wave_sync();
-                bp.add(kBpTileCyc, BandProf::now() - tt0);
-            }
+                load_tile(i);
             const uint32_t a = __builtin_amdgcn_readlane(ta, i - ti0);
             const uint32_t b = __builtin_amdgcn_readlane(tb, i - ti0);
             const uint32_t c = __builtin_amdgcn_readlane(tcw, i - ti0);
