@@ -95,7 +95,7 @@ struct BandAux
 // phase slots, see the kernel epilogue).
 struct BandProf
 {
-    uint64_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t v[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef GWAMD_BAND_PROFILE
     __device__ void add(int i, uint64_t x) { v[i] += x; }
     __device__ static uint64_t now() { return __builtin_amdgcn_s_memtime(); }
@@ -114,6 +114,8 @@ enum
     kBpTileCyc,      // traceback cycles spent staging tiles
     kBpTbCyc,        // traceback cycles
     kBpFlushCyc,     // traceback cycles in path flushes
+    kBpRefill,       // traceback move-window refills
+    kBpSlow,         // traceback steps through the general (non-window) step
 };
 
 __device__ __forceinline__ BandAux as_global(BandAux X)
@@ -985,9 +987,8 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
         ti0    = uniform(ti0);
         wi0    = uniform(wi0);
         wj0    = uniform(wj0);
-        loops  = uniform(loops) + 1;
-        bool found = false;
-        int pi = 0, pj = 0;
+        n      = uniform(n);
+        loops  = uniform(loops);
         if (win_ok && i >= 1 && j >= 1)
         {
             if (!(i <= wi0 && i > wi0 - kWinR && j <= wj0 && j > wj0 - kWinC))
@@ -999,21 +1000,47 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
                 wj0  = j;
                 wpk0 = decode_cell(lane);
                 wpk1 = decode_cell(lane + kWave);
+                bp.add(kBpRefill, 1);
             }
-            const int idx     = (wi0 - i) * kWinC + (wj0 - j);
-            const uint32_t nx = uint32_t(idx < kWave ? __builtin_amdgcn_readlane(int(wpk0), idx)
-                                                     : __builtin_amdgcn_readlane(int(wpk1), idx - kWave));
-            if (nx != kSlow)
+            // walk the window: every value here is wave-uniform (SGPRs)
+            int ci = i, cj = j, cn = n, cl = loops;
+            while (true)
             {
-                pi    = int(nx >> 16);
-                pj    = int(nx & 0xffffu);
-                found = true;
+                const int idx     = (wi0 - ci) * kWinC + (wj0 - cj);
+                const uint32_t nx = uint32_t(idx < kWave ? __builtin_amdgcn_readlane(int(wpk0), idx)
+                                                         : __builtin_amdgcn_readlane(int(wpk1), idx - kWave));
+                if (nx == kSlow)
+                    break;
+                const int pi = int(nx >> 16), pj = int(nx & 0xffffu);
+                cl++;
+                if (lane == (cn & (kWave - 1)))
+                {
+                    eg = ci == pi ? -1 : ci;
+                    er = cj == pj ? -1 : cj - 1;
+                }
+                cn++;
+                if ((cn & (kWave - 1)) == 0)
+                    flush(cn);
+                ci = pi;
+                cj = pj;
+                if ((ci == 0 && cj == 0) || cl >= bound || ci < 1 || cj < 1 || ci > wi0 ||
+                    ci <= wi0 - kWinR || cj > wj0 || cj <= wj0 - kWinC)
+                    break;
+            }
+            if (cl != loops)
+            {
+                prev_i = i = ci;
+                prev_j = j = cj;
+                n      = cn;
+                loops  = cl;
+                continue;
             }
         }
-        if (found)
-        {
-        }
-        else if (i == 0)
+        loops++;
+        bp.add(kBpSlow, 1);
+        bool found = false;
+        int pi = 0, pj = 0;
+        if (i == 0)
         {
             const int sij = (j <= bw) ? j * gap : minv;
             const int lft = (j - 1 >= 0 && j - 1 <= bw) ? (j - 1) * gap : minv;
@@ -1322,12 +1349,13 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
 #endif
 #ifdef GWAMD_BAND_PROFILE
             // counters over the phase slots (read raw: value = phase_ms * 1e5)
-            // backbone: rows, add: traceback tile cycles, topsort: flush cycles,
-            // output: forward cycles, rowprog: traceback steps, total: traceback cycles
+            // backbone: traceback general steps, add: traceback tile cycles,
+            // topsort: move-window refills, output: forward cycles, rowprog:
+            // traceback steps, total: traceback cycles
             int64_t* ph8 = b.phase + size_t(w) * kPhases;
-            ph8[kPhBackbone] = int64_t(bp.v[kBpRows]);
+            ph8[kPhBackbone] = int64_t(bp.v[kBpSlow]);
             ph8[kPhAdd]      = int64_t(bp.v[kBpTileCyc]);
-            ph8[kPhTopsort]  = int64_t(bp.v[kBpFlushCyc]);
+            ph8[kPhTopsort]  = int64_t(bp.v[kBpRefill]);
             ph8[kPhOutput]   = int64_t(bp.v[kBpFwdCyc]);
             ph8[kPhRowProg]  = int64_t(bp.v[kBpSteps]);
             ph8[kPhTotal]    = int64_t(bp.v[kBpTbCyc]);
