@@ -879,8 +879,132 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
             ar[k] = SizeT(er);
         }
     };
+    auto load_tile = [&](int ii, int cj) {
+        ti0 = max(0, ii - (kTileRows - 1));
+        tj0 = max(0, cj - (kTileCols - 16)) & ~15;
+        wave_sync();
+        // 16 loads per lane, issued 8 at a time before any is waited for
+        constexpr int kPer = kTileRows * (kTileCols / 16) / kWave;
+        constexpr int kB   = 8;
+#pragma unroll
+        for (int b0 = 0; b0 < kPer; b0 += kB)
+        {
+            uint4 v[kB];
+#pragma unroll
+            for (int u = 0; u < kB; u++)
+            {
+                const int t   = (b0 + u) * kWave + lane;
+                const int tr  = t / (kTileCols / 16);
+                const int tc  = (t % (kTileCols / 16)) * 16;
+                const int rr  = ti0 + tr;
+                const bool ok = rr <= V && tj0 + tc + 16 <= code_stride;
+                v[u] = *reinterpret_cast<const uint4*>(codes + size_t(ok ? rr : 0) * code_stride +
+                                                       (ok ? tj0 + tc : 0));
+                v[u] = ok ? v[u] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < kB; u++)
+            {
+                const int t  = (b0 + u) * kWave + lane;
+                const int tr = t / (kTileCols / 16);
+                const int tc = (t % (kTileCols / 16)) * 16;
+                *reinterpret_cast<uint4*>(tile + tr * kTileCols + tc) = v[u];
+            }
+        }
+        wave_sync();
+    };
+    // Move window (as in the banded traceback, poa_band.hip): the moves out of
+    // kWinR x kWinC cells decoded in one lane-parallel pass, two cells per
+    // lane, packed (row << 16 | column), then walked with readlane.  Cells
+    // outside the tile or with escaped predecessor lists are kSlow and take
+    // the general step.
+    constexpr int kWinR      = 16;
+    constexpr int kWinC      = 8;
+    constexpr uint32_t kSlow = 0xffffffffu;
+    const bool win_ok        = V < 65535 && L < 65535;
+    int wi0 = -1, wj0 = -1;
+    uint32_t wpk0 = kSlow, wpk1 = kSlow;
+    auto decode_cell = [&](int t) -> uint32_t {
+        const int r  = wi0 - t / kWinC;
+        const int c  = wj0 - t % kWinC;
+        const int cj = c + kColShift;
+        uint32_t res = kSlow;
+        if (r >= 1 && c >= 0 && r >= ti0 && r < ti0 + kTileRows && cj >= tj0 && cj < tj0 + kTileCols)
+        {
+            const int code     = int(tile[(r - ti0) * kTileCols + (cj - tj0)]);
+            const uint32_t rec = P.rec[r];
+            const int dir      = code & 3;
+            const int np       = int((rec >> 8) & 63);
+            const int pj       = dir == 1 ? c : c - 1;
+            if (pj < 0)
+                res = kSlow;
+            else if (dir == 2)
+                res = (uint32_t(r) << 16) | uint32_t(pj);
+            else if (np != int(kRecEscape))
+            {
+                const int p = np == 0 ? 0 : (np == 1 ? r - int(rec >> 16) : int(P.xl[(rec >> 16) + (code >> 2)]));
+                res         = (uint32_t(p) << 16) | uint32_t(pj);
+            }
+        }
+        return res;
+    };
     while (!(i == 0 && j == 0) && loops < bound)
     {
+        i     = uniform(i);
+        j     = uniform(j);
+        n     = uniform(n);
+        loops = uniform(loops);
+        ti0   = uniform(ti0);
+        tj0   = uniform(tj0);
+        wi0   = uniform(wi0);
+        wj0   = uniform(wj0);
+        if (win_ok && i >= 1)
+        {
+            if (!(i <= wi0 && i > wi0 - kWinR && j <= wj0 && j > wj0 - kWinC))
+            {
+                const int cj = j + kColShift;
+                if (i < ti0 || i >= ti0 + kTileRows || cj < tj0 || cj >= tj0 + kTileCols ||
+                    (i - (kWinR - 1) < ti0 && ti0 > 0) || (cj - (kWinC - 1) < tj0 && tj0 > 0))
+                    load_tile(i, cj);
+                wi0  = i;
+                wj0  = j;
+                wpk0 = decode_cell(lane);
+                wpk1 = decode_cell(lane + kWave);
+            }
+            // walk the window: every value here is wave-uniform (SGPRs)
+            int ci = i, cj = j, cn = n, cl = loops;
+            while (true)
+            {
+                const int idx     = (wi0 - ci) * kWinC + (wj0 - cj);
+                const uint32_t nx = uint32_t(idx < kWave ? __builtin_amdgcn_readlane(int(wpk0), idx)
+                                                         : __builtin_amdgcn_readlane(int(wpk1), idx - kWave));
+                if (nx == kSlow)
+                    break;
+                const int pi = int(nx >> 16), pj = int(nx & 0xffffu);
+                cl++;
+                if (lane == (cn & (kWave - 1)))
+                {
+                    eg = ci == pi ? -1 : ci;
+                    er = cj == pj ? -1 : cj - 1;
+                }
+                cn++;
+                if ((cn & (kWave - 1)) == 0)
+                    flush(cn);
+                ci = pi;
+                cj = pj;
+                if ((ci == 0 && cj == 0) || cl >= bound || ci < 1 || ci > wi0 || ci <= wi0 - kWinR ||
+                    cj > wj0 || cj <= wj0 - kWinC)
+                    break;
+            }
+            if (cl != loops)
+            {
+                i     = ci;
+                j     = cj;
+                n     = cn;
+                loops = cl;
+                continue;
+            }
+        }
         loops++;
         int pi, pj;
         if (i == 0)
@@ -892,40 +1016,7 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
         {
             const int cj = j + kColShift;
             if (i < ti0 || i >= ti0 + kTileRows || cj < tj0 || cj >= tj0 + kTileCols)
-            {
-                ti0 = max(0, i - (kTileRows - 1));
-                tj0 = max(0, cj - (kTileCols - 16)) & ~15;
-                wave_sync();
-                // 16 loads per lane, issued 8 at a time before any is waited for
-                constexpr int kPer = kTileRows * (kTileCols / 16) / kWave;
-                constexpr int kB   = 8;
-#pragma unroll
-                for (int b0 = 0; b0 < kPer; b0 += kB)
-                {
-                    uint4 v[kB];
-#pragma unroll
-                    for (int u = 0; u < kB; u++)
-                    {
-                        const int t   = (b0 + u) * kWave + lane;
-                        const int tr  = t / (kTileCols / 16);
-                        const int tc  = (t % (kTileCols / 16)) * 16;
-                        const int rr  = ti0 + tr;
-                        const bool ok = rr <= V && tj0 + tc + 16 <= code_stride;
-                        v[u] = *reinterpret_cast<const uint4*>(codes + size_t(ok ? rr : 0) * code_stride +
-                                                               (ok ? tj0 + tc : 0));
-                        v[u] = ok ? v[u] : make_uint4(0, 0, 0, 0);
-                    }
-#pragma unroll
-                    for (int u = 0; u < kB; u++)
-                    {
-                        const int t  = (b0 + u) * kWave + lane;
-                        const int tr = t / (kTileCols / 16);
-                        const int tc = (t % (kTileCols / 16)) * 16;
-                        *reinterpret_cast<uint4*>(tile + tr * kTileCols + tc) = v[u];
-                    }
-                }
-                wave_sync();
-            }
+                load_tile(i, cj);
             const int code_v   = int(tile[(i - ti0) * kTileCols + (cj - tj0)]);
             const int rec_v    = int(P.rec[i]);
             const int code     = uniform(code_v);
