@@ -1313,7 +1313,8 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
             if (rc == kSuccess)
             {
                 if (d.spoa_accurate)
-                    rc = topsort_racon_wave<SizeT>(g, nc, cscore, cpred, 4 * d.max_nodes, lane);
+                    rc = topsort_racon_wave<SizeT>(g, nc, cscore, cpred, 4 * d.max_nodes, lane,
+                                                   (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off);
                 else if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, (GWAMD_LDS int*)(shb),
                                              lane, tsprof))
                 {
@@ -1334,7 +1335,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
     }
 
     finish_window<SizeT, MSA>(b, d, w, lane, g, status, nseq, node_count, cscore, cpred, ecov, ecovc, seq_begin,
-                              sh_len, sh_status);
+                              sh_len, sh_status, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off);
     ph.lap<kPhOutput>();
     if (lane == 0)
     {

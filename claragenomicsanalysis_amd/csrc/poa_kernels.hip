@@ -1203,7 +1203,8 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
                 if (rc == kSuccess)
                 {
                     if (d.spoa_accurate)
-                        rc = topsort_racon_wave<SizeT>(g, nc, cscore, cpred, 4 * d.max_nodes, lane);
+                        rc = topsort_racon_wave<SizeT>(g, nc, cscore, cpred, 4 * d.max_nodes, lane,
+                                                       (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off);
                     // scratch: the read and the ring (both free after the add)
                     else if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, AX.sh, lane))
                     {
@@ -1231,7 +1232,7 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
     if (wave == 0)
     {
         finish_window<SizeT, MSA>(b, d, w, lane, g, status, nseq, node_count, cscore, cpred, ecov, ecovc, seq_begin,
-                                  sh_len, sh_status);
+                                  sh_len, sh_status, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off);
         ph.lap<kPhOutput>();
         if (lane == 0)
         {

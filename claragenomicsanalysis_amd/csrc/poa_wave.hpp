@@ -45,12 +45,19 @@ struct PhaseTimer
     }
 };
 
+template <typename SizeT>
+__device__ __forceinline__ bool topsort_racon_lds(WinGraph<SizeT> g, int n, GWAMD_LDS uint8_t* scratch,
+                                                  int scratch_bytes, int lane, SizeT* mpos = nullptr,
+                                                  int* ncols = nullptr);
+
 // Consensus and/or MSA of one finished window (cudapoa_generate_consensus.cuh:
-// 279-347, cudapoa_generate_msa.cuh:121-224).
+// 279-347, cudapoa_generate_msa.cuh:121-224).  scratch: free LDS of the
+// workgroup for the MSA's racon sort (nullptr: the lane-0 sort in HBM).
 template <typename SizeT, bool MSA>
 __device__ __forceinline__ void finish_window(const Buffers& b, const Dims& d, int w, int lane, WinGraph<SizeT> g, int status,
                               int nseq, int node_count, int32_t* cscore, SizeT* cpred, uint16_t* ecov,
-                              uint16_t* ecovc, SizeT* seq_begin, int& sh_len, int& sh_status)
+                              uint16_t* ecovc, SizeT* seq_begin, int& sh_len, int& sh_status,
+                              GWAMD_LDS uint8_t* scratch = nullptr, int scratch_bytes = 0)
 {
     g = as_global(g);
     uint8_t* cons_out = b.cons + size_t(w) * d.max_consensus;
@@ -97,11 +104,22 @@ __device__ __forceinline__ void finish_window(const Buffers& b, const Dims& d, i
     if (MSA)
     {
         uint8_t* msa_out = b.msa + size_t(w) * d.max_seqs * d.max_consensus;
+        // the racon sort and the node -> column map by the wave in LDS when the
+        // graph fits; the racon stack region (cpred) holds node -> column
+        int lds_cols        = 0;
+        const bool lds_done = graph_status == kSuccess && nseq > 0 &&
+                              topsort_racon_lds<SizeT>(g, node_count, scratch, scratch_bytes, lane, cpred, &lds_cols);
         if (lane == 0)
         {
             int msa_len = 0;
             int mst     = graph_status;
-            if (mst == kSuccess && nseq > 0)
+            if (mst == kSuccess && nseq > 0 && lds_done)
+            {
+                msa_len = lds_cols;
+                if (msa_len >= d.max_consensus)
+                    mst = kExceededMaxSeqSize;
+            }
+            else if (mst == kSuccess && nseq > 0)
             {
                 if (!topsort_racon<SizeT>(g, node_count, cscore, cpred, 4 * d.max_nodes))
                     mst = kGenericError;
@@ -463,12 +481,130 @@ __device__ __forceinline__ int add_alignment_parallel(WinGraph<SizeT> g, int& no
     return kSuccess;
 }
 
-// SPOA_ACCURATE per-read sort (cudapoa_kernels.cuh:324-337): the racon DFS on
-// lane 0 of the window's wave; returns the window status for every lane.
+// racon/SPOA DFS sort (cudapoa_topsort.cuh:94-189) by one wave with the node
+// marks and the DFS stack in LDS: the predecessor and aligned-node lists of
+// the node on top of the stack are read one entry per lane, and the entries to
+// visit are pushed in list order with a ballot (in-edges first, then aligned
+// nodes, as the sequential loop does).  With mpos it also writes the MSA column
+// of every node (getNodeIDToMSAPosDevice, cudapoa_generate_msa.cuh:27-45: one
+// column per emitted node and its aligned nodes) and the column count to
+// *ncols.  Returns false when the marks and a useful stack do not fit in the
+// scratch, or when the stack outgrows it (after a partial sort): the caller
+// then runs topsort_racon, which rewrites everything.
+template <typename SizeT>
+__device__ __forceinline__ bool topsort_racon_lds(WinGraph<SizeT> g, int n, GWAMD_LDS uint8_t* scratch,
+                                                  int scratch_bytes, int lane, SizeT* mpos, int* ncols)
+{
+    g = as_global(g);
+    n                 = uniform(n);
+    const int marks_b = (n + 15) & ~15;
+    const int cap     = scratch_bytes > marks_b ? (scratch_bytes - marks_b) / 2 : 0;
+    if (scratch == nullptr || n <= 0 || n > 65535 || cap < 4 * kWave)
+        return false;
+    GWAMD_LDS uint8_t* marks  = scratch;
+    GWAMD_LDS uint16_t* stack = (GWAMD_LDS uint16_t*)(scratch + marks_b);
+    for (int v = lane; v < n; v += kWave)
+        marks[v] = 4; // mark 0, check_aligned_nodes = true
+    wave_sync();
+    int k = 0, col = 0;
+    for (int v0 = 0; v0 < n; v0++)
+    {
+        if ((uniform(int(marks[v0])) & 3) != 0)
+            continue;
+        int top = 0, id = v0;
+        if (lane == 0)
+            stack[0] = uint16_t(v0);
+        while (top >= 0)
+        {
+            top         = uniform(top);
+            id          = uniform(id);
+            k           = uniform(k);
+            col         = uniform(col);
+            const int m = uniform(int(marks[id]));
+            bool valid  = true;
+            if ((m & 3) != 2)
+            {
+                const int ic      = uniform(int(g.in_cnt[id]));
+                const int ac      = (m & 4) ? uniform(int(g.aln_cnt[id])) : 0;
+                const int bl      = lane < ic ? int(g.in_e[id * kMaxEdges + lane]) : 0;
+                const int al      = lane < ac ? int(g.aln[id * kMaxAlignments + lane]) : 0;
+                const int mb      = lane < ic ? int(marks[bl]) : 2;
+                const int ma      = lane < ac ? int(marks[al]) : 2;
+                const bool nb     = lane < ic && (mb & 3) != 2;
+                const bool na     = lane < ac && (ma & 3) != 2;
+                const uint64_t bb = __builtin_amdgcn_ballot_w64(nb);
+                const uint64_t ba = __builtin_amdgcn_ballot_w64(na);
+                const int cb = __popcll(bb), ca = __popcll(ba);
+                if (cb + ca > 0)
+                {
+                    if (top + cb + ca >= cap)
+                        return false;
+                    const uint64_t below = (uint64_t(1) << lane) - 1;
+                    if (nb)
+                        stack[top + 1 + __popcll(bb & below)] = uint16_t(bl);
+                    if (na)
+                    {
+                        stack[top + 1 + cb + __popcll(ba & below)] = uint16_t(al);
+                        marks[al] = uint8_t(ma & 3); // check_aligned_nodes = false
+                    }
+                    if (lane == 0)
+                        marks[id] = uint8_t((m & 4) | 1);
+                    valid = false;
+                    // the last entry pushed is the new top
+                    id = ca > 0 ? __builtin_amdgcn_readlane(al, 63 - __builtin_clzll(ba))
+                                : __builtin_amdgcn_readlane(bl, 63 - __builtin_clzll(bb));
+                    top += cb + ca;
+                }
+                else
+                {
+                    if (m & 4)
+                    {
+                        // emit the node, then all its aligned nodes
+                        if (lane == 0)
+                        {
+                            g.sorted[k] = SizeT(id);
+                            g.pos[id]   = SizeT(k);
+                            if (mpos)
+                                mpos[id] = SizeT(col);
+                        }
+                        if (lane < ac)
+                        {
+                            g.sorted[k + 1 + lane] = SizeT(al);
+                            g.pos[al]              = SizeT(k + 1 + lane);
+                            if (mpos)
+                                mpos[al] = SizeT(col);
+                        }
+                        k += 1 + ac;
+                        col++;
+                    }
+                    if (lane == 0)
+                        marks[id] = uint8_t((m & 4) | 2);
+                }
+            }
+            if (valid)
+            {
+                top--;
+                if (top >= 0)
+                    id = uniform(int(stack[top]));
+            }
+            wave_sync();
+        }
+    }
+    if (ncols)
+        *ncols = col;
+    return true;
+}
+
+// SPOA_ACCURATE per-read sort (cudapoa_kernels.cuh:324-337): the LDS racon
+// sort when it fits in scratch, else the racon DFS on lane 0; returns the
+// window status for every lane.
 template <typename SizeT>
 __device__ __forceinline__ int topsort_racon_wave(WinGraph<SizeT> g, int n, int32_t* marks, SizeT* stack, int cap,
-                                                  int lane)
+                                                  int lane, GWAMD_LDS uint8_t* scratch = nullptr,
+                                                  int scratch_bytes = 0)
 {
+    if (topsort_racon_lds<SizeT>(g, n, scratch, scratch_bytes, lane))
+        return int(kSuccess);
     int ok = 1;
     if (lane == 0)
         ok = topsort_racon<SizeT>(g, n, marks, stack, cap) ? 1 : 0;
