@@ -1206,7 +1206,8 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
                         rc = topsort_racon_wave<SizeT>(g, nc, cscore, cpred, 4 * d.max_nodes, lane,
                                                        (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off);
                     // scratch: the read and the ring (both free after the add)
-                    else if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, AX.sh, lane))
+                    else if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, AX.sh, lane) &&
+                             !topsort_lds_big<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, lane))
                     {
                         if (lane == 0)
                             topsort_kahn<SizeT>(g, nc, cscore);

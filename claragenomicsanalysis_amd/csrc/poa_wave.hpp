@@ -798,5 +798,67 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
     return true;
 }
 
+// Kahn sort for graphs whose node words do not fit LDS (config C): only the
+// remaining in-degrees (one byte per node) and the FIFO (u16) live in LDS,
+// 3 bytes per node; the out-edge list of each popped node is read from HBM,
+// all slots in one lane-parallel load issued with its count.  Same order as
+// topsort_lds (successors released in slot order).  Returns false (nothing
+// written) when it does not fit either.
+template <typename SizeT>
+__device__ __forceinline__ bool topsort_lds_big(WinGraph<SizeT> g, int n, GWAMD_LDS uint8_t* scratch,
+                                                int scratch_bytes, int lane)
+{
+    g = as_global(g);
+    n               = uniform(n);
+    const int cnt_b = (n + 15) & ~15;
+    if (scratch == nullptr || n <= 0 || n > 65535 || cnt_b + 2 * n > scratch_bytes)
+        return false;
+    GWAMD_LDS uint8_t* cnt    = scratch;
+    GWAMD_LDS uint16_t* queue = (GWAMD_LDS uint16_t*)(scratch + cnt_b);
+    // in-degrees and the sources in id order
+    int k = 0;
+    for (int v0 = 0; v0 < n; v0 += kWave)
+    {
+        const int v    = v0 + lane;
+        const int ic   = v < n ? int(g.in_cnt[v]) : 1;
+        if (v < n)
+            cnt[v] = uint8_t(ic);
+        const bool src = ic == 0;
+        int total      = 0;
+        const int ex   = wave_excl_sum(src ? 1 : 0, lane, total);
+        if (src)
+            queue[k + ex] = uint16_t(v);
+        k += total;
+    }
+    wave_sync();
+    int tail = uniform(k);
+    for (int q = 0; q < tail; q++)
+    {
+        q                 = uniform(q);
+        tail              = uniform(tail);
+        const int v       = uniform(int(queue[q]));
+        const int ov      = lane < kMaxEdges ? int(g.out_e[v * kMaxEdges + lane]) : 0;
+        const int oc      = uniform(int(g.out_cnt[v]));
+        const bool act    = lane < oc;
+        const int c       = act ? int(cnt[ov]) - 1 : 1;
+        if (act)
+            cnt[ov] = uint8_t(c);
+        const bool rdy       = act && c == 0;
+        const uint64_t ready = __builtin_amdgcn_ballot_w64(rdy);
+        if (rdy)
+            queue[tail + __popcll(ready & ((uint64_t(1) << lane) - 1))] = uint16_t(ov);
+        tail += __popcll(ready);
+    }
+    wave_sync();
+    for (int q = lane; q < tail; q += kWave)
+    {
+        const int v = int(queue[q]);
+        g.sorted[q] = SizeT(v);
+        g.pos[v]    = SizeT(q);
+    }
+    wave_sync();
+    return true;
+}
+
 } // namespace poa
 } // namespace gwamd
