@@ -325,3 +325,23 @@ def test_spoa_accurate(variant, banded, out, monkeypatch):
         assert (st[i], got[i]) == (r.status, want), i
         differ += (k.msa if out == "msa" else (k.consensus, k.coverage)) != want
     assert differ > 0
+
+
+@pytest.mark.parametrize("banded", [False, True])
+def test_serialize_graph_case(banded):
+    # Test_CudapoaSerializeGraph.cpp:58-90: 500 reads generated from a 50 bp
+    # backbone with minstd_rand(1) (10 / 5 / 10 mutations), MSA output,
+    # BatchSize(1024, 500); the final graph equals the oracle's, edge weights
+    # included, and serialises to one DOT line per node label and per edge
+    wins = synth.poa_windows(1, 1, 50, 500, 10, 5, 10)
+    b = run_gpu(wins, 1024, 500, banded=banded, bw=256, output_type="msa")
+    graphs, st = b.get_graphs()
+    r = run_oracle(wins[0], 1024, 500, banded=banded, bw=256, msa=True, want_graph=True)
+    assert st == [r.status] == [0]
+    g = graphs[0]
+    expect = {(src, v): wt for v, ins in enumerate(r.graph["in"]) for (src, wt) in ins}
+    assert {(u, v): g.weight(u, v) for (u, v) in g.edges} == expect
+    assert "".join(g.label(v) for v in range(r.final_nodes)) == r.graph["bases"]
+    msa, mst = b.get_msa()
+    assert (mst[0], msa[0]) == (r.status, oracle.poa_window(wins[0], banded=banded, msa=True, max_nodes=(4 if banded else 3) * 1024,
+                                                            max_consensus=2048, max_seqs=500).msa)

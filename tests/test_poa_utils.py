@@ -92,3 +92,29 @@ def test_parse_fasta_files(tmp_path):
     b = tmp_path / "b.fa"
     b.write_text(">x\nTTTT\n")
     assert cudapoa.parse_fasta_files([str(a), str(b)]) == [["ACGTAC", "GGG"], ["TTTT"]]
+
+
+@pytest.mark.gpu
+def test_multi_batch_sizes_on_device_and_batches_run():
+    # free device memory queried (hipMemGetInfo, utils.cu:40-44); every group
+    # lands in exactly one batch, and a batch created with its size takes its
+    # groups and runs.  As in the reference, a merged bin keeps the batch size
+    # of its own largest group (utils.cu:111-130), so a group merged from
+    # another bin may bring more reads than max_sequences_per_poa: those reads
+    # get exceeded_maximum_sequences_per_poa (3) and are dropped
+    from claragenomicsanalysis_amd import synth
+    from claragenomicsanalysis_amd.cudapoa import CudaPoaBatch
+    groups = synth.poa_windows(5, 6, 300, 6, 15, 15, 15) + synth.poa_windows(9, 4, 1500, 4, 60, 60, 60)
+    sizes, per_batch = cudapoa.get_multi_batch_sizes(groups, gpu_memory_usage_quota=0.5)
+    assert sorted(i for b in per_batch for i in b) == list(range(len(groups)))
+    for (max_seq, max_reads), ids in zip(sizes, per_batch):
+        if not ids:
+            continue
+        b = CudaPoaBatch(max_reads, max_seq, 2 << 30, cuda_banded_alignment=True)
+        for i in ids:
+            st, seq_st = b.add_poa_group(list(groups[i]))
+            assert st == 0
+            assert seq_st == [0 if k < max_reads else 3 for k in range(len(groups[i]))]
+        b.generate_poa()
+        _, _, st = b.get_consensus()
+        assert all(s == 0 for s in st)
