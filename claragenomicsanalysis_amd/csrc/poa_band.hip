@@ -95,7 +95,7 @@ struct BandAux
 // phase slots, see the kernel epilogue).
 struct BandProf
 {
-    uint64_t v[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t v[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef GWAMD_BAND_PROFILE
     __device__ void add(int i, uint64_t x) { v[i] += x; }
     __device__ static uint64_t now() { return __builtin_amdgcn_s_memtime(); }
@@ -116,6 +116,7 @@ enum
     kBpFlushCyc,     // traceback cycles in path flushes
     kBpRefill,       // traceback move-window refills
     kBpSlow,         // traceback steps through the general (non-window) step
+    kBpAddSeq,       // reads added by the sequential add (parallel add declined)
 };
 
 __device__ __forceinline__ BandAux as_global(BandAux X)
@@ -1297,6 +1298,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
             }
             if (rc < 0)
             {
+                bp.add(kBpAddSeq, 1);
                 if (lane == 0)
                 {
                     sh_status = add_alignment<SizeT, MSA>(g, nc, ag, ar, alen, read_g, wts_g, s, ecov, ecovc,
@@ -1351,12 +1353,12 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
 #endif
 #ifdef GWAMD_BAND_PROFILE
             // counters over the phase slots (read raw: value = phase_ms * 1e5)
-            // backbone: traceback general steps, add: traceback tile cycles,
+            // backbone: traceback general steps, add: reads added sequentially,
             // topsort: move-window refills, output: forward cycles, rowprog:
             // traceback steps, total: traceback cycles
             int64_t* ph8 = b.phase + size_t(w) * kPhases;
             ph8[kPhBackbone] = int64_t(bp.v[kBpSlow]);
-            ph8[kPhAdd]      = int64_t(bp.v[kBpTileCyc]);
+            ph8[kPhAdd]      = int64_t(bp.v[kBpAddSeq]);
             ph8[kPhTopsort]  = int64_t(bp.v[kBpRefill]);
             ph8[kPhOutput]   = int64_t(bp.v[kBpFwdCyc]);
             ph8[kPhRowProg]  = int64_t(bp.v[kBpSteps]);

@@ -56,3 +56,48 @@ def gather_consensus(strings, width, device=None):
     for p in parts:
         out.extend(unpack_strings(p.cpu().numpy()))
     return out
+
+
+def window_cost(group):
+    """DP cells of a window up to a constant: (reads - 1) x (longest read)^2
+    (each read is aligned to a graph about as long as the reads)."""
+    lens = [len(r) for r in group]
+    if len(lens) < 2:
+        return 0
+    m = max(lens)
+    return (len(lens) - 1) * m * m
+
+
+def shard_windows(groups, world_size):
+    """Window indices per rank for real (uneven) data, SURVEY.md 8(e): the
+    windows are ordered by cost and dealt in snake order (0..N-1, N-1..0, ...),
+    so every rank gets a similar number of windows and of DP cells.  The
+    reference balances nothing across devices (main.cu:491-513 hands out
+    whole batches); this is the per-rank analogue of get_multi_batch_sizes'
+    size binning (utils.cu:24-138).  Each rank's list is ascending."""
+    if world_size < 1:
+        raise ValueError("world_size must be at least 1")
+    order = sorted(range(len(groups)), key=lambda i: (-window_cost(groups[i]), i))
+    shards = [[] for _ in range(world_size)]
+    for k, i in enumerate(order):
+        cyc, pos = divmod(k, world_size)
+        shards[pos if cyc % 2 == 0 else world_size - 1 - pos].append(i)
+    return [sorted(s) for s in shards]
+
+
+def gather_sharded(strings, shards, width, device=None):
+    """Gather every rank's strings (one per window of its shard, in shard
+    order) to rank 0 and return them in the original window order; other
+    ranks get None.  Shards may differ in size by one window."""
+    n = max(len(s) for s in shards)
+    rank = dist.get_rank()
+    if len(strings) != len(shards[rank]):
+        raise ValueError("rank %d passes %d strings for %d windows" % (rank, len(strings), len(shards[rank])))
+    got = gather_consensus(list(strings) + [""] * (n - len(strings)), width, device)
+    if got is None:
+        return None
+    out = [None] * sum(len(s) for s in shards)
+    for r, s in enumerate(shards):
+        for j, idx in enumerate(s):
+            out[idx] = got[r * n + j]
+    return out

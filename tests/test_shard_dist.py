@@ -57,3 +57,45 @@ def test_gather_world2_gloo():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert got == ["W%d_%s" % (s, "ACGT" * s) for s in range(1, 11)]
+
+
+def test_shard_windows_balance_and_cover():
+    import random
+    rng = random.Random(3)
+    groups = [["A" * rng.randint(100, 12000)] * rng.randint(2, 40) for _ in range(997)]
+    for world in (1, 2, 3, 8):
+        shards = shard.shard_windows(groups, world)
+        flat = sorted(i for s in shards for i in s)
+        assert flat == list(range(len(groups)))
+        counts = [len(s) for s in shards]
+        assert max(counts) - min(counts) <= 1
+        cost = [sum(shard.window_cost(groups[i]) for i in s) for s in shards]
+        assert max(cost) <= 1.05 * min(cost)
+    assert shard.shard_windows([], 4) == [[], [], [], []]
+
+
+def _sharded_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    groups = [["ACGT" * (i % 5 + 1)] * (i % 3 + 2) for i in range(7)]
+    shards = shard.shard_windows(groups, world)
+    mine = ["C%d" % i for i in shards[rank]]  # stand-in for this rank's consensus strings
+    got = shard.gather_sharded(mine, shards, 16)
+    if rank == 0:
+        out.put(got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_sharded_restores_window_order():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert got == ["C%d" % i for i in range(7)]
