@@ -174,6 +174,28 @@ def bench_aligner(args):
             got = paths[i, :plen[i]][::-1].tolist()
             ok = ok and got == want
         parity = {"pairs_checked": k, "bit_exact_vs_oracle": bool(ok)}
+        # size-independent check over every pair of the workload: a global
+        # alignment consumes the whole query (match/mismatch + deletion, i.e.
+        # present in query) and the whole target (match/mismatch + insertion,
+        # present in target; cudaaligner.hpp:46-52)
+        R = paths.shape[1]
+        live = np.arange(R)[None, :] < plen[:, None]
+        mm = (((paths == 0) | (paths == 1)) & live).sum(1)
+        full_ok = bool(np.all(mm + ((paths == 3) & live).sum(1) == np.array([len(q) for q in qs])) and
+                       np.all(mm + ((paths == 2) & live).sum(1) == np.array([len(t) for t in ts])))
+        parity["all_pairs_consume_query_and_target"] = full_ok
+        # and on the first 1000 pairs: match states join equal bases, mismatch states differing ones
+        kb = min(1000, n)
+        bases_ok = True
+        for i in range(kb):
+            p = paths[i, :plen[i]][::-1]
+            qi = np.cumsum((p == 0) | (p == 1) | (p == 3)) - 1
+            ti = np.cumsum((p == 0) | (p == 1) | (p == 2)) - 1
+            qb = np.frombuffer(qs[i] if isinstance(qs[i], bytes) else qs[i].encode(), np.uint8)
+            tb = np.frombuffer(ts[i] if isinstance(ts[i], bytes) else ts[i].encode(), np.uint8)
+            m, x = p == 0, p == 1
+            bases_ok = bases_ok and bool(np.all(qb[qi[m]] == tb[ti[m]]) and np.all(qb[qi[x]] != tb[ti[x]]))
+        parity["pairs_match_states_on_equal_bases"] = {"pairs": kb, "ok": bases_ok}
         cpu = None
         if not args.no_cpu and world == 1:
             th = cpu_threads()
@@ -345,6 +367,16 @@ def main():
             else:
                 ok = ok and (r.status == status[i] and r.consensus == cons[i] and r.coverage == cov[i])
         parity = {"windows_checked": k, "bit_exact_vs_oracle": bool(ok)}
+        # size-independent checks over every window of the workload
+        parity["all_windows_status_ok"] = n_ok == nwin
+        if msa:
+            # MSA rows de-gapped are the window's reads (Test_CudapoaGenerateMSA2.cu:125-140)
+            parity["all_msa_rows_degap_to_reads"] = bool(all(
+                [row.replace("-", "") for row in msa_rows[i]] ==
+                [r.decode() if isinstance(r, bytes) else r for r in windows[i]] for i in range(nwin)))
+        else:
+            parity["all_coverage_lengths_match"] = bool(all(len(cov[i]) == len(cons[i]) and len(cons[i]) > 0
+                                                            for i in range(nwin)))
         if not args.no_cpu and world == 1:
             th = cpu_threads()
             ns = args.cpu_sample or min(nwin, max(th * (2 if msa else 48), 64 if not msa else 16))
