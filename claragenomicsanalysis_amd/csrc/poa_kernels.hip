@@ -597,12 +597,16 @@ __device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, con
             int16_t* row       = ring + (r & mask) * ring_stride;
             const bool anyfar  = __builtin_amdgcn_ballot_w64(lane < np && pv != 0 && r - pv > mask) != 0;
             uint32_t sig[NR];
-            if (base == 'A' || base == 'C' || base == 'G' || base == 'T')
+            // 'A' 'C' 'G' 'T' are bits 1, 3, 7, 20 of 0x40..0x7f; (base >> 1) & 3
+            // gives A 0, C 1, T 2, G 3 (branch-free, a few scalar ops)
+            const uint32_t ub = uint32_t(base);
+            if ((ub & 0xc0u) == 0x40u && ((0x10008aull >> (ub & 0x3fu)) & 1u))
             {
                 // bitwise selects (a select between the profile arrays would
                 // index them dynamically, i.e. through scratch)
-                const uint32_t m1 = opaque_u32((base == 'C' || base == 'T') ? ~0u : 0u);
-                const uint32_t m2 = opaque_u32((base == 'G' || base == 'T') ? ~0u : 0u);
+                const uint32_t bcode = (ub >> 1) & 3u;
+                const uint32_t m1    = opaque_u32(((bcode ^ (bcode >> 1)) & 1u) ? ~0u : 0u); // C or T
+                const uint32_t m2    = opaque_u32((bcode >> 1) ? ~0u : 0u);                  // G or T
 #pragma unroll
                 for (int i = 0; i < NR; i++)
                 {
