@@ -1167,7 +1167,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
     __shared__ int sh_status;
     __shared__ int sh_len;
 
-    const int w = blockIdx.x;
+    const int w = b.order ? b.order[blockIdx.x] : int(blockIdx.x);
     if (w >= b.num_windows)
         return;
     const int lane = threadIdx.x;

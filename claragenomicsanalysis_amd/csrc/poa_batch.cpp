@@ -215,6 +215,51 @@ public:
         GWAMD_HIP_CHECK(hipMemcpyAsync(d_win_.p, h_win_.as<gwamd::poa::WindowDesc>(),
                                        size_t(poa_count_) * sizeof(gwamd::poa::WindowDesc), hipMemcpyHostToDevice,
                                        stream_));
+        plan_launch_order();
+    }
+
+    // Workgroup -> window order.  Workgroups i, i + C, i + 2C, ... (C = CUs)
+    // share a CU when a batch holds more windows than CUs; windows are
+    // ranked by estimated DP cells and dealt to those rounds in snake order,
+    // so every CU gets a mix of heavy and light windows and the batch does
+    // not wait on a CU full of heavy ones.  Outputs stay indexed by window.
+    void plan_launch_order()
+    {
+        bufs_.order = nullptr;
+        int cus     = 0;
+        GWAMD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
+        const int n = poa_count_;
+        if (cus <= 0 || n <= cus)
+            return;
+        const auto* wd = h_win_.as<gwamd::poa::WindowDesc>();
+        const auto* ln = h_len_.as<int32_t>();
+        std::vector<std::pair<int64_t, int32_t>> cost(static_cast<size_t>(n));
+        for (int w = 0; w < n; w++)
+        {
+            int64_t sum = 0, mx = 0;
+            for (int s = 0; s < wd[w].num_seqs; s++)
+            {
+                const int64_t l = ln[wd[w].first_seq + s];
+                mx              = std::max(mx, l);
+                if (s > 0)
+                    sum += l;
+            }
+            cost[size_t(w)] = {-sum * mx, w}; // heaviest first, ties by window
+        }
+        std::sort(cost.begin(), cost.end());
+        h_order_.assign(static_cast<size_t>(n), 0);
+        for (int k = 0; k < n; k++)
+        {
+            const int t = k / cus, pos = k % cus;
+            const int m = std::min(cus, n - t * cus); // workgroups in this round
+            const int j = (t % 2 == 0) ? pos : m - 1 - pos;
+            h_order_[size_t(t * cus + j)] = cost[size_t(k)].second;
+        }
+        int32_t* d_order = reinterpret_cast<int32_t*>(static_cast<uint8_t*>(d_win_.p) +
+                                                      ((size_t(max_poas_) * sizeof(gwamd::poa::WindowDesc) + 15) & ~size_t(15)));
+        GWAMD_HIP_CHECK(hipMemcpyAsync(d_order, h_order_.data(), size_t(n) * 4, hipMemcpyHostToDevice, stream_));
+        GWAMD_HIP_CHECK(hipStreamSynchronize(stream_)); // h_order_ is pageable
+        bufs_.order = d_order;
     }
 
     void launch()
@@ -702,7 +747,7 @@ private:
         d_wts_.n               = size_t(in_bytes);
         d_len_.n               = size_t(P * S * 4 + 8);
         d_off_.n               = size_t(P * S * 8 + 8);
-        d_win_.n               = size_t(P * sizeof(gwamd::poa::WindowDesc) + 8);
+        d_win_.n               = size_t(P * (sizeof(gwamd::poa::WindowDesc) + 4) + 16);
         for (auto* b : {&d_seqs_, &d_wts_, &d_len_, &d_off_, &d_win_})
             GWAMD_HIP_CHECK(hipMalloc(&b->p, b->n));
         bufs_.seqs    = static_cast<const uint8_t*>(d_seqs_.p);
@@ -803,6 +848,7 @@ private:
     bool generated_     = false;
     int32_t bid_        = 0;
     gwamd::poa::Dims dims_{};
+    std::vector<int32_t> h_order_; // workgroup -> window (plan_launch_order)
     gwamd::poa::Buffers bufs_{};
     DevBuf d_seqs_, d_wts_, d_len_, d_off_, d_win_, d_slab_, d_codes_;
     PinnedBuf h_seqs_, h_wts_, h_len_, h_off_, h_win_;

@@ -114,6 +114,7 @@ struct Buffers
     const int32_t* seq_len;
     const int64_t* seq_off;
     const WindowDesc* windows;
+    const int32_t* order; // window of each workgroup (nullptr: workgroup i runs window i)
     int32_t num_windows;
     // graph scratch
     uint8_t* base;

@@ -34,7 +34,7 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel(Buffers b, Dims d, Sc
     __shared__ int sh_status;
     __shared__ int sh_len;
 
-    const int w = blockIdx.x;
+    const int w = b.order ? b.order[blockIdx.x] : int(blockIdx.x);
     if (w >= b.num_windows)
         return;
     const int lane = threadIdx.x;
@@ -1068,7 +1068,7 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
     __shared__ int sh_status;
     __shared__ int sh_len;
 
-    const int w = blockIdx.x;
+    const int w = b.order ? b.order[blockIdx.x] : int(blockIdx.x);
     if (w >= b.num_windows)
         return;
     const int tid      = threadIdx.x;
