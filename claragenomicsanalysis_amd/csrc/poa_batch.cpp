@@ -247,18 +247,19 @@ public:
             cost[size_t(w)] = {-sum * mx, w}; // heaviest first, ties by window
         }
         std::sort(cost.begin(), cost.end());
-        h_order_.assign(static_cast<size_t>(n), 0);
+        // pinned, so the copy stays asynchronous (generate_poa does not block)
+        h_order_.reserve(size_t(n) * 4, stream_);
+        int32_t* order = h_order_.as<int32_t>();
         for (int k = 0; k < n; k++)
         {
             const int t = k / cus, pos = k % cus;
             const int m = std::min(cus, n - t * cus); // workgroups in this round
             const int j = (t % 2 == 0) ? pos : m - 1 - pos;
-            h_order_[size_t(t * cus + j)] = cost[size_t(k)].second;
+            order[t * cus + j] = cost[size_t(k)].second;
         }
         int32_t* d_order = reinterpret_cast<int32_t*>(static_cast<uint8_t*>(d_win_.p) +
                                                       ((size_t(max_poas_) * sizeof(gwamd::poa::WindowDesc) + 15) & ~size_t(15)));
-        GWAMD_HIP_CHECK(hipMemcpyAsync(d_order, h_order_.data(), size_t(n) * 4, hipMemcpyHostToDevice, stream_));
-        GWAMD_HIP_CHECK(hipStreamSynchronize(stream_)); // h_order_ is pageable
+        GWAMD_HIP_CHECK(hipMemcpyAsync(d_order, order, size_t(n) * 4, hipMemcpyHostToDevice, stream_));
         bufs_.order = d_order;
     }
 
@@ -848,7 +849,7 @@ private:
     bool generated_     = false;
     int32_t bid_        = 0;
     gwamd::poa::Dims dims_{};
-    std::vector<int32_t> h_order_; // workgroup -> window (plan_launch_order)
+    PinnedBuf h_order_; // workgroup -> window (plan_launch_order)
     gwamd::poa::Buffers bufs_{};
     DevBuf d_seqs_, d_wts_, d_len_, d_off_, d_win_, d_slab_, d_codes_;
     PinnedBuf h_seqs_, h_wts_, h_len_, h_off_, h_win_;
