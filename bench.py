@@ -1,15 +1,25 @@
-"""Benchmark: POA consensus windows/s on MI355X (BASELINE.json configs[1], "B").
+"""Benchmark: POA consensus windows/s and global alignments/s on MI355X
+(BASELINE.json metric).
 
-Workload: 1024 windows per GPU; window w uses
-std::minstd_rand(seed w) -> 1000-base backbone + 31 mutated copies
-(generate_random_sequences(bb, 32, rng, 50, 50, 50)), BatchSize(1100, 32),
-full alignment, scores -8/-6/8, int16 scores.  A step is one pass of the POA
-kernel over the whole resident batch (graph build + NW + add + topsort +
-consensus for every window).  Inputs are uploaded before timing.
+Default (`python bench.py`, one GPU): config B, the reference's single-batch
+benchmark unit (cudapoa/benchmarks/main.cpp:30-39, single_batch.hpp:82-89): one
+step is generate_poa() (H2D of the packed reads + the POA kernel) followed by
+get_consensus() (D2H + the per-window result vectors) on a batch of 1024
+windows x 32 reads x ~1 kb (std::minstd_rand(seed w) generators,
+BatchSize(1100, 32), full alignment, -8/-6/8, int16 scores); windows are added
+outside the timed region, as the reference's PauseTiming does.  The same line
+carries `secondary` objects for config D (cudaaligner global alignment,
+align_all() + sync_alignments() on 100k pairs x 5 kb) and config E (the
+multi-batch streaming driver on one GPU's share of the 1M-window job).
 
-N GPUs: one process per GPU (torch.distributed, RCCL), each rank runs its own
-1024 windows (weak scaling); the consensus strings are gathered to rank 0 over
-RCCL once after the timed region.
+Config E (`--config E`, and the default when WORLD_SIZE > 1): the reference's
+multi-batch benchmark unit (multi_batch.hpp:64-171, BM_MultiBatchTest): windows
+stream through concurrent batches on separate HIP streams fed by host threads
+(fill + H2D + kernel + D2H all timed).  A step is E_STEP_WINDOWS windows; the K
+timed steps of rank r are its K x 6250 windows, seeds 1 + r*K*6250 ..., streamed
+by one process_batches call (K = 20: 125k windows per GPU, the 1M-window job
+on 8 GPUs).  Weak scaling; one process per GPU; no collective inside the timed
+region; after it, rank 0 gathers every rank's consensus over RCCL.
 
 Prints one JSON line (rank 0) with roofline and cpu_baseline objects.
 """
@@ -27,6 +37,7 @@ import torch  # noqa: E402  (import before libgwamd so both share one HIP runtim
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+E_STEP_WINDOWS = 6250   # config E: windows per step (20 steps = 125k windows per GPU)
 
 ALIGNER_CONFIGS = {
     # 100k pairs x 5 kb, ~10% difference; Hirschberg-Myers
@@ -45,6 +56,17 @@ ALIGNER_ALGOS = {
     "myers_banded": (2, "myers_banded_kernel"),
     "ukkonen": (3, "ukkonen_kernel"),
 }
+
+CONFIGS = {
+    "B": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=False, bw=256, windows=1024),
+    "B_banded": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=True, bw=256, windows=1024),
+    # SURVEY.md 8(d) config C: MSA mode, 10 kb windows x 16 reads, banded bw 256,
+    # BatchSize(10600, 16, 256) -> int32 scores and node ids
+    "C": dict(backbone=10000, reads=16, err=500, max_seq=10600, banded=True, bw=256, windows=128, msa=True,
+              mem_per_window=400e6),
+}
+# the config-B generator, seeds 1..1e6, 125k per GPU
+STREAM_CONFIGS = {"E": dict(CONFIGS["B"], windows_per_step=E_STEP_WINDOWS)}
 
 
 def aligner_alg_bytes(algorithm, q, t):
@@ -68,37 +90,54 @@ def aligner_alg_bytes(algorithm, q, t):
     # full Myers state: ceil(q/32) words x (t+1) columns x 12 B
     return ((Q + 31) // 32) * (T + 1) * 12
 
-CONFIGS = {
-    # name: (backbone, reads, mut, ins, del, max_seq, banded, band_width, windows per GPU)
-    "B": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=False, bw=256, windows=1024),
-    "B_banded": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=True, bw=256, windows=1024),
-    # SURVEY.md 8(d) config C: MSA mode, 10 kb windows x 16 reads, banded bw 256,
-    # BatchSize(10600, 16, 256) -> int32 scores and node ids
-    "C": dict(backbone=10000, reads=16, err=500, max_seq=10600, banded=True, bw=256, windows=128, msa=True,
-              mem_per_window=400e6),
-}
-
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--config", default="B", choices=sorted(CONFIGS) + sorted(ALIGNER_CONFIGS))
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default=None,
+                   choices=sorted(CONFIGS) + sorted(ALIGNER_CONFIGS) + sorted(STREAM_CONFIGS),
+                   help="default: B on one GPU (with D and E as secondary objects), E when WORLD_SIZE > 1")
     p.add_argument("--pairs", type=int, default=None, help="override aligner pairs per GPU")
-    p.add_argument("--windows", type=int, default=None, help="override windows per GPU")
-    p.add_argument("--cpu-sample", type=int, default=None, help="windows in the CPU baseline sample")
+    p.add_argument("--windows", type=int, default=None, help="override windows per GPU (B, C)")
+    p.add_argument("--cpu-sample", type=int, default=None, help="windows / pairs in the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-secondary", action="store_true", help="default run: skip the D and E objects")
+    p.add_argument("--secondary-steps", type=int, default=3, help="timed steps of the D object")
+    p.add_argument("--stream-batches", type=int, default=2, help="E: concurrent batches (streams + host threads)")
+    p.add_argument("--stream-batch-windows", type=int, default=4096, help="E: windows per batch")
     p.add_argument("--traffic-file", default=None,
                    help="PMC HBM bytes per launch (default profiles/traffic_poa_<config>.json)")
     return p.parse_args()
 
 
+def affinity_cpus():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def cpu_threads():
-    v = os.environ.get("OMP_NUM_THREADS")
-    if v and v.isdigit() and int(v) > 0:
-        return int(v)
-    return os.cpu_count() or 1
+    """Host CPUs this process can use: the CPUs it may run on
+    (sched_getaffinity), capped by the cgroup's CPU-time quota (cpu.max) when
+    one is set -- more threads than the quota only time-slice the same CPU
+    time.  The CPU baseline runs on all of them."""
+    n = affinity_cpus()
+    q = cgroup_cpu_quota()
+    if q:
+        n = max(1, min(n, int(q)))
+    return n
+
+
+def cgroup_cpu_quota():
+    """CPUs' worth of time the cgroup grants (None: unlimited / unknown)."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_model():
@@ -111,338 +150,492 @@ def cpu_model():
     return None
 
 
-def bench_aligner(args):
-    """Global alignments/s on this rank's pairs."""
-    cfg = dict(ALIGNER_CONFIGS[args.config])
+def cpu_fields(th, used):
+    return {"cores": int(used), "threads_requested": th, "nproc": os.cpu_count(),
+            "affinity_cpus": affinity_cpus(), "cgroup_cpu_quota": cgroup_cpu_quota(), "cpu_model": cpu_model()}
+
+
+def load_traffic(kind, key, n):
+    tfile = os.path.join(ROOT, "profiles", "traffic_%s_%s.json" % (kind, key))
+    if not os.path.exists(tfile):
+        return None, None
+    try:
+        tf = json.load(open(tfile))
+    except (OSError, ValueError):
+        return None, None
+    if tf.get("windows", tf.get("pairs")) != n:
+        return None, None
+    return tf.get("hbm_bytes_per_launch"), tf.get("source")
+
+
+def load_sq(key):
+    """SQ counter summary of the dominant kernel (scripts/pmc_sq.sh), if committed."""
+    f = os.path.join(ROOT, "profiles", "sq_%s.json" % key)
+    if not os.path.exists(f):
+        return None
+    try:
+        return json.load(open(f))
+    except (OSError, ValueError):
+        return None
+
+
+class Ctx:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world > 1:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
+        torch.cuda.set_device(self.local_rank)
+        self.dev = self.local_rank
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+    def max_over_ranks(self, v):
+        t = torch.tensor([v], dtype=torch.float64, device="cuda")
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def roofline(alg_bytes, kernel_ms, traffic, kernel, source=None, sq=None):
+    kernel_s = kernel_ms / 1e3
+    achieved = alg_bytes / kernel_s / 1e9
+    r = {"bound": "issue", "priced_as": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
+         "kernel_ms": round(kernel_ms, 3), "algorithmic_bytes_per_launch": alg_bytes,
+         "note": "integer DP; achieved = SURVEY 8(d) algorithmic bytes / kernel time; the kernel is "
+                 "instruction-issue / latency bound, measured HBM traffic is in hbm_measured_*"}
+    if traffic:
+        r["hbm_measured_gbs"] = round(traffic / kernel_s / 1e9, 2)
+        r["hbm_measured_frac"] = round(traffic / kernel_s / 1e9 / HBM_PEAK_GBS, 4)
+        r["traffic_source"] = source
+    if sq:
+        r["sq"] = sq
+    return r
+
+
+# ---------------------------------------------------------------------------
+# config D (and D_*): global alignments/s, step = align_all() + sync_alignments()
+# ---------------------------------------------------------------------------
+def bench_aligner(ctx, key, steps, warmup, args, with_cpu):
+    cfg = dict(ALIGNER_CONFIGS[key])
     if args.pairs:
         cfg["pairs"] = args.pairs
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    torch.cuda.set_device(local_rank)
     from claragenomicsanalysis_amd import synth
     from claragenomicsanalysis_amd.cudaaligner import CudaAlignerBatch
 
     n, L = cfg["pairs"], cfg["length"]
     t0 = time.time()
-    qs, ts = synth.pairs(1 + rank * n, n, L, L, 166, 166, 166)
+    qs, ts = synth.pairs(1 + ctx.rank * n, n, L, L, 166, 166, 166)
     gen_s = time.time() - t0
     stream = torch.cuda.Stream()
     b = CudaAlignerBatch(L, L, n, stream=stream, algorithm=cfg["algorithm"])
     for q, t in zip(qs, ts):
         if b.add_alignment(q, t) != 0:
             raise RuntimeError("add_alignment failed")
-    b.upload()
-    b.synchronize()
-    for _ in range(args.warmup):
-        b.launch()
-    b.synchronize()
-    if world > 1:
-        dist.barrier()
+    for _ in range(warmup):
+        b.align_all()
+        b.sync_alignments()
+    ctx.barrier()
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     t_start = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
+    for k in range(steps):
+        # align_all = H2D + kernel + D2H (aligner_global.cpp:131-159); the events bracket the kernel
+        b.upload()
+        evs[k][0].record(stream)
         b.launch()
-    ev1.record(stream)
-    b.synchronize()
+        evs[k][1].record(stream)
+        b.download()
+        b.sync_alignments()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    ctx.barrier()
     wall = time.perf_counter() - t_start
-    kernel_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
-    t_max = torch.tensor([wall], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-    wall_max = float(t_max.item())
-    b.download()
-    b.synchronize()
+    kernel_ms = float(np.mean([a.elapsed_time(e) for a, e in evs]))
+    wall_max = ctx.max_over_ranks(wall)
     paths, plen = b.raw_paths()
+    if ctx.rank != 0:
+        return None
+    from oracle import oracle
     cells = sum(len(q) * len(t) for q, t in zip(qs, ts))
     alg_bytes = sum(aligner_alg_bytes(cfg["algorithm"], q, t) for q, t in zip(qs, ts))
-    out = None
-    if rank == 0:
-        from oracle import oracle
-        k = min(8, n)
-        ok = True
-        algo = ALIGNER_ALGOS[cfg["algorithm"]][0]
-        for i in range(k):
-            want = oracle.align(qs[i], ts[i], algo, L)
-            got = paths[i, :plen[i]][::-1].tolist()
-            ok = ok and got == want
-        parity = {"pairs_checked": k, "bit_exact_vs_oracle": bool(ok)}
-        # size-independent check over every pair of the workload: a global
-        # alignment consumes the whole query (match/mismatch + deletion, i.e.
-        # present in query) and the whole target (match/mismatch + insertion,
-        # present in target; cudaaligner.hpp:46-52)
-        R = paths.shape[1]
-        live = np.arange(R)[None, :] < plen[:, None]
-        mm = (((paths == 0) | (paths == 1)) & live).sum(1)
-        full_ok = bool(np.all(mm + ((paths == 3) & live).sum(1) == np.array([len(q) for q in qs])) and
-                       np.all(mm + ((paths == 2) & live).sum(1) == np.array([len(t) for t in ts])))
-        parity["all_pairs_consume_query_and_target"] = full_ok
-        # and on the first 1000 pairs: match states join equal bases, mismatch states differing ones
-        kb = min(1000, n)
-        bases_ok = True
-        for i in range(kb):
-            p = paths[i, :plen[i]][::-1]
-            qi = np.cumsum((p == 0) | (p == 1) | (p == 3)) - 1
-            ti = np.cumsum((p == 0) | (p == 1) | (p == 2)) - 1
-            qb = np.frombuffer(qs[i] if isinstance(qs[i], bytes) else qs[i].encode(), np.uint8)
-            tb = np.frombuffer(ts[i] if isinstance(ts[i], bytes) else ts[i].encode(), np.uint8)
-            m, x = p == 0, p == 1
-            bases_ok = bases_ok and bool(np.all(qb[qi[m]] == tb[ti[m]]) and np.all(qb[qi[x]] != tb[ti[x]]))
-        parity["pairs_match_states_on_equal_bases"] = {"pairs": kb, "ok": bases_ok}
-        cpu = None
-        if not args.no_cpu and world == 1:
-            th = cpu_threads()
-            ns = args.cpu_sample or min(n, max(th * 4, 16))
-            tc = time.perf_counter()
-            cres, used = oracle.align_batch(list(zip(qs[:ns], ts[:ns])), algo, L, th)
-            cpu_s = time.perf_counter() - tc
-            match = all(cres[i] == paths[i, :plen[i]][::-1].tolist() for i in range(ns))
-            cpu = {"value": round(ns / cpu_s, 3), "unit": "alignments/s", "cores": int(used), "kind": "port",
-                   "nproc": os.cpu_count(), "cpu_model": cpu_model(),
-                   "sample": "first %d pairs of the same workload, oracle/aligner_oracle.cpp (reference-algorithm "
-                             "C++ restatement, scalar DP), OpenMP one pair per thread, %.1f s wall" % (ns, cpu_s),
-                   "matches_gpu": bool(match)}
-        kernel_s = kernel_ms / 1e3
-        achieved = alg_bytes / kernel_s / 1e9
-        grid, dev_bytes = b.config()
-        traffic = None
-        tfile = os.path.join(ROOT, "profiles", "traffic_aligner_%s.json" % args.config)
-        if os.path.exists(tfile):
-            try:
-                tf = json.load(open(tfile))
-                if tf.get("pairs") == n:
-                    traffic = tf.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        out = {
-            "metric": "global alignments/sec",
-            "value": round(n * world * args.steps / wall_max, 3),
-            "unit": "alignments/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(wall_max / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "int16" if cfg["algorithm"] == "ukkonen" else "u32 bit-vectors",
-            "data": "synthetic (reference genomeutils generators, seeds 1..N)",
-            "config": {"workload": "cudaaligner global, %d pairs/GPU x %d bp, ~10%% difference, %s"
-                                   % (n, L, cfg["algorithm"]),
-                       "config_key": args.config, "pairs_per_gpu": n, "length": L,
-                       "algorithm": cfg["algorithm"], "grid": grid, "device_bytes": dev_bytes,
-                       "gcups": round(cells / kernel_s / 1e9, 3), "input_gen_s": round(gen_s, 2),
-                       "parallelism": "dp%d (pairs sharded)" % world},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": ALIGNER_ALGOS[cfg["algorithm"]][1],
-                         "kernel_ms": round(kernel_ms, 3), "algorithmic_bytes_per_launch": alg_bytes},
-            "cpu_baseline": cpu,
-            "parity": parity,
-        }
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    k = min(8, n)
+    algo = ALIGNER_ALGOS[cfg["algorithm"]][0]
+    ok = all(paths[i, :plen[i]][::-1].tolist() == oracle.align(qs[i], ts[i], algo, L) for i in range(k))
+    parity = {"pairs_checked": k, "bit_exact_vs_oracle": bool(ok)}
+    # size-independent check over every pair: a global alignment consumes the
+    # whole query (match/mismatch + deletion) and the whole target (match/
+    # mismatch + insertion; cudaaligner.hpp:46-52)
+    R = paths.shape[1]
+    live = np.arange(R)[None, :] < plen[:, None]
+    mm = (((paths == 0) | (paths == 1)) & live).sum(1)
+    parity["all_pairs_consume_query_and_target"] = bool(
+        np.all(mm + ((paths == 3) & live).sum(1) == np.array([len(q) for q in qs])) and
+        np.all(mm + ((paths == 2) & live).sum(1) == np.array([len(t) for t in ts])))
+    kb = min(1000, n)
+    bases_ok = True
+    for i in range(kb):
+        p = paths[i, :plen[i]][::-1]
+        qi = np.cumsum((p == 0) | (p == 1) | (p == 3)) - 1
+        ti = np.cumsum((p == 0) | (p == 1) | (p == 2)) - 1
+        qb = np.frombuffer(qs[i], np.uint8)
+        tb = np.frombuffer(ts[i], np.uint8)
+        m, x = p == 0, p == 1
+        bases_ok = bases_ok and bool(np.all(qb[qi[m]] == tb[ti[m]]) and np.all(qb[qi[x]] != tb[ti[x]]))
+    parity["pairs_match_states_on_equal_bases"] = {"pairs": kb, "ok": bases_ok}
+    cpu = None
+    if with_cpu and ctx.world == 1:
+        th = cpu_threads()
+        ns = args.cpu_sample or min(n, max(th * 12, 64))
+        tc = time.perf_counter()
+        cres, used = oracle.align_batch(list(zip(qs[:ns], ts[:ns])), algo, L, th)
+        cpu_s = time.perf_counter() - tc
+        match = all(cres[i] == paths[i, :plen[i]][::-1].tolist() for i in range(ns))
+        cpu = dict({"value": round(ns / cpu_s, 3), "unit": "alignments/s", "kind": "port",
+                    "sample": "first %d pairs of the same workload, oracle/aligner_oracle.cpp (reference-algorithm "
+                              "C++ restatement, scalar DP), OpenMP one pair per thread, %.1f s wall" % (ns, cpu_s),
+                    "matches_gpu": bool(match)}, **cpu_fields(th, used))
+    grid, dev_bytes = b.config()
+    traffic, tsrc = load_traffic("aligner", key, n)
+    return {
+        "metric": "global alignments/sec",
+        "value": round(n * ctx.world * steps / wall_max, 3),
+        "unit": "alignments/s",
+        "n_gpus": ctx.world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(wall_max / steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "int16" if cfg["algorithm"] == "ukkonen" else "u32 bit-vectors",
+        "data": "synthetic (reference genomeutils generators, seeds 1..N)",
+        "config": {"workload": "cudaaligner global, %d pairs/GPU x %d bp, ~10%% difference, %s"
+                               % (n, L, cfg["algorithm"]),
+                   "config_key": key, "step": "align_all() + sync_alignments() (aligner_global.cpp:131-191)",
+                   "pairs_per_gpu": n, "length": L, "algorithm": cfg["algorithm"], "grid": grid,
+                   "device_bytes": dev_bytes, "gcups": round(cells / (kernel_ms / 1e3) / 1e9, 3),
+                   "kernel_only_alignments_per_s": round(n / (kernel_ms / 1e3), 1),
+                   "input_gen_s": round(gen_s, 2), "parallelism": "dp%d (pairs sharded)" % ctx.world},
+        "roofline": roofline(alg_bytes, kernel_ms, traffic, ALIGNER_ALGOS[cfg["algorithm"]][1], tsrc,
+                             load_sq("aligner_" + key)),
+        "cpu_baseline": cpu,
+        "parity": parity,
+    }
 
 
-def main():
-    args = parse()
-    if args.config in ALIGNER_CONFIGS:
-        return bench_aligner(args)
-    cfg = dict(CONFIGS[args.config])
+# ---------------------------------------------------------------------------
+# configs B, B_banded, C: one resident batch, step = generate_poa() + get_consensus()
+# ---------------------------------------------------------------------------
+def windows_from_packed(bases, lens):
+    raw = bases.tobytes()
+    off, out = 0, []
+    for w in range(lens.shape[0]):
+        win = []
+        for r in range(lens.shape[1]):
+            k = int(lens[w, r])
+            win.append(raw[off:off + k])
+            off += k
+        out.append(win)
+    return out
+
+
+def bench_poa(ctx, key, steps, warmup, args, with_cpu):
+    cfg = dict(CONFIGS[key])
     if args.windows:
         cfg["windows"] = args.windows
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    torch.cuda.set_device(local_rank)
-    dev = local_rank
-
     from claragenomicsanalysis_amd import synth
     from claragenomicsanalysis_amd.cudapoa import CudaPoaBatch
-
     from claragenomicsanalysis_amd.shard import window_range
-    first_seed, nwin = window_range(rank, cfg["windows"])
+
+    first_seed, nwin = window_range(ctx.rank, cfg["windows"])
     t0 = time.time()
     bases, lens = synth.poa_windows_packed(first_seed, nwin, cfg["backbone"], cfg["reads"], cfg["err"], cfg["err"],
                                            cfg["err"])
-    raw = bases.tobytes()
+    windows = windows_from_packed(bases, lens)
     gen_s = time.time() - t0
 
-    stream = torch.cuda.Stream(device=dev)
+    stream = torch.cuda.Stream(device=ctx.dev)
     msa = bool(cfg.get("msa", False))
     max_mem = int(nwin * cfg.get("mem_per_window", 12.5e6)) + (2 << 30)
-    batch = CudaPoaBatch(cfg["reads"], cfg["max_seq"], max_mem, device_id=dev, stream=stream,
+    batch = CudaPoaBatch(cfg["reads"], cfg["max_seq"], max_mem, device_id=ctx.dev, stream=stream,
                          output_type="msa" if msa else "consensus",
                          cuda_banded_alignment=cfg["banded"], alignment_band_width=cfg["bw"])
     if batch.get_capacity()[1] < nwin:
         raise RuntimeError("batch holds %d windows, need %d" % (batch.get_capacity()[1], nwin))
-    off = 0
-    windows = []
-    for w in range(nwin):
-        win = []
-        for r in range(cfg["reads"]):
-            k = int(lens[w, r])
-            win.append(raw[off:off + k])
-            off += k
-        windows.append(win)
+    for w, win in enumerate(windows):
         st, _ = batch.add_poa_group(win)
         if st != 0:
             raise RuntimeError("add_poa_group failed for window %d: %d" % (w, st))
-    batch.upload()
-    batch.synchronize()
     score_bits, size_bits = batch.get_types()
 
-    for _ in range(args.warmup):
-        batch.launch()
-    batch.synchronize()
+    def fetch():
+        if msa:
+            return batch.get_msa()  # Batch::get_msa (D2H + the per-window row vectors)
+        return batch.get_consensus_raw()
 
-    # timed region: barrier + sync on both sides, HIP events on the batch stream
-    if world > 1:
-        dist.barrier()
+    for _ in range(warmup):
+        batch.generate_poa()
+        fetch()
+    ctx.barrier()
     torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     t_start = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
+    for k in range(steps):
+        # generate_poa() = H2D of the batch + the kernel (cudapoa_batch.cuh:163-171);
+        # the events bracket the kernel on the batch's stream
+        batch.upload()
+        evs[k][0].record(stream)
         batch.launch()
-    ev1.record(stream)
-    batch.synchronize()
+        evs[k][1].record(stream)
+        fetch()  # get_consensus(): blocks, D2H, result vectors
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    ctx.barrier()
     wall = time.perf_counter() - t_start
-    kernel_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
-
-    t_max = torch.tensor([wall], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-    wall_max = float(t_max.item())
+    kernel_ms = float(np.mean([a.elapsed_time(e) for a, e in evs]))
+    wall_max = ctx.max_over_ranks(wall)
 
     # outputs + work counters (outside the timed region)
     if msa:
         msa_rows, status = batch.get_msa()
-        cons = ["".join(rows) for rows in msa_rows]  # gathered / counted as output bytes
+        cons = ["".join(rows) for rows in msa_rows]
         cov = None
     else:
         cons, cov, status = batch.get_consensus()
     cells, final_nodes = batch.get_stats()
     ticks = batch.get_phase_ticks()  # last launch, 100 MHz
     n_ok = int(sum(1 for s in status if s == 0))
-    sb = score_bits // 8
     cells_total = int(cells.sum())
-    alg_bytes = cells_total * sb * 2 + 2 * int(lens.sum()) + 3 * int(sum(len(c) for c in cons))
+    alg_bytes = cells_total * (score_bits // 8) * 2 + 2 * int(lens.sum()) + 3 * int(sum(len(c) for c in cons))
 
-    # final consensus gather to rank 0 over RCCL (SURVEY.md 8(e))
     gather_ms = None
-    if world > 1:
+    if ctx.world > 1:  # final consensus gather to rank 0 over RCCL (SURVEY.md 8(e))
         from claragenomicsanalysis_amd.shard import gather_consensus
         torch.cuda.synchronize()
         tg = time.perf_counter()
         allc = gather_consensus(cons, max(len(c) for c in cons) if msa else 2 * cfg["max_seq"], device="cuda")
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
-        if rank == 0 and len(allc) != nwin * world:
+        if ctx.rank == 0 and len(allc) != nwin * ctx.world:
             raise RuntimeError("gather returned %d strings" % len(allc))
+    if ctx.rank != 0:
+        return None
 
-    # parity spot-check and CPU baseline (rank 0, test infrastructure)
-    parity = None
-    cpu = None
-    if rank == 0:
-        from oracle import oracle
-        mn = ((4 if cfg["banded"] else 3) * cfg["max_seq"] + 3) // 4 * 4
-        k = min(4, nwin)
-        ok = True
-        for i in range(k):
-            r = oracle.poa_window(windows[i], banded=cfg["banded"], band_width=cfg["bw"], score_bits=score_bits,
-                                  max_nodes=mn, max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"], msa=msa)
-            if msa:
-                ok = ok and (r.status == status[i] and (r.msa or []) == msa_rows[i])
-            else:
-                ok = ok and (r.status == status[i] and r.consensus == cons[i] and r.coverage == cov[i])
-        parity = {"windows_checked": k, "bit_exact_vs_oracle": bool(ok)}
-        # size-independent checks over every window of the workload
-        parity["all_windows_status_ok"] = n_ok == nwin
+    from oracle import oracle
+    mn = ((4 if cfg["banded"] else 3) * cfg["max_seq"] + 3) // 4 * 4
+    k = min(4, nwin)
+    ok = True
+    for i in range(k):
+        r = oracle.poa_window(windows[i], banded=cfg["banded"], band_width=cfg["bw"], score_bits=score_bits,
+                              max_nodes=mn, max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"], msa=msa)
         if msa:
-            # MSA rows de-gapped are the window's reads (Test_CudapoaGenerateMSA2.cu:125-140)
-            parity["all_msa_rows_degap_to_reads"] = bool(all(
-                [row.replace("-", "") for row in msa_rows[i]] ==
-                [r.decode() if isinstance(r, bytes) else r for r in windows[i]] for i in range(nwin)))
+            ok = ok and (r.status == status[i] and (r.msa or []) == msa_rows[i])
         else:
-            parity["all_coverage_lengths_match"] = bool(all(len(cov[i]) == len(cons[i]) and len(cons[i]) > 0
-                                                            for i in range(nwin)))
-        if not args.no_cpu and world == 1:
-            th = cpu_threads()
-            ns = args.cpu_sample or min(nwin, max(th * (2 if msa else 48), 64 if not msa else 16))
-            tc = time.perf_counter()
-            ccons, cst, _, used = oracle.poa_batch(windows[:ns], nthreads=th, banded=cfg["banded"],
-                                                   band_width=cfg["bw"], score_bits=score_bits, max_nodes=mn,
-                                                   max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"], msa=msa)
-            cpu_s = time.perf_counter() - tc
-            if msa:
-                ccons = ["".join(rows) for rows in ccons]
-            cpu = {"value": round(ns / cpu_s, 3), "unit": "windows/s", "cores": int(used), "kind": "port",
-                   "nproc": os.cpu_count(), "cpu_model": cpu_model(),
-                   "sample": "first %d windows of the same workload, oracle/poa_oracle.cpp (reference-algorithm "
-                             "C++ restatement, not SPOA), OpenMP one window per thread, %.1f s wall" % (ns, cpu_s),
-                   "matches_gpu": bool(all(ccons[i] == cons[i] for i in range(ns)))}
+            ok = ok and (r.status == status[i] and r.consensus == cons[i] and r.coverage == cov[i])
+    parity = {"windows_checked": k, "bit_exact_vs_oracle": bool(ok), "all_windows_status_ok": n_ok == nwin}
+    if msa:
+        # MSA rows de-gapped are the window's reads (Test_CudapoaGenerateMSA2.cu:125-140)
+        parity["all_msa_rows_degap_to_reads"] = bool(all(
+            [row.replace("-", "") for row in msa_rows[i]] == [r.decode() for r in windows[i]] for i in range(nwin)))
+        parity["pinned_by"] = ("banded + MSA: the reference holds no banded or MSA known-answer vector; parity is "
+                               "HIP == IEEE-division oracle restatement (SURVEY 8(c) gap (i)), plus the de-gap "
+                               "property above")
+    else:
+        parity["all_coverage_lengths_match"] = bool(all(len(cov[i]) == len(cons[i]) and len(cons[i]) > 0
+                                                        for i in range(nwin)))
+        if cfg["banded"]:
+            parity["pinned_by"] = ("banded: no reference banded known-answer vector; parity is HIP == IEEE-division "
+                                   "oracle restatement (SURVEY 8(c) gap (i))")
+    cpu = None
+    if with_cpu and ctx.world == 1:
+        th = cpu_threads()
+        ns = args.cpu_sample or min(nwin, max(th * (1 if msa else 8), 16 if msa else 64))
+        tc = time.perf_counter()
+        res = oracle.poa_batch(windows[:ns], nthreads=th, banded=cfg["banded"], band_width=cfg["bw"],
+                               score_bits=score_bits, max_nodes=mn, max_consensus=2 * cfg["max_seq"],
+                               max_seqs=cfg["reads"], msa=msa, coverage=not msa)
+        if msa:
+            ccons, cst, _, used = res
+        else:
+            ccons, cst, ccov, _, used = res
+        cpu_s = time.perf_counter() - tc
+        if msa:
+            ccons = ["".join(rows) for rows in ccons]
+            match = all(ccons[i] == cons[i] and cst[i] == status[i] for i in range(ns))
+        else:
+            match = all(ccons[i] == cons[i] and cst[i] == status[i] and list(ccov[i]) == cov[i] for i in range(ns))
+        cpu = dict({"value": round(ns / cpu_s, 3), "unit": "windows/s", "kind": "port",
+                    "sample": "first %d windows of the same workload, oracle/poa_oracle.cpp (reference-algorithm "
+                              "C++ restatement, not SPOA), OpenMP one window per thread, %.1f s wall" % (ns, cpu_s),
+                    "matches_gpu": bool(match),
+                    "compared": "status, consensus, coverage" if not msa else "status, MSA rows"},
+                   **cpu_fields(th, used))
+    traffic, tsrc = load_traffic("poa", key, nwin)
+    slots, resident = batch.get_grid()
+    return {
+        "metric": "POA windows/sec (%s)" % ("MSA" if msa else "consensus"),
+        "value": round(nwin * ctx.world * steps / wall_max, 3),
+        "unit": "windows/s",
+        "n_gpus": ctx.world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(wall_max / steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "int16" if score_bits == 16 else "int32",
+        "data": "synthetic (reference genomeutils generators, seeds 1..N)",
+        "config": {"workload": "cudapoa %s, %d windows/GPU x %d reads x ~%d bp synthetic ONT, %s"
+                               % ("MSA" if msa else "consensus", nwin, cfg["reads"], cfg["backbone"],
+                                  "banded bw=%d" % cfg["bw"] if cfg["banded"] else "full alignment"),
+                   "config_key": key,
+                   "step": "generate_poa() (H2D + kernel) + get_%s() (D2H + result vectors), as BM_SingleBatchTest"
+                           % ("msa" if msa else "consensus"),
+                   "windows_per_gpu": nwin, "batch_size": [cfg["max_seq"], cfg["reads"]],
+                   "scores": [-8, -6, 8], "parallelism": "dp%d (windows sharded, RCCL gather)" % ctx.world,
+                   "score_bits": score_bits, "size_bits": size_bits,
+                   "kernel_variant": ["", "global", "lds", "band"][batch.kernel_variant()],
+                   "grid_slots": slots, "resident_workgroups": resident,
+                   "windows_ok": n_ok, "dp_cells_per_step": cells_total,
+                   "gcups": round(cells_total / (kernel_ms / 1e3) / 1e9, 3),
+                   "kernel_only_windows_per_s": round(nwin / (kernel_ms / 1e3), 1),
+                   "mean_final_nodes": round(float(np.mean(final_nodes)), 1),
+                   "gather_ms": gather_ms, "input_gen_s": round(gen_s, 2),
+                   "phase_ms_mean_per_window": {name: round(float(ticks[:, i].mean()) / 1e5, 3)
+                                                for i, name in enumerate(batch.PHASES)}},
+        "roofline": roofline(alg_bytes, kernel_ms, traffic, "poa_window_kernel_%s" %
+                             ["", "v1", "lds", "band"][batch.kernel_variant()], tsrc, load_sq("poa_" + key)),
+        "cpu_baseline": cpu,
+        "parity": parity,
+    }
 
-    if rank == 0:
-        kernel_s = kernel_ms / 1e3
-        achieved = alg_bytes / kernel_s / 1e9
-        traffic = None
-        if args.traffic_file is None:
-            args.traffic_file = os.path.join(ROOT, "profiles", "traffic_poa_%s.json" % args.config)
-        if os.path.exists(args.traffic_file):
-            try:
-                tf = json.load(open(args.traffic_file))
-                if tf.get("config") == args.config and tf.get("windows") == nwin:
-                    traffic = tf.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        total_windows = nwin * world
-        out = {
-            "metric": "POA windows/sec (%s)" % ("MSA" if msa else "consensus"),
-            "value": round(total_windows * args.steps / wall_max, 3),
-            "unit": "windows/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(wall_max / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "int16" if score_bits == 16 else "int32",
-            "data": "synthetic (reference genomeutils generators, seeds 1..N)",
-            "config": {"workload": "cudapoa %s, %d windows/GPU x %d reads x ~%d bp synthetic ONT, %s"
-                                   % ("MSA" if msa else "consensus", nwin, cfg["reads"], cfg["backbone"],
-                                      "banded bw=%d" % cfg["bw"] if cfg["banded"] else "full alignment"),
-                       "config_key": args.config, "windows_per_gpu": nwin, "batch_size": [cfg["max_seq"],
-                                                                                        cfg["reads"]],
-                       "scores": [-8, -6, 8], "parallelism": "dp%d (windows sharded, RCCL gather)" % world,
-                       "score_bits": score_bits, "size_bits": size_bits,
-                       "kernel_variant": ["", "global", "lds", "band"][batch.kernel_variant()],
-                       "windows_ok": n_ok, "dp_cells_per_step": cells_total,
-                       "gcups": round(cells_total / kernel_s / 1e9, 3),
-                       "mean_final_nodes": round(float(np.mean(final_nodes)), 1),
-                       "gather_ms": gather_ms, "input_gen_s": round(gen_s, 2),
-                       "phase_ms_mean_per_window": {name: round(float(ticks[:, i].mean()) / 1e5, 3)
-                                                    for i, name in enumerate(batch.PHASES)}},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "poa_window_kernel", "kernel_ms": round(kernel_ms, 3),
-                         "algorithmic_bytes_per_launch": alg_bytes},
-            "cpu_baseline": cpu,
-            "parity": parity,
-        }
-        print(json.dumps(out), flush=True)
-    if world > 1:
+
+# ---------------------------------------------------------------------------
+# config E: the multi-batch streaming driver, step = E_STEP_WINDOWS windows
+# ---------------------------------------------------------------------------
+def bench_stream(ctx, key, steps, warmup, args, with_cpu):
+    cfg = dict(STREAM_CONFIGS[key])
+    from claragenomicsanalysis_amd import synth
+    from claragenomicsanalysis_amd.cudapoa import CudaPoaMultiBatch, estimate_max_poas
+
+    from claragenomicsanalysis_amd.shard import stream_window_range
+    per_step = cfg["windows_per_step"]
+    first_seed, nwin = stream_window_range(ctx.rank, steps, per_step)
+    t0 = time.time()
+    bases, lens = synth.poa_windows_packed(first_seed, nwin, cfg["backbone"], cfg["reads"], cfg["err"], cfg["err"],
+                                           cfg["err"])
+    gen_s = time.time() - t0
+    read_lens = lens.ravel()
+    rpw = np.full(nwin, cfg["reads"], np.int64)
+    # device bytes per batch so that a batch holds stream_batch_windows windows
+    # by the reference's own capacity rule (BatchBlock::estimate_max_poas)
+    probe = 64 << 30
+    per_window = probe / max(1, estimate_max_poas(cfg["max_seq"], cfg["reads"], cfg["bw"], banded=cfg["banded"],
+                                                  msa=False, free_device_memory=probe,
+                                                  gpu_memory_usage_quota=1.0))
+    mem = int(per_window * args.stream_batch_windows) + (64 << 20)
+    mb = CudaPoaMultiBatch(cfg["reads"], cfg["max_seq"], num_batches=args.stream_batches, mem_per_batch=mem,
+                           device_id=ctx.dev, cuda_banded_alignment=cfg["banded"], alignment_band_width=cfg["bw"])
+    stride = mb.stride
+    out = (np.zeros(nwin, np.int32), np.zeros(nwin, np.int32), np.zeros((nwin, stride), np.uint8),
+           np.zeros((nwin, stride), np.uint16))
+    for a in out:  # touch the pages outside the timed region
+        a.fill(0)
+    if warmup > 0:  # untimed pass over this rank's first warmup x step windows
+        wn = min(nwin, warmup * per_step)
+        nb = int(read_lens[:wn * cfg["reads"]].sum())
+        mb.process_packed(bases[:nb], read_lens[:wn * cfg["reads"]], rpw[:wn])
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    mb.process_packed(bases, read_lens, rpw, out=out)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    wall = time.perf_counter() - t_start
+    wall_max = ctx.max_over_ranks(wall)
+    status, clen, cons, cov = out
+    nb_used, per_batch, rounds = mb.info()
+    n_ok = int((status == 0).sum())
+
+    gather_ms = None
+    gathered = None
+    if ctx.world > 1:  # every rank's consensus rows to rank 0 over RCCL (SURVEY.md 8(e))
+        from claragenomicsanalysis_amd.shard import gather_rows
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        rows = np.concatenate([clen.view(np.uint8).reshape(nwin, 4), status.view(np.uint8).reshape(nwin, 4), cons],
+                              axis=1)
+        gathered = gather_rows(rows, device="cuda")
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) * 1e3
+    if ctx.rank != 0:
+        return None
+    parity = {"all_windows_status_ok": n_ok == nwin}
+    if gathered is not None:
+        glen = gathered[:, :4].copy().view(np.int32).ravel()
+        gst = gathered[:, 4:8].copy().view(np.int32).ravel()
+        parity["gathered_windows"] = int(gathered.shape[0])
+        parity["gathered_all_status_ok"] = bool((gst == 0).all() and (glen > 0).all())
+        parity["gathered_rank0_rows_equal_local"] = bool(
+            np.array_equal(gathered[:nwin, 8:], cons) and np.array_equal(glen[:nwin], clen))
+    # oracle check of a sample spread over the rank's stream (windows from every batch round)
+    from oracle import oracle
+    idx = sorted(set(np.linspace(0, nwin - 1, 12).astype(int).tolist()))
+    starts = np.concatenate([[0], np.cumsum(read_lens)])
+    samp = []
+    for i in idx:
+        r0 = i * cfg["reads"]
+        samp.append([bases[starts[r]:starts[r + 1]].tobytes() for r in range(r0, r0 + cfg["reads"])])
+    mn = 3 * cfg["max_seq"]
+    rcons, rst, rcov, _, used = oracle.poa_batch(samp, nthreads=cpu_threads(), max_nodes=mn,
+                                                 max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"],
+                                                 coverage=True)
+    ok = all(rst[j] == status[i] and rcons[j] == cons[i, :clen[i]].tobytes().decode() and
+             list(rcov[j]) == cov[i, :clen[i]].tolist() for j, i in enumerate(idx))
+    parity.update({"windows_checked": len(idx), "bit_exact_vs_oracle": bool(ok)})
+    total = nwin * ctx.world
+    return {
+        "metric": "POA windows/sec (consensus)",
+        "value": round(total / wall_max, 3),
+        "unit": "windows/s",
+        "n_gpus": ctx.world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(wall_max / steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "int16",
+        "data": "synthetic (reference genomeutils generators, seeds 1 + rank*%d ...)" % nwin,
+        "config": {"workload": "cudapoa consensus, multi-batch stream of %d windows/GPU (%d steps x %d) x %d reads "
+                               "x ~%d bp synthetic ONT, full alignment (1M-window job at 8 GPUs x 20 steps)"
+                               % (nwin, steps, per_step, cfg["reads"], cfg["backbone"]),
+                   "config_key": key,
+                   "step": "%d windows through MultiBatch::process_batches (fill + H2D + kernel + D2H timed, "
+                           "multi_batch.hpp:64-171)" % per_step,
+                   "windows_per_gpu": nwin, "batches": nb_used, "windows_per_batch": per_batch,
+                   "batch_rounds": rounds, "mem_per_batch": mem, "batch_size": [cfg["max_seq"], cfg["reads"]],
+                   "scores": [-8, -6, 8], "parallelism": "dp%d (windows sharded, RCCL gather)" % ctx.world,
+                   "windows_ok": n_ok, "gather_ms": gather_ms, "input_gen_s": round(gen_s, 2)},
+        "roofline": None,
+        "cpu_baseline": None,
+        "parity": parity,
+    }
+
+
+RUNNERS = {}
+RUNNERS.update({k: bench_poa for k in CONFIGS})
+RUNNERS.update({k: bench_aligner for k in ALIGNER_CONFIGS})
+RUNNERS.update({k: bench_stream for k in STREAM_CONFIGS})
+
+
+def main():
+    args = parse()
+    ctx = Ctx()
+    default = args.config is None
+    key = args.config or ("B" if ctx.world == 1 else "E")
+    line = RUNNERS[key](ctx, key, args.steps, args.warmup, args, not args.no_cpu)
+    if default and ctx.world == 1 and not args.no_secondary:
+        # the metric's second half and the streaming driver, in the same run
+        sec = {}
+        sec["D"] = bench_aligner(ctx, "D", max(1, args.secondary_steps), 1, args, not args.no_cpu)
+        sec["E"] = bench_stream(ctx, "E", args.steps, min(args.warmup, 1), args, False)
+        if line is not None:
+            line["secondary"] = sec
+    if ctx.rank == 0 and line is not None:
+        print(json.dumps(line), flush=True)
+    if ctx.world > 1:
         dist.destroy_process_group()
 
 

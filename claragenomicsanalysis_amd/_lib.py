@@ -66,6 +66,8 @@ def _declare(L):
     L.gwamd_poa_get_types.argtypes = [vp, P(i32), P(i32)]
     L.gwamd_poa_get_capacity.restype = i32
     L.gwamd_poa_get_capacity.argtypes = [vp, P(i64), P(i32)]
+    L.gwamd_poa_get_grid.restype = i32
+    L.gwamd_poa_get_grid.argtypes = [vp, P(i32), P(i32)]
     L.gwamd_poa_set_spoa_accurate.restype = i32
     L.gwamd_poa_set_spoa_accurate.argtypes = [vp, i32]
     if hasattr(L, "gwamd_aligner_create"):

@@ -1167,10 +1167,11 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
     __shared__ int sh_status;
     __shared__ int sh_len;
 
-    const int w = b.order ? b.order[blockIdx.x] : int(blockIdx.x);
-    if (w >= b.num_windows)
+    __shared__ int sh_next;
+    if (int(blockIdx.x) >= b.num_windows)
         return;
-    const int lane = threadIdx.x;
+    const int lane    = threadIdx.x;
+    const size_t slot = blockIdx.x; // scratch slot (grid <= slots)
 
     uint8_t* lread          = lds;
     GWAMD_LDS uint8_t* work = (GWAMD_LDS uint8_t*)(lds) + d.lds_ring_off;
@@ -1181,6 +1182,9 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
     // row-record staging after the ring (planned by poa_batch.cpp)
     GWAMD_LDS uint32_t* stage = (GWAMD_LDS uint32_t*)(work + ((kBandRing * rowsz * int(sizeof(ScoreT)) + 15) & ~15));
 
+    for (int idx = blockIdx.x; idx < b.num_windows;)
+    {
+    const int w     = b.order ? b.order[idx] : idx;
     const size_t mn = size_t(d.max_nodes);
     WinGraph<SizeT> g;
     g.base      = b.base + w * mn;
@@ -1196,10 +1200,10 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
     g.pos       = static_cast<SizeT*>(b.pos) + w * mn;
     g.max_nodes = d.max_nodes;
 
-    SizeT* ag        = static_cast<SizeT*>(b.ag) + size_t(w) * d.aln_cap;
-    SizeT* ar        = static_cast<SizeT*>(b.ar) + size_t(w) * d.aln_cap;
-    ScoreT* spill    = static_cast<ScoreT*>(b.scores) + size_t(w) * d.score_rows * size_t(rowsz);
-    uint8_t* aux     = b.codes + size_t(w) * size_t(d.aux_stride);
+    SizeT* ag        = static_cast<SizeT*>(b.ag) + slot * d.aln_cap;
+    SizeT* ar        = static_cast<SizeT*>(b.ar) + slot * d.aln_cap;
+    ScoreT* spill    = static_cast<ScoreT*>(b.scores) + slot * d.score_rows * size_t(rowsz);
+    uint8_t* aux     = b.codes + slot * size_t(d.aux_stride);
     BandAux X;
     X.codes          = aux;
     X.reca           = reinterpret_cast<uint32_t*>(aux + d.aux_reca_off);
@@ -1211,8 +1215,8 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
     X.xl             = reinterpret_cast<int32_t*>(aux + d.aux_xl_off);
     X.bx             = reinterpret_cast<int32_t*>(aux + d.aux_bx_off);
     X.xl_cap         = d.aux_xl_cap;
-    int32_t* cscore  = b.cscore + w * mn;
-    SizeT* cpred     = static_cast<SizeT*>(b.cpred) + w * mn * 4;
+    int32_t* cscore  = b.cscore + slot * mn;
+    SizeT* cpred     = static_cast<SizeT*>(b.cpred) + slot * mn * 4;
     uint16_t* ecov   = MSA ? b.edge_cov + w * mn * kMaxEdges * d.max_seqs : nullptr;
     uint16_t* ecovc  = MSA ? b.edge_cov_cnt + w * mn * kMaxEdges : nullptr;
     SizeT* seq_begin = MSA ? static_cast<SizeT*>(b.seq_begin) + size_t(w) * d.max_seqs : nullptr;
@@ -1368,6 +1372,17 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
         b.final_nodes[w] = node_count;
         b.cells[w]       = cells;
     }
+    if (b.head == nullptr)
+        break;
+    // next queue position; the LDS image is rewritten by the next window
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    wave_sync();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (lane == 0)
+        sh_next = b.num_slots + atomicAdd(b.head, 1);
+    wave_sync();
+    idx = uniform(sh_next);
+    }
 }
 
 } // namespace poa
@@ -1379,7 +1394,7 @@ extern "C" hipError_t gwamd_internal_poa_band_launch(const gwamd::poa::Buffers* 
                                                      int msa, hipStream_t stream)
 {
     using namespace gwamd::poa;
-    const dim3 grid(b->num_windows), blk(kWave);
+    const dim3 grid(b->head ? b->num_slots : b->num_windows), blk(kWave);
     const size_t lb = size_t(d->lds_bytes);
 #define GWAMD_BAND_LAUNCH(ST, ZT, MS, CPL)                                                                      \
     {                                                                                                         \
@@ -1418,4 +1433,46 @@ extern "C" hipError_t gwamd_internal_poa_band_launch(const gwamd::poa::Buffers* 
 #undef GWAMD_BAND_MSA
 #undef GWAMD_BAND_CPL
 #undef GWAMD_BAND_LAUNCH
+}
+
+// Resident workgroups per CU of the planned banded kernel (persistent grid).
+extern "C" int gwamd_internal_poa_band_blocks_per_cu(const gwamd::poa::Dims* d, int score_bits, int size_bits, int msa)
+{
+    using namespace gwamd::poa;
+    const size_t lb = size_t(d->lds_bytes);
+#define GWAMD_BAND_OCC(ST, ZT, MS, CPL)                                                                         \
+    {                                                                                                         \
+        auto kfn = poa_window_kernel_band<ST, ZT, MS, CPL>;                                                   \
+        if (lb > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                             \
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lb)) != hipSuccess) \
+            return 0;                                                                                         \
+        int n = 0;                                                                                            \
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kfn, kWave, lb) != hipSuccess)                   \
+            return 0;                                                                                         \
+        return n;                                                                                             \
+    }
+#define GWAMD_BAND_OCC_CPL(ST, ZT, MS)     \
+    if (d->lds_cpl == 4)                   \
+        GWAMD_BAND_OCC(ST, ZT, MS, 4)      \
+    if (d->lds_cpl == 2)                   \
+        GWAMD_BAND_OCC(ST, ZT, MS, 2)      \
+    return 0;
+#define GWAMD_BAND_OCC_MSA(ST, ZT)         \
+    if (msa)                               \
+    {                                      \
+        GWAMD_BAND_OCC_CPL(ST, ZT, true)   \
+    }                                      \
+    GWAMD_BAND_OCC_CPL(ST, ZT, false)
+    if (score_bits == 16)
+    {
+        GWAMD_BAND_OCC_MSA(int16_t, int16_t)
+    }
+    if (size_bits == 16)
+    {
+        GWAMD_BAND_OCC_MSA(int32_t, int16_t)
+    }
+    GWAMD_BAND_OCC_MSA(int32_t, int32_t)
+#undef GWAMD_BAND_OCC_MSA
+#undef GWAMD_BAND_OCC_CPL
+#undef GWAMD_BAND_OCC
 }

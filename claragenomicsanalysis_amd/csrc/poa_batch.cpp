@@ -28,6 +28,8 @@
 extern "C" hipError_t gwamd_internal_poa_launch(const gwamd::poa::Buffers* b, const gwamd::poa::Dims* d,
                                        const gwamd::poa::Scores* sc, int score_bits, int size_bits, int banded,
                                        int msa, hipStream_t stream);
+extern "C" int gwamd_internal_poa_blocks_per_cu(const gwamd::poa::Dims* d, int score_bits, int size_bits, int banded,
+                                                int msa);
 
 namespace claraparabricks
 {
@@ -150,12 +152,32 @@ public:
             dims_.spoa_accurate = std::atoi(sa) != 0 ? 1 : 0;
         plan_lds_kernel();
         plan_band_kernel();
-        const int64_t own = own_bytes_per_window(sz, sbytes, msa);
-        if (own > 0)
-            max_poas = std::min<int64_t>(max_poas, int64_t(max_mem) / own);
+        // this build's footprint: graph + inputs + outputs per window, and the
+        // forward/traceback scratch per slot.  The LDS and banded kernels run
+        // a persistent grid of as many workgroups as are resident at once, so
+        // they need only that many slots however many windows the batch holds.
+        const int64_t wbytes = window_bytes(sz, msa);
+        const int64_t sbytes_slot = slot_bytes(sz, sbytes);
+        int64_t own_cap = int64_t(max_mem) / (wbytes + sbytes_slot); // a slot per window
+        int64_t resident = 0;
+        if (dims_.lds_kernel)
+        {
+            int cus = 0;
+            GWAMD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
+            resident = int64_t(gwamd_internal_poa_blocks_per_cu(&dims_, score_bits_, size_bits_, banded_ ? 1 : 0,
+                                                                msa ? 1 : 0)) * cus;
+            if (const char* ev = std::getenv("GWAMD_POA_SLOTS")) // diagnostic: a smaller persistent grid
+                if (std::atoi(ev) > 0)
+                    resident = std::min<int64_t>(resident > 0 ? resident : INT32_MAX, std::atoi(ev));
+            if (resident > 0 && own_cap > resident)
+                own_cap = std::max(own_cap, (int64_t(max_mem) - resident * sbytes_slot) / wbytes);
+        }
+        max_poas = std::min<int64_t>(max_poas, own_cap);
         if (max_poas < 1)
             throw std::runtime_error("Require more device memory per CUDAPOA batch to process correctly.");
         max_poas_ = int32_t(std::min<int64_t>(max_poas, INT32_MAX));
+        slots_    = resident > 0 ? int32_t(std::min<int64_t>(resident, max_poas_)) : max_poas_;
+        blocks_per_cu_ = resident > 0 ? int32_t(resident) : 0;
 
         // score budget (allocate_block.hpp:196-201): what the reference's slab
         // leaves for the variable-width score matrices
@@ -218,18 +240,25 @@ public:
         plan_launch_order();
     }
 
-    // Workgroup -> window order.  Workgroups i, i + C, i + 2C, ... (C = CUs)
-    // share a CU when a batch holds more windows than CUs; windows are
-    // ranked by estimated DP cells and dealt to those rounds in snake order,
-    // so every CU gets a mix of heavy and light windows and the batch does
-    // not wait on a CU full of heavy ones.  Outputs stay indexed by window.
+    // Queue order of the windows.  Workgroups i, i + C, i + 2C, ... (C =
+    // CUs) share a CU; windows are ranked by estimated DP cells and the
+    // first grid's worth is dealt to those rounds in snake order, so every CU
+    // gets a mix of heavy and light windows.  When the batch holds more
+    // windows than the persistent grid has slots, the rest follow heaviest
+    // first and are dequeued by whichever workgroup finishes first (longest
+    // processing time first).  Outputs stay indexed by window.
     void plan_launch_order()
     {
         bufs_.order = nullptr;
+        bufs_.head  = nullptr;
         int cus     = 0;
         GWAMD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
-        const int n = poa_count_;
-        if (cus <= 0 || n <= cus)
+        if (const char* ev = std::getenv("GWAMD_LAUNCH_ORDER_CUS")) // diagnostic: plan for fewer CUs
+            if (std::atoi(ev) > 0)
+                cus = std::atoi(ev);
+        const int n           = poa_count_;
+        const bool persistent = dims_.lds_kernel != 0 && n > slots_;
+        if (!persistent && (cus <= 0 || n <= cus))
             return;
         const auto* wd = h_win_.as<gwamd::poa::WindowDesc>();
         const auto* ln = h_len_.as<int32_t>();
@@ -250,17 +279,28 @@ public:
         // pinned, so the copy stays asynchronous (generate_poa does not block)
         h_order_.reserve(size_t(n) * 4, stream_);
         int32_t* order = h_order_.as<int32_t>();
-        for (int k = 0; k < n; k++)
+        const int m    = persistent ? slots_ : n; // positions placed statically
+        for (int k = 0; k < m; k++)
         {
+            if (cus <= 0)
+            {
+                order[k] = cost[size_t(k)].second;
+                continue;
+            }
             const int t = k / cus, pos = k % cus;
-            const int m = std::min(cus, n - t * cus); // workgroups in this round
-            const int j = (t % 2 == 0) ? pos : m - 1 - pos;
+            const int r = std::min(cus, m - t * cus); // workgroups in this round
+            const int j = (t % 2 == 0) ? pos : r - 1 - pos;
             order[t * cus + j] = cost[size_t(k)].second;
         }
-        int32_t* d_order = reinterpret_cast<int32_t*>(static_cast<uint8_t*>(d_win_.p) +
-                                                      ((size_t(max_poas_) * sizeof(gwamd::poa::WindowDesc) + 15) & ~size_t(15)));
+        for (int k = m; k < n; k++)
+            order[k] = cost[size_t(k)].second;
+        const size_t order_off = (size_t(max_poas_) * sizeof(gwamd::poa::WindowDesc) + 15) & ~size_t(15);
+        int32_t* d_order       = reinterpret_cast<int32_t*>(static_cast<uint8_t*>(d_win_.p) + order_off);
         GWAMD_HIP_CHECK(hipMemcpyAsync(d_order, order, size_t(n) * 4, hipMemcpyHostToDevice, stream_));
         bufs_.order = d_order;
+        if (persistent)
+            bufs_.head = reinterpret_cast<int32_t*>(static_cast<uint8_t*>(d_win_.p) +
+                                                    ((order_off + size_t(max_poas_) * 4 + 15) & ~size_t(15)));
     }
 
     void launch()
@@ -270,6 +310,9 @@ public:
         ScopedDevice dev(device_id_);
         gwamd::poa::Buffers b = bufs_;
         b.num_windows         = poa_count_;
+        b.num_slots           = slots_;
+        if (b.head) // the dequeue counter starts at 0 for every launch
+            GWAMD_HIP_CHECK(hipMemsetAsync(b.head, 0, sizeof(int32_t), stream_));
         gwamd::poa::Scores sc{gap_, mismatch_, match_};
         const bool msa = (output_mask_ & OutputType::msa) != 0;
         GWAMD_HIP_CHECK(gwamd_internal_poa_launch(&b, &dims_, &sc, score_bits_, size_bits_, banded_ ? 1 : 0, msa ? 1 : 0,
@@ -463,6 +506,8 @@ public:
     int64_t device_bytes() const { return int64_t(d_slab_.n + d_codes_.n + d_seqs_.n + d_wts_.n + d_len_.n + d_off_.n + d_win_.n); }
     int32_t kernel_kind() const { return dims_.lds_kernel == 3 ? 3 : (dims_.lds_kernel ? 2 : 1); }
     int32_t max_poas() const { return max_poas_; }
+    int32_t slots() const { return slots_; }
+    int32_t resident_slots() const { return blocks_per_cu_; }
     void set_spoa_accurate(bool on) { dims_.spoa_accurate = on ? 1 : 0; }
     bool spoa_accurate() const { return dims_.spoa_accurate != 0; }
 
@@ -488,22 +533,31 @@ public:
     }
 
 private:
-    int64_t own_bytes_per_window(int sz, int sbytes, bool msa) const
+    // Graph, inputs and outputs of one window.
+    int64_t window_bytes(int sz, bool msa) const
     {
         const int64_t mn = dims_.max_nodes, E = gwamd::poa::kMaxEdges, S = dims_.max_seqs;
         int64_t b        = 0;
         b += align8(mn) + 4 * align8(mn * 2) + align8(mn * E * 2);   // base, counts, coverage, in_w
         b += 3 * align8(mn * E * sz) + 2 * align8(mn * sz);           // in_e, out_e, aln, sorted, pos
-        b += 2 * align8(int64_t(dims_.aln_cap) * sz);                 // ag, ar
-        b += int64_t(dims_.score_rows) * dims_.score_stride * sbytes; // scores (LDS kernel: spill rows)
-        if (dims_.lds_kernel)
-            b += dims_.aux_stride; // traceback codes, row program, predecessor lists, carries
-        b += align8(mn * 4) + align8(mn * 4 * sz);                    // cscore, cpred
         b += align8(dims_.max_consensus) + align8(int64_t(dims_.max_consensus) * 2) + 32; // outputs
         b += int64_t(S) * dims_.max_seq_len * 2 + S * 12;             // inputs
         if (msa)
             b += align8(mn * E * S * 2) + align8(mn * E * 2) + align8(S * sz) +
                  align8(S * int64_t(dims_.max_consensus));
+        return b;
+    }
+
+    // Forward-pass / traceback / consensus scratch of one slot.
+    int64_t slot_bytes(int sz, int sbytes) const
+    {
+        const int64_t mn = dims_.max_nodes;
+        int64_t b        = 0;
+        b += 2 * align8(int64_t(dims_.aln_cap) * sz);                 // ag, ar
+        b += int64_t(dims_.score_rows) * dims_.score_stride * sbytes; // scores (LDS kernel: spill rows)
+        if (dims_.lds_kernel)
+            b += dims_.aux_stride; // traceback codes, row program, predecessor lists, carries
+        b += align8(mn * 4) + align8(mn * 4 * sz);                    // cscore, cpred
         return b;
     }
 
@@ -681,6 +735,7 @@ private:
     void allocate(int sz, int sbytes, bool msa)
     {
         const int64_t P = max_poas_, mn = dims_.max_nodes, E = gwamd::poa::kMaxEdges, S = dims_.max_seqs;
+        const int64_t Z = slots_; // scratch slots
         struct Item
         {
             void** dst;
@@ -699,10 +754,10 @@ private:
             {&bufs_.aln, align8(P * mn * E * sz)},
             {&bufs_.sorted, align8(P * mn * sz)},
             {&bufs_.pos, align8(P * mn * sz)},
-            {&bufs_.ag, align8(P * dims_.aln_cap * sz)},
-            {&bufs_.ar, align8(P * dims_.aln_cap * sz)},
-            {reinterpret_cast<void**>(&bufs_.cscore), align8(P * mn * 4)},
-            {&bufs_.cpred, align8(P * mn * 4 * sz)},
+            {&bufs_.ag, align8(Z * dims_.aln_cap * sz)},
+            {&bufs_.ar, align8(Z * dims_.aln_cap * sz)},
+            {reinterpret_cast<void**>(&bufs_.cscore), align8(Z * mn * 4)},
+            {&bufs_.cpred, align8(Z * mn * 4 * sz)},
             {reinterpret_cast<void**>(&bufs_.cons), align8(P * dims_.max_consensus)},
             {reinterpret_cast<void**>(&bufs_.cov), align8(P * dims_.max_consensus * 2)},
             {reinterpret_cast<void**>(&bufs_.cons_len), align8(P * 4)},
@@ -723,7 +778,7 @@ private:
             off += it.bytes;
         off                   = (off + 255) & ~int64_t(255);
         const int64_t sc_off  = off;
-        const int64_t sc_size = P * int64_t(dims_.score_rows) * dims_.score_stride * sbytes;
+        const int64_t sc_size = Z * int64_t(dims_.score_rows) * dims_.score_stride * sbytes;
         d_slab_.n             = size_t(off + sc_size);
         GWAMD_HIP_CHECK(hipMalloc(&d_slab_.p, d_slab_.n));
         uint8_t* base = static_cast<uint8_t*>(d_slab_.p);
@@ -737,7 +792,7 @@ private:
         bufs_.scores = base + sc_off;
         if (dims_.lds_kernel)
         {
-            const size_t code_bytes = size_t(P) * size_t(dims_.aux_stride);
+            const size_t code_bytes = size_t(Z) * size_t(dims_.aux_stride);
             GWAMD_HIP_CHECK(hipMalloc(&d_codes_.p, code_bytes));
             d_codes_.n   = code_bytes;
             bufs_.codes = static_cast<uint8_t*>(d_codes_.p);
@@ -748,7 +803,7 @@ private:
         d_wts_.n               = size_t(in_bytes);
         d_len_.n               = size_t(P * S * 4 + 8);
         d_off_.n               = size_t(P * S * 8 + 8);
-        d_win_.n               = size_t(P * (sizeof(gwamd::poa::WindowDesc) + 4) + 16);
+        d_win_.n               = size_t(P * (sizeof(gwamd::poa::WindowDesc) + 4) + 64); // + order, dequeue head
         for (auto* b : {&d_seqs_, &d_wts_, &d_len_, &d_off_, &d_win_})
             GWAMD_HIP_CHECK(hipMalloc(&b->p, b->n));
         bufs_.seqs    = static_cast<const uint8_t*>(d_seqs_.p);
@@ -842,6 +897,8 @@ private:
     bool banded_;
     int32_t score_bits_ = 16, size_bits_ = 16;
     int32_t max_poas_   = 0;
+    int32_t slots_      = 0; // scratch slots (persistent grid size for the LDS / banded kernels)
+    int32_t blocks_per_cu_ = 0; // resident workgroups on the device (0: v1 kernel)
     int64_t scorebuf_alloc_ = 0, avail_scorebuf_ = 0, next_scores_offset_ = 0;
     int32_t poa_count_  = 0;
     int32_t num_seqs_   = 0;
@@ -1260,6 +1317,13 @@ int32_t gwamd_poa_get_capacity(const gwamd_poa_batch* batch, int64_t* device_byt
 {
     *device_bytes = batch->impl->device_bytes();
     *max_poas     = batch->impl->max_poas();
+    return 0;
+}
+
+int32_t gwamd_poa_get_grid(const gwamd_poa_batch* batch, int32_t* slots, int32_t* resident)
+{
+    *slots    = batch->impl->slots();
+    *resident = batch->impl->resident_slots();
     return 0;
 }
 

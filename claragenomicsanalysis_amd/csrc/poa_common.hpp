@@ -114,8 +114,16 @@ struct Buffers
     const int32_t* seq_len;
     const int64_t* seq_off;
     const WindowDesc* windows;
-    const int32_t* order; // window of each workgroup (nullptr: workgroup i runs window i)
+    const int32_t* order; // window of each queue position (nullptr: position i is window i)
     int32_t num_windows;
+    // Persistent grid (LDS and banded kernels): workgroup i first runs queue
+    // position i, then dequeues num_slots + atomicAdd(head, 1) until the queue
+    // is empty.  head == nullptr: one window per workgroup.  The per-window
+    // scratch of the forward pass and traceback (spill rows, codes, row
+    // records, alignment path, consensus scores) is indexed by workgroup
+    // ("slot"), the graph and the outputs by window.
+    int32_t* head;
+    int32_t num_slots;
     // graph scratch
     uint8_t* base;
     uint16_t* in_cnt;

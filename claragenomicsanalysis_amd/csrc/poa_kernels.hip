@@ -1068,13 +1068,14 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
     __shared__ int sh_status;
     __shared__ int sh_len;
 
-    const int w = b.order ? b.order[blockIdx.x] : int(blockIdx.x);
-    if (w >= b.num_windows)
+    __shared__ int sh_next;
+    if (int(blockIdx.x) >= b.num_windows)
         return;
     const int tid      = threadIdx.x;
     const int lane     = tid & (kWave - 1);
     const int wave     = uniform(tid / kWave);
     constexpr int kThr = kWave * NW;
+    const size_t slot  = blockIdx.x; // scratch slot (grid <= slots)
 
     uint8_t* lread   = lds;
     int16_t* ring    = reinterpret_cast<int16_t*>(lds + d.lds_ring_off);
@@ -1093,6 +1094,9 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
         AX.sh                = (GWAMD_LDS int*)(shb);
     }
 
+    for (int idx = blockIdx.x; idx < b.num_windows;)
+    {
+    const int w     = b.order ? b.order[idx] : idx;
     const size_t mn = size_t(d.max_nodes);
     WinGraph<SizeT> g;
     g.base      = b.base + w * mn;
@@ -1108,16 +1112,16 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
     g.pos       = static_cast<SizeT*>(b.pos) + w * mn;
     g.max_nodes = d.max_nodes;
 
-    SizeT* ag        = static_cast<SizeT*>(b.ag) + size_t(w) * d.aln_cap;
-    SizeT* ar        = static_cast<SizeT*>(b.ar) + size_t(w) * d.aln_cap;
-    int16_t* spill   = static_cast<int16_t*>(b.scores) + size_t(w) * d.score_rows * size_t(rstride);
-    uint8_t* codes   = b.codes + size_t(w) * size_t(d.aux_stride);
+    SizeT* ag        = static_cast<SizeT*>(b.ag) + slot * d.aln_cap;
+    SizeT* ar        = static_cast<SizeT*>(b.ar) + slot * d.aln_cap;
+    int16_t* spill   = static_cast<int16_t*>(b.scores) + slot * d.score_rows * size_t(rstride);
+    uint8_t* codes   = b.codes + slot * size_t(d.aux_stride);
     uint32_t* rec    = reinterpret_cast<uint32_t*>(lds + d.lds_rec_off);
     uint16_t* xl     = reinterpret_cast<uint16_t*>(lds + d.lds_xl_off);
     int16_t* carry   = reinterpret_cast<int16_t*>(codes + d.aux_carry_off);
     RowProg P{rec, xl, d.lds_ring_rows - 1};
-    int32_t* cscore  = b.cscore + w * mn;
-    SizeT* cpred     = static_cast<SizeT*>(b.cpred) + w * mn * 4;
+    int32_t* cscore  = b.cscore + slot * mn;
+    SizeT* cpred     = static_cast<SizeT*>(b.cpred) + slot * mn * 4;
     uint16_t* ecov   = MSA ? b.edge_cov + w * mn * kMaxEdges * d.max_seqs : nullptr;
     uint16_t* ecovc  = MSA ? b.edge_cov_cnt + w * mn * kMaxEdges : nullptr;
     SizeT* seq_begin = MSA ? static_cast<SizeT*>(b.seq_begin) + size_t(w) * d.max_seqs : nullptr;
@@ -1255,6 +1259,15 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
             b.cells[w]       = cells;
         }
     }
+    if (b.head == nullptr)
+        break;
+    // next queue position; the LDS image is rewritten by the next window
+    __syncthreads();
+    if (tid == 0)
+        sh_next = b.num_slots + atomicAdd(b.head, 1);
+    __syncthreads();
+    idx = uniform(sh_next);
+    }
 }
 
 } // namespace poa
@@ -1264,6 +1277,48 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
 extern "C" hipError_t gwamd_internal_poa_band_launch(const gwamd::poa::Buffers* b, const gwamd::poa::Dims* d,
                                                      const gwamd::poa::Scores* sc, int score_bits, int size_bits,
                                                      int msa, hipStream_t stream); // poa_band.hip
+extern "C" int gwamd_internal_poa_band_blocks_per_cu(const gwamd::poa::Dims* d, int score_bits, int size_bits,
+                                                     int msa); // poa_band.hip
+
+namespace
+{
+template <typename K>
+int blocks_per_cu(K kfn, int threads, size_t lds)
+{
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kfn, threads, lds) != hipSuccess)
+        return 0;
+    return n;
+}
+} // namespace
+
+// Workgroups of the planned LDS or banded kernel that are resident on one CU
+// at once (the persistent grid is this times the CU count); 0 for the v1
+// kernel, which runs one workgroup per window.
+extern "C" int gwamd_internal_poa_blocks_per_cu(const gwamd::poa::Dims* d, int score_bits, int size_bits, int banded,
+                                                int msa)
+{
+    using namespace gwamd::poa;
+    if (d->lds_kernel == 3 && banded)
+        return gwamd_internal_poa_band_blocks_per_cu(d, score_bits, size_bits, msa);
+    if (d->lds_kernel != 1 || banded || score_bits != 16 || size_bits != 16)
+        return 0;
+    const size_t lb = size_t(d->lds_bytes);
+#define GWAMD_LDS_OCC(CPL, NW)                                                                                 \
+    if (d->lds_cpl == CPL && d->lds_waves == NW)                                                               \
+        return msa ? blocks_per_cu(poa_window_kernel_lds<true, CPL, NW>, kWave * NW, lb)                       \
+                   : blocks_per_cu(poa_window_kernel_lds<false, CPL, NW>, kWave * NW, lb);
+    GWAMD_LDS_OCC(8, 1)
+    GWAMD_LDS_OCC(16, 1)
+    GWAMD_LDS_OCC(24, 1)
+    GWAMD_LDS_OCC(32, 1)
+    GWAMD_LDS_OCC(8, 2)
+    GWAMD_LDS_OCC(8, 3)
+    GWAMD_LDS_OCC(8, 4)
+    GWAMD_LDS_OCC(16, 4)
+#undef GWAMD_LDS_OCC
+    return 0;
+}
 
 // Internal launch ABI used by the C++ batch (poa_batch.cpp).
 extern "C" hipError_t gwamd_internal_poa_launch(const gwamd::poa::Buffers* b, const gwamd::poa::Dims* d,
@@ -1274,6 +1329,8 @@ extern "C" hipError_t gwamd_internal_poa_launch(const gwamd::poa::Buffers* b, co
     if (b->num_windows <= 0)
         return hipSuccess;
     dim3 grid(b->num_windows), block(kWave);
+    if (d->lds_kernel && b->head)
+        grid = dim3(b->num_slots); // persistent grid: one workgroup per scratch slot
     if (d->lds_kernel == 3 && banded)
         return gwamd_internal_poa_band_launch(b, d, sc, score_bits, size_bits, msa, stream);
     if (d->lds_kernel == 1 && !banded && score_bits == 16 && size_bits == 16)

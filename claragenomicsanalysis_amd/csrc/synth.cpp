@@ -5,8 +5,10 @@
 // generate_random_sequences(generate_random_genome(L, rng(seed)), ...) output.
 #include <cstdint>
 #include <cstring>
+#include <algorithm>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace
@@ -76,20 +78,41 @@ int64_t gwamd_synth_poa_windows(int32_t first_seed, int32_t n, int32_t backbone_
                                 int32_t max_mut, int32_t max_ins, int32_t max_del, uint8_t* bases_out,
                                 int64_t bases_cap, int32_t* lens_out)
 {
-    int64_t off = 0;
-    for (int32_t w = 0; w < n; w++)
-    {
-        std::minstd_rand rng(uint32_t(first_seed + w));
-        const std::string bb = random_genome(backbone_len, rng);
-        for (int32_t r = 0; r < num_reads; r++)
+    // windows are independent (one generator per window): chunks of windows
+    // are generated on host threads, then packed in window order
+    const int32_t chunk = 512;
+    const int32_t nchunks = (n + chunk - 1) / chunk;
+    std::vector<std::string> text(size_t(std::max(nchunks, 0)));
+    auto gen = [&](int32_t c) {
+        std::string& out = text[size_t(c)];
+        for (int32_t w = c * chunk; w < std::min(n, (c + 1) * chunk); w++)
         {
-            const std::string s = (r == 0) ? bb : mutate(bb, rng, max_mut, max_ins, max_del);
-            if (off + int64_t(s.size()) > bases_cap)
-                return -1;
-            std::memcpy(bases_out + off, s.data(), s.size());
-            lens_out[size_t(w) * num_reads + r] = int32_t(s.size());
-            off += int64_t(s.size());
+            std::minstd_rand rng(uint32_t(first_seed + w));
+            const std::string bb = random_genome(backbone_len, rng);
+            for (int32_t r = 0; r < num_reads; r++)
+            {
+                const std::string s = (r == 0) ? bb : mutate(bb, rng, max_mut, max_ins, max_del);
+                out += s;
+                lens_out[size_t(w) * num_reads + r] = int32_t(s.size());
+            }
         }
+    };
+    const int32_t nth = std::max(1, std::min<int32_t>(nchunks, int32_t(std::min(16u, std::thread::hardware_concurrency()))));
+    std::vector<std::thread> th;
+    for (int32_t t = 0; t < nth; t++)
+        th.emplace_back([&, t] {
+            for (int32_t c = t; c < nchunks; c += nth)
+                gen(c);
+        });
+    for (auto& t : th)
+        t.join();
+    int64_t off = 0;
+    for (const auto& s : text)
+    {
+        if (off + int64_t(s.size()) > bases_cap)
+            return -1;
+        std::memcpy(bases_out + off, s.data(), s.size());
+        off += int64_t(s.size());
     }
     return off;
 }

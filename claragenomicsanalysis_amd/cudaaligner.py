@@ -145,6 +145,12 @@ class CudaAlignerBatch:
         _check(self._lib.gwamd_aligner_align_all(self._handle))
         self._synced = False
 
+    def sync_alignments(self):
+        """Aligner::sync_alignments (aligner.hpp:58): waits for align_all and
+        fills the alignments' states (aligner_global.cpp:161-191)."""
+        _check(self._lib.gwamd_aligner_sync_alignments(self._handle))
+        self._synced = True
+
     def num_alignments(self):
         return self._lib.gwamd_aligner_num_alignments(self._handle)
 

@@ -215,6 +215,22 @@ class CudaPoaBatch:
                 covs.append([])
         return cons, covs, [status[i] for i in range(n)]
 
+    def get_consensus_raw(self):
+        """Batch::get_consensus (D2H + the C++ result vectors) without building
+        Python strings: returns (status int32[n], lengths int32[n], consensus
+        base address, coverage base address, stride).  The buffers stay valid
+        until the next generate_poa / reset."""
+        n = self.total_poas
+        status = np.zeros(max(n, 1), np.int32)
+        lens = np.zeros(max(n, 1), np.int32)
+        cbase, vbase, stride = C.c_void_p(), C.c_void_p(), C.c_int32()
+        rc = _check(self._lib.gwamd_poa_get_consensus(
+            self._handle, status.ctypes.data_as(C.POINTER(C.c_int32)), lens.ctypes.data_as(C.POINTER(C.c_int32)),
+            C.byref(cbase), C.byref(vbase), C.byref(stride)))
+        if rc == OUTPUT_TYPE_UNAVAILABLE:
+            raise RuntimeError("Output type not requested during batch initialization")
+        return status[:n], lens[:n], cbase.value, vbase.value, stride.value
+
     def get_msa(self):
         """cudapoa.pyx:207-224: (list of per-window MSA row lists, status list)."""
         n = self.total_poas
@@ -301,8 +317,115 @@ class CudaPoaBatch:
         self._lib.gwamd_poa_get_capacity(self._handle, C.byref(nb), C.byref(mp))
         return nb.value, mp.value
 
+    def get_grid(self):
+        """(scratch slots, resident workgroups on the device) of the persistent
+        grid; resident 0 means the global-memory kernel (one workgroup per window)."""
+        sl, rs = C.c_int32(), C.c_int32()
+        self._lib.gwamd_poa_get_grid(self._handle, C.byref(sl), C.byref(rs))
+        return sl.value, rs.value
+
     def reset(self):
         self._lib.gwamd_poa_reset(self._handle)
+
+
+class CudaPoaMultiBatch:
+    """Concurrent multi-batch driver (reference cudapoa/benchmarks/multi_batch.hpp:30-215):
+    num_batches batches, each on its own HIP stream and host thread, fed windows
+    in order under a mutex; consensus output.  mem_per_batch 0 takes 0.9 x free
+    device memory / num_batches, as the reference does."""
+
+    def __init__(self, max_sequences_per_poa, max_sequence_size, num_batches=2, mem_per_batch=0, device_id=0,
+                 gap_score=-8, mismatch_score=-6, match_score=8, cuda_banded_alignment=False,
+                 alignment_band_width=256, max_consensus_size=None):
+        self._lib = load_library()
+        _declare_multibatch(self._lib)
+        self._handle = C.c_void_p()
+        mx_cons = 2 * max_sequence_size if max_consensus_size is None else max_consensus_size
+        self.batch_size = BatchSize.make_full(max_sequence_size, mx_cons, 3 * max_sequence_size,
+                                              4 * max_sequence_size, alignment_band_width, max_sequences_per_poa)
+        self.stride = mx_cons
+        _check(self._lib.gwamd_poa_multibatch_create(C.byref(self._handle), device_id, num_batches,
+                                                     int(mem_per_batch), CONSENSUS, C.byref(self.batch_size),
+                                                     gap_score, mismatch_score, match_score,
+                                                     int(bool(cuda_banded_alignment))))
+
+    def __del__(self):
+        h = getattr(self, "_handle", None)
+        if h is not None and h.value:
+            self._lib.gwamd_poa_multibatch_destroy(h)
+            self._handle = None
+
+    def process_packed(self, bases, read_lens, reads_per_window, out=None):
+        """bases: uint8 array of all reads back to back; read_lens: int32 per read;
+        reads_per_window: reads of each window, in order.  Returns (status, lengths,
+        consensus uint8[n, stride], coverage uint16[n, stride]); pass `out` (a tuple
+        from an earlier call of the same size) to reuse the output arrays."""
+        read_lens = np.ascontiguousarray(read_lens, dtype=np.int32).ravel()
+        rpw = np.asarray(reads_per_window, dtype=np.int64).ravel()
+        n = len(rpw)
+        first = np.zeros(n + 1, np.int64)
+        np.cumsum(rpw, out=first[1:])
+        off = np.zeros(len(read_lens), np.int64)
+        if len(read_lens) > 1:
+            np.cumsum(read_lens[:-1], out=off[1:])
+        bases = np.ascontiguousarray(bases, dtype=np.uint8)
+        if out is None:
+            out = (np.zeros(n, np.int32), np.zeros(n, np.int32), np.zeros((n, self.stride), np.uint8),
+                   np.zeros((n, self.stride), np.uint16))
+        status, lens, cons, cov = out
+        self._inputs = (bases, read_lens, first, off)
+        _check(self._lib.gwamd_poa_multibatch_process(
+            self._handle, bases.ctypes.data, off.ctypes.data, read_lens.ctypes.data, first.ctypes.data, n,
+            status.ctypes.data, lens.ctypes.data, cons.ctypes.data, cov.ctypes.data, self.stride))
+        return out
+
+    def process(self, windows):
+        """windows: list of lists of reads (str/bytes).  Returns (consensus, coverage, status) lists."""
+        data = [[r.encode() if isinstance(r, str) else bytes(r) for r in w] for w in windows]
+        flat = b"".join(b"".join(w) for w in data)
+        lens = np.array([len(r) for w in data for r in w], np.int32)
+        rpw = [len(w) for w in data]
+        status, ln, cons, cov = self.process_packed(np.frombuffer(flat, np.uint8), lens, rpw)
+        cs = [cons[i, :ln[i]].tobytes().decode() for i in range(len(data))]
+        cv = [cov[i, :ln[i]].tolist() for i in range(len(data))]
+        return cs, cv, status.tolist()
+
+    def info(self):
+        """(batches, the most windows one batch took, generate_poa calls) of the last process."""
+        a, b, c = C.c_int32(), C.c_int32(), C.c_int32()
+        self._lib.gwamd_poa_multibatch_info(self._handle, C.byref(a), C.byref(b), C.byref(c))
+        return a.value, b.value, c.value
+
+
+def multibatch_file_assembly(filename, num_batches=2, total_windows=-1):
+    """MultiBatch(num_batches, filename, total_windows).process_batches().assembly()
+    (Test_CudapoaBatchEnd2End.cu:55-69)."""
+    L = load_library()
+    _declare_multibatch(L)
+    n = C.c_int64()
+    _check(L.gwamd_poa_multibatch_run_file(str(filename).encode(), num_batches, total_windows, None, 0, C.byref(n)))
+    buf = C.create_string_buffer(n.value + 1)
+    _check(L.gwamd_poa_multibatch_run_file(str(filename).encode(), num_batches, total_windows, buf, n.value,
+                                           C.byref(n)))
+    return buf.raw[:n.value].decode()
+
+
+def _declare_multibatch(L):
+    if getattr(L, "_mb_declared", False):
+        return
+    vp, i8, i16, i32, i64, sz = C.c_void_p, C.c_int8, C.c_int16, C.c_int32, C.c_int64, C.c_size_t
+    P = C.POINTER
+    L.gwamd_poa_multibatch_create.restype = i32
+    L.gwamd_poa_multibatch_create.argtypes = [P(vp), i32, i32, sz, i8, vp, i16, i16, i16, i32]
+    L.gwamd_poa_multibatch_destroy.restype = None
+    L.gwamd_poa_multibatch_destroy.argtypes = [vp]
+    L.gwamd_poa_multibatch_process.restype = i32
+    L.gwamd_poa_multibatch_process.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, i32]
+    L.gwamd_poa_multibatch_info.restype = i32
+    L.gwamd_poa_multibatch_info.argtypes = [vp, P(i32), P(i32), P(i32)]
+    L.gwamd_poa_multibatch_run_file.restype = i32
+    L.gwamd_poa_multibatch_run_file.argtypes = [C.c_char_p, i32, i32, vp, i64, P(i64)]
+    L._mb_declared = True
 
 
 # --- window batching (cudapoa/include/.../utils.hpp:48-66, cudapoa/src/utils.cu:24-138) ---

@@ -58,6 +58,30 @@ def gather_consensus(strings, width, device=None):
     return out
 
 
+def gather_rows(rows, device=None):
+    """Gather every rank's uint8 row array (same shape on every rank) to rank 0
+    in rank order: returns the concatenated numpy array on rank 0, None
+    elsewhere.  Used for config E's packed [len | status | consensus] rows,
+    so no per-window Python strings are built on either side."""
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    t = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.uint8))
+    if device is not None:
+        t = t.to(device)
+    parts = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+    dist.gather(t, parts, dst=0)
+    if rank != 0:
+        return None
+    return np.concatenate([p.cpu().numpy() for p in parts], axis=0)
+
+
+def stream_window_range(rank, steps, windows_per_step):
+    """Config E: first seed and count of a rank's windows (steps x windows_per_step
+    per rank, seeds 1 + rank * count ...; 20 x 6250 = 125k per rank)."""
+    n = steps * windows_per_step
+    return 1 + rank * n, n
+
+
 def window_cost(group):
     """DP cells of a window up to a constant: (reads - 1) x (longest read)^2
     (each read is aligned to a graph about as long as the reads)."""

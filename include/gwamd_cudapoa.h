@@ -18,6 +18,10 @@
  *   gwamd_poa_get_graphs            Batch::get_graphs                              batch.hpp:195-196
  *   gwamd_poa_batch_id              Batch::batch_id                                batch.hpp:201
  *   gwamd_poa_reset                 Batch::reset                                   batch.hpp:204
+ *   gwamd_poa_multibatch_create     MultiBatch(num_batches, ...)     benchmarks/multi_batch.hpp:36-58
+ *   gwamd_poa_multibatch_process    MultiBatch::process_batches      benchmarks/multi_batch.hpp:64-171
+ *   gwamd_poa_multibatch_run_file   MultiBatch(file) + process_batches + assembly
+ *                                                                    Test_CudapoaBatchEnd2End.cu:55-69
  *
  * Extra entry points (no reference counterpart; used by bench.py): split
  * generate_poa into its H2D copy and its kernel launch, and read per-window
@@ -126,6 +130,12 @@ int32_t gwamd_poa_set_spoa_accurate(gwamd_poa_batch* batch, int32_t on);
 /* Device bytes allocated by the batch and its window capacity (max_poas). */
 int32_t gwamd_poa_get_capacity(const gwamd_poa_batch* batch, int64_t* device_bytes, int32_t* max_poas);
 
+/* Persistent grid of the batch: scratch slots (= workgroups launched when the
+ * batch holds more windows than slots; each workgroup then dequeues windows
+ * heaviest first) and the device's resident workgroup count for the planned
+ * kernel (0: global-memory kernel, one workgroup per window, slots = max_poas). */
+int32_t gwamd_poa_get_grid(const gwamd_poa_batch* batch, int32_t* slots, int32_t* resident);
+
 /* BatchBlock::estimate_max_poas (allocate_block.hpp:364-401) for a
  * BatchSize(max_seq_sz, max_seq_per_poa, band_width); free_device_memory 0
  * queries the current device. */
@@ -146,6 +156,34 @@ int32_t gwamd_poa_get_multi_batch_sizes(const int32_t* group_max_len, const int3
                                         float quota, int32_t mismatch, int32_t gap, int32_t match,
                                         int32_t* num_batches, int32_t* batch_max_seq, int32_t* batch_num_reads,
                                         int32_t* group_batch, int32_t* group_rank);
+
+/* ---- Concurrent multi-batch driver (cudapoa/benchmarks/multi_batch.hpp) ----
+ * num_batches batches of the given BatchSize, each on its own HIP stream and
+ * host thread, mem_per_batch device bytes each (0: 0.9 x free / num_batches).
+ * output_mask must include consensus. */
+typedef struct gwamd_poa_multibatch gwamd_poa_multibatch;
+int32_t gwamd_poa_multibatch_create(gwamd_poa_multibatch** out, int32_t device_id, int32_t num_batches,
+                                    size_t mem_per_batch, int8_t output_mask, const gwamd_poa_batch_size* batch_size,
+                                    int16_t gap_score, int16_t mismatch_score, int16_t match_score,
+                                    int32_t cuda_banded_alignment);
+void gwamd_poa_multibatch_destroy(gwamd_poa_multibatch* mb);
+/* Runs num_windows windows through the batches.  Window w holds reads
+ * first_read[w] .. first_read[w+1]-1 (first_read has num_windows+1 entries);
+ * read r is bases[read_off[r] .. read_off[r]+read_len[r]).  Host bytes are
+ * read while the call runs only.  Outputs per window (NULL arrays are
+ * skipped): status[w] (StatusType), cons_len[w], consensus at
+ * cons + w*stride, coverage at cov + w*stride.  Blocks until done. */
+int32_t gwamd_poa_multibatch_process(gwamd_poa_multibatch* mb, const char* bases, const int64_t* read_off,
+                                     const int32_t* read_len, const int64_t* first_read, int32_t num_windows,
+                                     int32_t* status, int32_t* cons_len, char* cons, uint16_t* cov, int32_t stride);
+/* Batches, the most windows one batch took, generate_poa calls of the last process. */
+int32_t gwamd_poa_multibatch_info(const gwamd_poa_multibatch* mb, int32_t* num_batches, int32_t* max_poas_per_batch,
+                                  int32_t* rounds);
+/* The reference's end-to-end flow: MultiBatch(num_batches, filename,
+ * total_windows), process_batches(), assembly().  Writes up to capacity bytes
+ * of the assembly and its full length to *length. */
+int32_t gwamd_poa_multibatch_run_file(const char* filename, int32_t num_batches, int32_t total_windows,
+                                      char* assembly, int64_t capacity, int64_t* length);
 
 #ifdef __cplusplus
 }

@@ -138,10 +138,12 @@ def poa_window(reads, weights=None, gap=-8, mismatch=-6, match=8, banded=False, 
 
 
 def poa_batch(windows, nthreads=0, gap=-8, mismatch=-6, match=8, banded=False, band_width=256, score_bits=16,
-              max_nodes=None, max_consensus=None, max_seqs=None, msa=False, spoa_accurate=False):
+              max_nodes=None, max_consensus=None, max_seqs=None, msa=False, spoa_accurate=False, coverage=False):
     """Run many windows (list of lists of bytes) on all host cores (OpenMP).
     Returns (consensus list, status array, cells array, threads used); with
-    msa=True the first element is the list of MSA row lists instead."""
+    msa=True the first element is the list of MSA row lists instead; with
+    coverage=True (consensus only) the coverage lists are returned after the
+    status array: (consensus, status, coverage, cells, threads)."""
     flat = []
     lens = []
     first = []
@@ -194,6 +196,9 @@ def poa_batch(windows, nthreads=0, gap=-8, mismatch=-6, match=8, banded=False, b
             rows.append(win)
         return rows, status, cells, used
     out = [bytes(cons[i * max_consensus:i * max_consensus + clen[i]]).decode() for i in range(nw)]
+    if coverage:
+        covs = [cov[i * max_consensus:i * max_consensus + clen[i]].tolist() for i in range(nw)]
+        return out, status, covs, cells, used
     return out, status, cells, used
 
 

@@ -345,3 +345,60 @@ def test_serialize_graph_case(banded):
     msa, mst = b.get_msa()
     assert (mst[0], msa[0]) == (r.status, oracle.poa_window(wins[0], banded=banded, msa=True, max_nodes=(4 if banded else 3) * 1024,
                                                             max_consensus=2048, max_seqs=500).msa)
+
+
+# Persistent grid and launch order (poa_batch.cpp plan_launch_order): with
+# GWAMD_POA_SLOTS the batch gets fewer scratch slots than windows, so every
+# workgroup dequeues several windows (heaviest first) and reuses its slot's
+# scratch; GWAMD_LAUNCH_ORDER_CUS plans the snake order for a 2-CU device, so
+# batches far smaller than the real CU count run reordered.  Every output stays
+# bit-exact per window, and a second generate (dequeue counter reset) repeats it.
+@pytest.mark.parametrize("mode", ["full", "full_msa", "banded", "banded_msa", "v1", "full_spoa"])
+@pytest.mark.parametrize("grid", ["slots3", "cus2", "slots5_cus2"])
+def test_persistent_grid_and_launch_order(mode, grid, monkeypatch):
+    monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    if "slots" in grid:
+        monkeypatch.setenv("GWAMD_POA_SLOTS", grid.split("_")[0][5:])
+    else:
+        monkeypatch.delenv("GWAMD_POA_SLOTS", raising=False)
+    if "cus" in grid:
+        monkeypatch.setenv("GWAMD_LAUNCH_ORDER_CUS", "2")
+    else:
+        monkeypatch.delenv("GWAMD_LAUNCH_ORDER_CUS", raising=False)
+    if mode == "v1":
+        monkeypatch.setenv("GWAMD_POA_KERNEL", "v1")
+    banded = mode.startswith("banded")
+    msa = mode.endswith("msa")
+    # windows of very different cost, so the heaviest-first order is not the window order
+    wins = synth.poa_windows(901, 6, 120, 6, 8, 8, 8)
+    wins += synth.poa_windows(911, 5, 500, 10, 25, 25, 25)
+    wins += synth.poa_windows(921, 6, 250, 4, 12, 12, 12)
+    wins.append([b"ACGT", b"ACGA"])
+    wins.append([b"GATTACA" * 40] + [b"GATTACA" * 40 + b"T"] * 7)
+    max_seq = 600
+    b = run_gpu(wins, max_seq, 10, banded=banded, bw=256, output_type="msa" if msa else "consensus",
+                spoa_accurate=(mode == "full_spoa"))
+    slots, resident = b.get_grid()
+    if mode == "v1":
+        assert resident == 0 and b.kernel_variant() == 1
+    else:
+        assert b.kernel_variant() == (3 if banded else 2)
+        if "slots" in grid:
+            assert slots < len(wins)
+    sbits = b.get_types()[0]
+    for rep in range(2):
+        if rep:
+            b.generate_poa()
+        if msa:
+            got, st = b.get_msa()
+        else:
+            cons, cov, st = b.get_consensus()
+            got = list(zip(cons, cov))
+        graphs, gst = b.get_graphs()
+        for i, w in enumerate(wins):
+            r = run_oracle(w, max_seq, 10, banded=banded, bw=256, msa=msa, score_bits=sbits, want_graph=True,
+                           spoa_accurate=(mode == "full_spoa"))
+            want = r.msa if msa else (r.consensus, r.coverage)
+            assert (st[i], got[i]) == (r.status, want), (mode, grid, rep, i)
+            expect = {(src, v): wt for v, ins in enumerate(r.graph["in"]) for (src, wt) in ins}
+            assert {(u, v): graphs[i].weight(u, v) for (u, v) in graphs[i].edges} == expect, (mode, grid, rep, i)

@@ -99,3 +99,54 @@ def test_gather_sharded_restores_window_order():
     for p in procs:
         p.join(timeout=60)
     assert got == ["C%d" % i for i in range(7)]
+
+
+def _stream_worker(rank, world, port, out):
+    # config E's rank partition and gather (bench.py bench_stream): rank r owns
+    # seeds stream_window_range(r, steps, per_step); its consensus rows
+    # [len | status | bytes] are gathered to rank 0 in rank order
+    import numpy as np
+    from claragenomicsanalysis_amd import synth
+    from oracle import oracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    first, n = shard.stream_window_range(rank, 2, 3)
+    wins = synth.poa_windows(first, n, 120, 5, 6, 6, 6)
+    cons, status, cells, _ = oracle.poa_batch(wins, max_nodes=600, max_consensus=400, max_seqs=5)
+    rows = np.zeros((n, 8 + 400), np.uint8)
+    for i, c in enumerate(cons):
+        rows[i, :4] = np.frombuffer(np.int32(len(c)).tobytes(), np.uint8)
+        rows[i, 4:8] = np.frombuffer(np.int32(status[i]).tobytes(), np.uint8)
+        rows[i, 8:8 + len(c)] = np.frombuffer(c.encode(), np.uint8)
+    got = shard.gather_rows(rows)
+    if rank == 0:
+        out.put(got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_stream_partition_and_gather_world2_gloo():
+    import numpy as np
+    from claragenomicsanalysis_amd import synth
+    from oracle import oracle
+    assert [shard.stream_window_range(r, 20, 6250) for r in range(8)] == [(1 + 125000 * r, 125000)
+                                                                          for r in range(8)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stream_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    # the gathered rows are seeds 1..12 in order, as one rank would have computed them
+    wins = synth.poa_windows(1, 12, 120, 5, 6, 6, 6)
+    cons, status, _, _ = oracle.poa_batch(wins, max_nodes=600, max_consensus=400, max_seqs=5)
+    assert got.shape == (12, 408)
+    lens = got[:, :4].copy().view(np.int32).ravel()
+    st = got[:, 4:8].copy().view(np.int32).ravel()
+    assert st.tolist() == [int(s) for s in status]
+    assert [got[i, 8:8 + lens[i]].tobytes().decode() for i in range(12)] == cons
