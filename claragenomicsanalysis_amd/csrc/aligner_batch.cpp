@@ -653,6 +653,47 @@ int32_t gwamd_aligner_get_cigar(gwamd_aligner* a, int32_t i, char* buf, int32_t 
 
 void gwamd_aligner_reset(gwamd_aligner* a) { a->impl->reset(); }
 
+int32_t gwamd_alignment_format(const char* query, int32_t query_length, const char* target, int32_t target_length,
+                               const int8_t* states, int32_t num_states, int32_t maximal_line_length,
+                               char* query_out, char* pairing_out, char* target_out, int32_t cap,
+                               int32_t* linebreak_after)
+{
+    return guarded_aln([&] {
+        ca::AlignmentImpl al(query, query_length, target, target_length);
+        std::vector<ca::AlignmentState> st(size_t(std::max(num_states, 0)));
+        for (int32_t k = 0; k < num_states; k++)
+            st[size_t(k)] = static_cast<ca::AlignmentState>(states[k]);
+        al.set_alignment(std::move(st));
+        const ca::FormattedAlignment f = al.format_alignment(maximal_line_length);
+        if (linebreak_after)
+            *linebreak_after = f.linebreak_after;
+        const int32_t n = int32_t(f.query.size());
+        if (n < cap)
+        {
+            for (auto pr : {std::make_pair(query_out, &f.query), std::make_pair(pairing_out, &f.pairing),
+                            std::make_pair(target_out, &f.target)})
+                if (pr.first)
+                    std::memcpy(pr.first, pr.second->c_str(), pr.second->size() + 1);
+        }
+        return n;
+    });
+}
+
+int32_t gwamd_alignment_cigar(const int8_t* states, int32_t num_states, char* buf, int32_t cap)
+{
+    return guarded_aln([&] {
+        ca::AlignmentImpl al("", 0, "", 0);
+        std::vector<ca::AlignmentState> st(size_t(std::max(num_states, 0)));
+        for (int32_t k = 0; k < num_states; k++)
+            st[size_t(k)] = static_cast<ca::AlignmentState>(states[k]);
+        al.set_alignment(std::move(st));
+        const std::string c = al.convert_to_cigar();
+        if (buf && int32_t(c.size()) < cap)
+            std::memcpy(buf, c.c_str(), c.size() + 1);
+        return int32_t(c.size());
+    });
+}
+
 int32_t gwamd_aligner_upload(gwamd_aligner* a)
 {
     return guarded_aln([&] {

@@ -18,6 +18,9 @@
  *   gwamd_aligner_get_sequences   Alignment::get_query/target_sequence     alignment.hpp:53-56
  *   gwamd_aligner_get_cigar       Alignment::convert_to_cigar              alignment.hpp:62
  *   gwamd_aligner_reset           Aligner::reset                           aligner.hpp:79
+ *   gwamd_alignment_format        Alignment::format_alignment              alignment.hpp:82-85
+ *                                 (AlignmentImpl over given states,        alignment_impl.cpp:75-112)
+ *   gwamd_alignment_cigar         Alignment::convert_to_cigar              alignment_impl.cpp:47-73
  *
  * Extra entry points (bench.py): split align_all into upload / launch /
  * download and read the raw device paths.
@@ -77,6 +80,17 @@ int32_t gwamd_aligner_get_sequences(gwamd_aligner* aligner, int32_t i, const cha
 /* CIGAR of alignment i, NUL-terminated if it fits; returns its length. */
 int32_t gwamd_aligner_get_cigar(gwamd_aligner* aligner, int32_t i, char* buf, int32_t cap);
 void gwamd_aligner_reset(gwamd_aligner* aligner);
+
+/* AlignmentImpl(query, target) with the given AlignmentState sequence (start ->
+ * end): format_alignment(maximal_line_length) writes the three NUL-terminated
+ * rows (query with '-', pairing '|'/'x'/' ', target with '-') when their
+ * length is below cap; returns that length.  No device work. */
+int32_t gwamd_alignment_format(const char* query, int32_t query_length, const char* target, int32_t target_length,
+                               const int8_t* states, int32_t num_states, int32_t maximal_line_length,
+                               char* query_out, char* pairing_out, char* target_out, int32_t cap,
+                               int32_t* linebreak_after);
+/* convert_to_cigar of the given AlignmentState sequence; returns its length. */
+int32_t gwamd_alignment_cigar(const int8_t* states, int32_t num_states, char* buf, int32_t cap);
 
 /* bench.py helpers: align_all == upload + launch + download. */
 int32_t gwamd_aligner_upload(gwamd_aligner* aligner);

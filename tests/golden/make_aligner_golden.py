@@ -41,6 +41,23 @@ def cigar_cases():
     return out
 
 
+def formatted_cases():
+    # cudaaligner/tests/Test_AlignmentImpl.cpp:54-127: query, target, the
+    # AlignmentState sequence (0 match, 1 mismatch, 2 insertion, 3 deletion;
+    # cudaaligner.hpp:46-52), the formatted triple and the CIGAR
+    M, X, I, D = 0, 1, 2, 3
+    return [
+        {"query": "AAAA", "target": "TTATG", "states": [X, X, M, X, I],
+         "formatted": ["AAAA-", "xx|x ", "TTATG"], "cigar": "4M1I"},
+        {"query": "CGATAATG", "target": "CATAA", "states": [D, X, M, M, M, M, D, D],
+         "formatted": ["CGATAATG", " x||||  ", "-CATAA--"], "cigar": "1D5M2D"},
+        {"query": "GTTAG", "target": "AAGTCTAGAA", "states": [I, I, M, M, I, M, M, M, I, I],
+         "formatted": ["--GT-TAG--", "  || |||  ", "AAGTCTAGAA"], "cigar": "2I2M1I3M2I"},
+        {"query": "GTTACA", "target": "GATTCA", "states": [M, I, M, M, D, M, M],
+         "formatted": ["G-TTACA", "| || ||", "GATT-CA"], "cigar": "1M1I2M1D2M"},
+    ]
+
+
 def pattern_cases():
     # cudaaligner/tests/Test_HirschbergMyers.cu:93-140 (A=0, C=1, T=2, G=3; +4 reverse)
     q = "AACCGGTTACGTACGT" "AAACCCGGGTTTACGT" "AAACCCGGGTTTACG"
@@ -114,7 +131,8 @@ def add_cases_ukkonen():
 
 def main():
     data = {"cigar": cigar_cases(), "patterns": pattern_cases(), "distances": distance_cases(),
-            "add_alignment": add_cases(), "ukkonen": ukkonen_cases(), "add_alignment_ukkonen": add_cases_ukkonen()}
+            "add_alignment": add_cases(), "ukkonen": ukkonen_cases(), "add_alignment_ukkonen": add_cases_ukkonen(),
+            "formatted": formatted_cases()}
     with open(os.path.join(HERE, "aligner_kat.json"), "w") as f:
         json.dump(data, f, indent=1)
     print("wrote", os.path.join(HERE, "aligner_kat.json"))

@@ -92,8 +92,43 @@ def test_cudapoa_file_consensus(tmp_path, banded):
     assert r.returncode == 0, r.stderr
     lines = r.stdout.split("\n")[:-1]
     assert len(lines) == len(wins)
-    # windows are printed in get_multi_batch_sizes bin order (main.cpp:200-280)
-    assert sorted(lines) == sorted(_oracle_consensus(w, banded).consensus for w in wins)
+    # one batch here, so the printed order is the input order (main.cpp:200-280)
+    assert lines == [_oracle_consensus(w, banded).consensus for w in wins]
+
+
+@pytest.mark.gpu
+def test_cudapoa_print_order_follows_batch_bins(tmp_path):
+    # main.cpp:189-289: windows are binned by get_multi_batch_sizes (utils.cu:24-138)
+    # and printed batch by batch in each batch's group order.  A small memory
+    # quota (-R) puts windows of different sizes into different capacity bins,
+    # so the printed order differs from the input order; the expected order
+    # comes from the same binning (C ABI) at the device's free memory.
+    from claragenomicsanalysis_amd.cudapoa import get_multi_batch_sizes
+    from claragenomicsanalysis_amd._lib import load_library
+    import ctypes as C
+    shapes = [(200, 4, 8), (2500, 6, 100), (900, 8, 40)]
+    wins = []
+    for k in range(3):
+        for j, (L, n, e) in enumerate(shapes):
+            wins += synth.poa_windows(131 + 10 * k + j, 1, L, n, e, e, e)
+    quota = 0.002
+    free, total = C.c_size_t(), C.c_size_t()
+    hip = C.CDLL("libamdhip64.so")
+    load_library()
+    assert hip.hipMemGetInfo(C.byref(free), C.byref(total)) == 0
+    groups = [[s.decode() for s in w] for w in wins]
+    plans = [get_multi_batch_sizes(groups, banded_alignment=True, msa_flag=False, band_width=256,
+                                   gpu_memory_usage_quota=quota, free_device_memory=int(free.value * f))
+             for f in (0.95, 1.0, 1.05)]
+    assert plans[0][1] == plans[1][1] == plans[2][1], "binning not stable around the free memory; adjust sizes"
+    order = [g for batch in plans[1][1] for g in batch]
+    assert order != list(range(len(wins))) and sorted(order) == list(range(len(wins)))
+    p = tmp_path / "windows.txt"
+    _write_cudapoa(p, wins)
+    r = _run(["-i", str(p), "-R", str(quota)])
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.split("\n")[:-1]
+    assert lines == [_oracle_consensus(wins[g], True).consensus for g in order]
 
 
 @pytest.mark.gpu
@@ -105,7 +140,7 @@ def test_max_groups_repeats_windows(tmp_path):
     assert r.returncode == 0, r.stderr
     lines = r.stdout.split("\n")[:-1]
     assert len(lines) == 7
-    assert sorted(lines) == sorted(_oracle_consensus(wins[i % 3], True).consensus for i in range(7))
+    assert lines == [_oracle_consensus(wins[i % 3], True).consensus for i in range(7)]
 
 
 @pytest.mark.gpu
@@ -129,6 +164,6 @@ def test_fasta_msa_and_dot(tmp_path):
         res = oracle.poa_window(w, banded=True, band_width=256, msa=True, max_nodes=(4 * max_seq + 3) // 4 * 4,
                                 max_consensus=2 * max_seq, max_seqs=len(w))
         expect += [m.decode() if isinstance(m, bytes) else m for m in res.msa]
-    assert sorted(rows) == sorted(expect)
+    assert rows == expect  # one batch: windows in input order, rows in read order
     text = dot.read_text()
     assert text.count("digraph") == len(wins)
