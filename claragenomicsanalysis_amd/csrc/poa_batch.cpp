@@ -186,6 +186,20 @@ public:
             scorebuf_alloc_ = 0;
 
         allocate(sz, sbytes, msa);
+        // pinned host staging for a full batch, as the reference's BatchBlock
+        // allocates it up front (allocate_block.hpp:84-118), so filling a
+        // batch never re-pins memory (capped; beyond the cap it grows)
+        {
+            const size_t cap_b = size_t(2) << 30;
+            const size_t in_b  = std::min(cap_b, size_t(max_poas_) * size_t(bs_.max_sequences_per_poa) *
+                                                    size_t(bs_.max_sequence_size) + 16);
+            h_seqs_.reserve(in_b, stream_);
+            h_wts_.reserve(in_b, stream_);
+            const size_t nseq = std::min(cap_b / 8, size_t(max_poas_) * size_t(bs_.max_sequences_per_poa));
+            h_len_.reserve(nseq * 4, stream_);
+            h_off_.reserve(nseq * 8, stream_);
+            h_win_.reserve(size_t(max_poas_) * sizeof(gwamd::poa::WindowDesc), stream_);
+        }
         bid_ = batches_++;
         reset();
     }
@@ -591,7 +605,7 @@ private:
             if (std::sscanf(sh, "%d,%d", &c, &n) == 2)
             {
                 const bool known = (n == 1 && (c == 8 || c == 16 || c == 24 || c == 32)) ||
-                                   (c == 8 && n >= 2 && n <= 4) || (c == 16 && n == 4);
+                                   (c == 8 && n >= 2 && n <= 4) || (c == 16 && n == 4) || (c == 4 && n == 4);
                 if (!known)
                     throw std::invalid_argument("GWAMD_POA_LDS_SHAPE: unsupported columns/waves pair");
                 cpl = c, nw = n;

@@ -353,6 +353,19 @@ __device__ __forceinline__ uint32_t opaque_u32(uint32_t v)
     return v;
 }
 __device__ __forceinline__ uint32_t pk_bcast(int v) { return (uint32_t(uint16_t(v)) * 0x10001u); }
+// (lo, max(hi, lo)): one v_pk_max_i16 with op_sel_hi selecting src1's low half
+__device__ __forceinline__ uint32_t pk_max_lo_into_hi(uint32_t a)
+{
+    const pk_s16x2 v = __builtin_bit_cast(pk_s16x2, a);
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(v, __builtin_shufflevector(v, v, 0, 0)));
+}
+// max(a, (c.hi, c.hi)): the carry of the previous register pair, via op_sel
+__device__ __forceinline__ uint32_t pk_max_hi_carry(uint32_t a, uint32_t c)
+{
+    const pk_s16x2 v = __builtin_bit_cast(pk_s16x2, c);
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(pk_s16x2, a),
+                                                                  __builtin_shufflevector(v, v, 1, 1)));
+}
 
 // Global loads on the rare far-predecessor paths are waited for inside their
 // branch: a value still in flight where the paths join makes the compiler wait
@@ -418,7 +431,7 @@ __device__ __forceinline__ void diag_src(const uint32_t (&P)[NR], uint32_t prev,
 #ifdef GWAMD_FWD_PROFILE
 struct FwdProf
 {
-    uint64_t t[4] = {0, 0, 0, 0};
+    uint64_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t m    = 0;
     __device__ void start() { m = __builtin_amdgcn_s_memtime(); }
     template <int I>
@@ -484,11 +497,20 @@ __device__ __forceinline__ int row_preds(const RowProg& P, WinGraph<SizeT> g, in
 template <int NR>
 __device__ __forceinline__ void load_row_pk(const int16_t* p, uint32_t (&P)[NR], uint32_t& prev)
 {
-#pragma unroll
-    for (int q = 0; q < NR / 4; q++)
+    if constexpr (NR % 4 == 0)
     {
-        const uint4 v = *reinterpret_cast<const uint4*>(p + 1 + 8 * q);
-        P[4 * q] = v.x, P[4 * q + 1] = v.y, P[4 * q + 2] = v.z, P[4 * q + 3] = v.w;
+#pragma unroll
+        for (int q = 0; q < NR / 4; q++)
+        {
+            const uint4 v = *reinterpret_cast<const uint4*>(p + 1 + 8 * q);
+            P[4 * q] = v.x, P[4 * q + 1] = v.y, P[4 * q + 2] = v.z, P[4 * q + 3] = v.w;
+        }
+    }
+    else
+    {
+        static_assert(NR == 2, "4 or a multiple of 8 cells per lane");
+        const uint2 v = *reinterpret_cast<const uint2*>(p + 1);
+        P[0] = v.x, P[1] = v.y;
     }
     prev = uint32_t(uint16_t(p[0]));
 }
@@ -512,7 +534,6 @@ __device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, con
     const uint32_t gap2 = pk_bcast(gap);
     const uint32_t one2 = opaque_u32(0x00010001u);
     const uint32_t two2 = opaque_u32(0x00020002u);
-    const uint32_t four2 = opaque_u32(0x00040004u);
     const int mask      = P.ring_mask;
     GWAMD_LDS int* prog          = (GWAMD_LDS int*)(shb + kShProg);
     GWAMD_LDS int16_t* bnd       = (GWAMD_LDS int16_t*)(shb + kShBnd) + wave * (mask + 1);
@@ -588,6 +609,7 @@ __device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, con
             if (r + 2 <= V)
                 pv_b = row_preds<SizeT>(P, g, r + 2, rec_b, lane, np_b);
             const uint32_t rec_bb = P.rec[min(r + 3, V)];
+            GWAMD_FP_LAP(fp, 4);
 
             const uint32_t rec = rec_c;
             const int np       = np_c;
@@ -627,6 +649,7 @@ __device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, con
                              (uint32_t(uint16_t(ch1 == base ? s_eq : s_ne)) << 16);
                 }
             }
+            GWAMD_FP_LAP(fp, 5);
             // E values of predecessor row p for the lane's cells, and E_p[jb]
             auto load_pred = [&](int p, uint32_t(&Q)[NR], uint32_t& qprev) {
                 if (p == r - 1)
@@ -671,48 +694,63 @@ __device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, con
                 {
                     dg[i] = pk_add(dg[i], sig[i]);
                     vt[i] = pk_add(Pv[i], gap2);
-                    kd[i] = kv[i] = 0;
                 }
             }
-            for (int k = 1; k < np; k++)
-            {
-                uint32_t Q[NR], qprev, dq[NR];
-                load_pred(__builtin_amdgcn_readlane(pv, k), Q, qprev);
-                {
-                    // column 0: first maximising predecessor slot
-                    const int pe = int(int16_t(qprev));
-                    c0kv         = pe > c0v ? k : c0kv;
-                    c0v          = max(c0v, pe);
-                }
-                diag_src<NR>(Q, qprev, dq);
-                const uint32_t kk = pk_bcast(k);
+            GWAMD_FP_LAP(fp, 6);
+            // in-lane prefix maximum: per register pair max(diag, vertical),
+            // then its low half into its high half, then the previous pair's
+            // high half into both (op_sel forms, no shifts or permutes)
+            auto prefix = [&]() {
 #pragma unroll
                 for (int i = 0; i < NR; i++)
                 {
-                    // running maxima with the first maximising predecessor slot
-                    const uint32_t d  = pk_add(dq[i], sig[i]);
-                    const uint32_t nd = pk_max(dg[i], d);
-                    kd[i]             = pk_mad(pk_min_u(pk_sub(nd, dg[i]), one2), pk_sub(kk, kd[i]), kd[i]);
-                    dg[i]             = nd;
-                    const uint32_t v  = pk_add(Q[i], gap2);
-                    const uint32_t nv = pk_max(vt[i], v);
-                    kv[i]             = pk_mad(pk_min_u(pk_sub(nv, vt[i]), one2), pk_sub(kk, kv[i]), kv[i]);
-                    vt[i]             = nv;
+                    const uint32_t s = pk_max_lo_into_hi(pk_max(dg[i], vt[i]));
+                    E[i]             = i == 0 ? s : pk_max_hi_carry(s, E[i - 1]);
                 }
-            }
-            // in-lane prefix maximum
+            };
+            if (np > 1)
             {
-                uint32_t c = 0x80008000u;
+                // rows with several predecessors track the first maximising
+                // slot of each cell, pre-scaled to the code layout: kd = 4 *
+                // slot, kv = 4 * slot + 1 (codes: 0 diagonal, 1 vertical,
+                // 2 horizontal, + slot << 2)
 #pragma unroll
                 for (int i = 0; i < NR; i++)
                 {
-                    const uint32_t dmax = pk_max(dg[i], vt[i]);
-                    uint32_t s          = pk_max(dmax, (dmax << 16) | 0x8000u);
-                    s                   = pk_max(s, c);
-                    E[i]                = s;
-                    c                   = __builtin_amdgcn_perm(s, s, 0x07060706u);
+                    kd[i] = 0;
+                    kv[i] = one2;
                 }
+                for (int k = 1; k < np; k++)
+                {
+                    uint32_t Q[NR], qprev, dq[NR];
+                    load_pred(__builtin_amdgcn_readlane(pv, k), Q, qprev);
+                    {
+                        // column 0: first maximising predecessor slot
+                        const int pe = int(int16_t(qprev));
+                        c0kv         = pe > c0v ? k : c0kv;
+                        c0v          = max(c0v, pe);
+                    }
+                    diag_src<NR>(Q, qprev, dq);
+                    const uint32_t kk4 = pk_bcast(4 * k);
+                    const uint32_t kk1 = pk_bcast(4 * k + 1);
+#pragma unroll
+                    for (int i = 0; i < NR; i++)
+                    {
+                        // running maxima with the first maximising predecessor slot
+                        const uint32_t d  = pk_add(dq[i], sig[i]);
+                        const uint32_t nd = pk_max(dg[i], d);
+                        kd[i]             = pk_mad(pk_min_u(pk_sub(nd, dg[i]), one2), pk_sub(kk4, kd[i]), kd[i]);
+                        dg[i]             = nd;
+                        const uint32_t v  = pk_add(Q[i], gap2);
+                        const uint32_t nv = pk_max(vt[i], v);
+                        kv[i]             = pk_mad(pk_min_u(pk_sub(nv, vt[i]), one2), pk_sub(kk1, kv[i]), kv[i]);
+                        vt[i]             = nv;
+                    }
+                }
+                prefix();
             }
+            else
+                prefix();
             const int m    = active ? int(int16_t(E[NR - 1] >> 16)) : kNeg;
             GWAMD_FP_LAP(fp, 0);
             const int incl = wave_incl_max_dpp(m);
@@ -786,27 +824,52 @@ __device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, con
             {
                 // codes: 0 diagonal, 1 vertical, 2 horizontal (+ slot << 2)
                 uint32_t code[NR];
-#pragma unroll
-                for (int i = 0; i < NR; i++)
+                if (np > 1)
                 {
-                    const uint32_t a   = pk_min_u(pk_sub(E[i], dg[i]), one2); // 0: diagonal match
-                    const uint32_t bb  = pk_min_u(pk_sub(E[i], vt[i]), one2); // 0: vertical match
-                    const uint32_t cv  = pk_mad(kv[i], four2, one2);          // 1 | kv << 2
-                    const uint32_t cvh = pk_mad(bb, pk_sub(two2, cv), cv);    // vertical or horizontal
-                    const uint32_t cd  = kd[i] << 2; // kd < 64: no cross-half carry
-                    code[i]            = pk_mad(a, pk_sub(cvh, cd), cd);
+#pragma unroll
+                    for (int i = 0; i < NR; i++)
+                    {
+                        const uint32_t a   = pk_min_u(pk_sub(E[i], dg[i]), one2); // 0: diagonal match
+                        const uint32_t bb  = pk_min_u(pk_sub(E[i], vt[i]), one2); // 0: vertical match
+                        const uint32_t cvh = pk_mad(bb, pk_sub(two2, kv[i]), kv[i]); // vertical or horizontal
+                        code[i]            = pk_mad(a, pk_sub(cvh, kd[i]), kd[i]);
+                    }
                 }
-#pragma unroll
-                for (int q = 0; q < NR / 4; q++)
+                else
                 {
-                    const uint4 ev = make_uint4(E[4 * q], E[4 * q + 1], E[4 * q + 2], E[4 * q + 3]);
-                    *reinterpret_cast<uint4*>(row + jb + kColShift + 1 + 8 * q) = ev;
+                    // one predecessor (slot 0): a * (1 + bb)
+#pragma unroll
+                    for (int i = 0; i < NR; i++)
+                    {
+                        const uint32_t a  = pk_min_u(pk_sub(E[i], dg[i]), one2);
+                        const uint32_t bb = pk_min_u(pk_sub(E[i], vt[i]), one2);
+                        code[i]           = pk_mad(a, bb, a);
+                    }
+                }
+                if constexpr (NR % 4 == 0)
+                {
+#pragma unroll
+                    for (int q = 0; q < NR / 4; q++)
+                    {
+                        const uint4 ev = make_uint4(E[4 * q], E[4 * q + 1], E[4 * q + 2], E[4 * q + 3]);
+                        *reinterpret_cast<uint4*>(row + jb + kColShift + 1 + 8 * q) = ev;
+                        if (spill_r)
+                            *reinterpret_cast<uint4*>(srow + jb + kColShift + 1 + 8 * q) = ev;
+                        const uint32_t w0 = __builtin_amdgcn_perm(code[4 * q + 1], code[4 * q], 0x06040200u);
+                        const uint32_t w1 = __builtin_amdgcn_perm(code[4 * q + 3], code[4 * q + 2], 0x06040200u);
+                        __builtin_nontemporal_store(uint64_t(w0) | (uint64_t(w1) << 32),
+                                                    reinterpret_cast<uint64_t*>(crow + jb + kColShift + 1 + 8 * q));
+                    }
+                }
+                else
+                {
+                    // 4 cells per lane: 8-byte E stores, one 4-byte code word
+                    const uint2 ev = make_uint2(E[0], E[1]);
+                    *reinterpret_cast<uint2*>(row + jb + kColShift + 1) = ev;
                     if (spill_r)
-                        *reinterpret_cast<uint4*>(srow + jb + kColShift + 1 + 8 * q) = ev;
-                    const uint32_t w0 = __builtin_amdgcn_perm(code[4 * q + 1], code[4 * q], 0x06040200u);
-                    const uint32_t w1 = __builtin_amdgcn_perm(code[4 * q + 3], code[4 * q + 2], 0x06040200u);
-                    __builtin_nontemporal_store(uint64_t(w0) | (uint64_t(w1) << 32),
-                                                reinterpret_cast<uint64_t*>(crow + jb + kColShift + 1 + 8 * q));
+                        *reinterpret_cast<uint2*>(srow + jb + kColShift + 1) = ev;
+                    __builtin_nontemporal_store(__builtin_amdgcn_perm(code[1], code[0], 0x06040200u),
+                                                reinterpret_cast<uint32_t*>(crow + jb + kColShift + 1));
                 }
             }
             if ((rec & (1u << 14)) && owner)
@@ -1061,7 +1124,7 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
 // update, topological sort, consensus, MSA) run on wave 0 while the other
 // waves wait at the next barrier.
 template <bool MSA, int CPL, int NW>
-__global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, Dims d, Scores sc)
+__global__ void __launch_bounds__(kWave * NW, NW >= 4 ? 4 : 1) poa_window_kernel_lds(Buffers b, Dims d, Scores sc)
 {
     using SizeT  = int16_t;
     extern __shared__ __align__(16) uint8_t lds[];
@@ -1250,8 +1313,9 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
                 ph.store(b.phase + size_t(w) * kPhases);
 #ifdef GWAMD_FWD_PROFILE
                 // cycles / 1000 so the 100 MHz tick scaling reads as kcycles*1e-5
-                const int slot[4] = {kPhBackbone, kPhAdd, kPhTopsort, kPhOutput};
-                for (int i = 0; i < 4; i++)
+                const int slot[8] = {kPhBackbone, kPhAdd, kPhTopsort, kPhOutput, kPhForward, kPhTraceback, kPhRowProg,
+                                     kPhTotal};
+                for (int i = 0; i < 8; i++)
                     b.phase[size_t(w) * kPhases + slot[i]] = int64_t(fp.t[i]);
 #endif
             }
@@ -1259,6 +1323,17 @@ __global__ void __launch_bounds__(kWave * NW) poa_window_kernel_lds(Buffers b, D
             b.cells[w]       = cells;
         }
     }
+#if defined(GWAMD_FWD_PROFILE) && defined(GWAMD_FWD_PROFILE_WAVE)
+    // diagnostic: another wave's section timers replace wave 0's
+    __syncthreads();
+    if (wave == GWAMD_FWD_PROFILE_WAVE && lane == 0 && b.phase)
+    {
+        const int slot[8] = {kPhBackbone, kPhAdd, kPhTopsort, kPhOutput, kPhForward, kPhTraceback, kPhRowProg,
+                             kPhTotal};
+        for (int i = 0; i < 8; i++)
+            b.phase[size_t(w) * kPhases + slot[i]] = int64_t(fp.t[i]);
+    }
+#endif
     if (b.head == nullptr)
         break;
     // next queue position; the LDS image is rewritten by the next window
@@ -1316,6 +1391,7 @@ extern "C" int gwamd_internal_poa_blocks_per_cu(const gwamd::poa::Dims* d, int s
     GWAMD_LDS_OCC(8, 3)
     GWAMD_LDS_OCC(8, 4)
     GWAMD_LDS_OCC(16, 4)
+    GWAMD_LDS_OCC(4, 4)
 #undef GWAMD_LDS_OCC
     return 0;
 }
@@ -1355,6 +1431,7 @@ extern "C" hipError_t gwamd_internal_poa_launch(const gwamd::poa::Buffers* b, co
         GWAMD_LDS_LAUNCH(8, 3)
         GWAMD_LDS_LAUNCH(8, 4)
         GWAMD_LDS_LAUNCH(16, 4)
+        GWAMD_LDS_LAUNCH(4, 4)
         return hipErrorInvalidConfiguration;
 #undef GWAMD_LDS_LAUNCH
     }

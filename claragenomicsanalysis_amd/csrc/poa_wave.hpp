@@ -215,14 +215,22 @@ __device__ __forceinline__ int dpp_max(int v, int ctrl, int row_mask)
 }
 
 // Inclusive max-scan over the wave with DPP (row_shr 1/2/4/8, row_bcast 15/31).
+// A lane with no source (outside the row, or a row masked off) keeps its own
+// value as the DPP "old" operand, and max(v, v) = v: no identity constant has
+// to be rematerialised for every step.
+// One v_max_i32_dpp per step, written in place (dst = both sources): a lane
+// whose DPP source is invalid is not written (bound_ctrl off).  The s_nop
+// gives the 2 wait states a DPP read needs after the VALU write of its source.
 __device__ __forceinline__ int wave_incl_max_dpp(int v)
 {
-    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x111, 0xf, 0xf, false));
-    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x112, 0xf, 0xf, false));
-    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x114, 0xf, 0xf, false));
-    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x118, 0xf, 0xf, false));
-    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x142, 0xa, 0xf, false));
-    v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x143, 0xc, 0xf, false));
+    asm volatile("s_nop 1\n\tv_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\tv_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\tv_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\tv_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\tv_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+                 "s_nop 1\n\tv_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+                 "s_nop 1"
+                 : "+v"(v));
     return v;
 }
 

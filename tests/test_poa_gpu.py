@@ -219,7 +219,7 @@ def test_lds_kernel_empty_and_tiny_reads():
         assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), i
 
 
-@pytest.mark.parametrize("shape", ["8,1", "16,1", "24,1", "32,1", "8,2", "8,3", "8,4", "16,4"])
+@pytest.mark.parametrize("shape", ["8,1", "16,1", "24,1", "32,1", "8,2", "8,3", "8,4", "16,4", "4,4"])
 def test_lds_forward_shapes(shape, monkeypatch):
     # every (columns per lane, waves per window) forward-pass shape; reads
     # longer than one sweep (NW*64*CPL columns) take several sweeps, and span /
