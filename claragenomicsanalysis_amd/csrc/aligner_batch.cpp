@@ -424,8 +424,15 @@ private:
         GWAMD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
         slots_ = std::max(1, per_cu * cus);
         if (algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS)
-            // base cases too wide for LDS, then the split scores of wide segments
-            slot_bytes_ = a16(a16(int64_t(stride_ + 1) * kLeafColBytes) + int64_t(stride_ + 1) * 4 + 64);
+        {
+            // base cases too wide for LDS, the split scores of wide segments
+            // and of packed ones, then the breadth-first frontier: at most
+            // 2 * (query + 1) segments (every leaf has a query row or is one
+            // of the target-only halves of a split)
+            front_cap_  = 2 * (max_q_ + 2);
+            front_off_  = a16(a16(int64_t(stride_ + 1) * kLeafColBytes) + int64_t(stride_ + 1 + kWave) * 4 + 64);
+            slot_bytes_ = a16(front_off_ + int64_t(front_cap_) * (2 * 8 + 2) + 64);
+        }
         else
         {
             // full matrix: pv, mv, score per (word, column)
@@ -451,6 +458,8 @@ private:
         a.max_matrix_elems = int64_t((max_q_ + 3) / 4) * (gwamd::aln::kFullMyers + 1);
         a.ws               = d_ws_;
         a.ws_slot_bytes    = slot_bytes_;
+        a.ws_front_off     = front_off_;
+        a.front_cap        = front_cap_;
         a.lds_target_off   = lds_target_off_;
         a.lds_pat_off      = lds_pat_off_;
         a.lds_scratch_off  = lds_scratch_off_;
@@ -472,6 +481,8 @@ private:
     int32_t stride_ = 0, max_result_ = 0;
     int32_t lds_target_off_ = 0, lds_pat_off_ = 0, lds_scratch_off_ = 0, lds_stack_off_ = 0, lds_bytes_ = 0;
     int32_t pat_words_ = 0, scratch_bytes_ = 0;
+    int64_t front_off_ = 0;
+    int32_t front_cap_ = 0;
     int32_t lds_seq2_off_ = 0, lds_tile_off_ = 0, tile_bytes_ = 0;
     int32_t slots_ = 1;
     int64_t slot_bytes_ = 0, device_bytes_ = 0;

@@ -51,6 +51,8 @@ struct Args
     // global workspace, one slot per resident workgroup
     uint8_t* ws;
     int64_t ws_slot_bytes;
+    int64_t ws_front_off;    // Hirschberg-Myers: frontier of the breadth-first recursion in the slot
+    int32_t front_cap;       //   entries per frontier buffer (two buffers, then one u16 split column each)
     // LDS layout (bytes)
     int32_t lds_target_off;
     int32_t lds_pat_off;     // [pat_words][8] u32: forward A C T G, reverse A C T G

@@ -419,17 +419,187 @@ __device__ void run_split(int nblk, const GWAMD_LDS uint32_t* pat, int pat_words
     }
 }
 
-struct Range
+// ---------------------------------------------------------------------------
+// Hirschberg + Myers, breadth first.
+//
+// The reference recursion (hirschberg_myers, :569-638) pops segments from a
+// LIFO stack, so it visits the recursion tree depth first and emits the base
+// cases from the last (rightmost) to the first.  A segment's split column
+// depends only on its own ranges, so the tree can be built level by level
+// instead: the frontier is the in-order list of the current segments; every
+// level computes the split column of each segment that is not a base case and
+// replaces it by its two halves; when only base cases are left they are
+// emitted from the last to the first, which is the reference's output order.
+// The stack never holds more than the recursion depth + 1 <= 16 entries for
+// queries of up to 16384 bases, so the reference's 64-entry overflow case
+// cannot occur and is not modelled.
+//
+// Building the tree by levels lets the many short segments of the deep levels
+// share a wave: a "pack" puts the forward and reverse halves of several
+// segments side by side in the lanes of one Myers block (one lane group per
+// half, one 32-row word per lane), with the carry look-ahead and the one-bit
+// shift cut at the group boundaries and the target letter read per lane.
+
+struct Seg16
 {
-    int32_t qb, qe, tb, te;
+    uint16_t qb, qe, tb, te;
 };
 
-__device__ __forceinline__ void put_range(GWAMD_LDS Range* p, int qb, int qe, int tb, int te)
+__device__ __forceinline__ uint2 seg_pack(int qb, int qe, int tb, int te)
 {
-    p->qb = qb;
-    p->qe = qe;
-    p->tb = tb;
-    p->te = te;
+    return make_uint2(uint32_t(qb) | (uint32_t(qe) << 16), uint32_t(tb) | (uint32_t(te) << 16));
+}
+
+// base case kinds (:577-611): 1 no target, 2 no query, 3 one query base,
+// 4 full Myers; 0: split
+__device__ __forceinline__ int base_kind(int m, int Ts, int64_t max_elems)
+{
+    if (Ts == 0)
+        return 1;
+    if (m == 0)
+        return 2;
+    if (m == 1)
+        return 3;
+    const int nw = (m + kWordBits - 1) / kWordBits;
+    if (m < kFullMyers && int64_t(Ts + 1) * nw <= max_elems)
+        return 4;
+    return 0;
+}
+
+// One packed segment: rows [qb, qe) split at qm, target [tb, te); its split
+// scores at buffer offset boff (Ts + 1 entries each), frontier entry f.
+struct PackSeg
+{
+    int32_t qb, qm, qe, tb, te, f, boff, pad;
+};
+
+// Both sweeps of up to 32 small segments in one pass: lane group F of a
+// segment holds the words of rows [qb, qm) (forward), group R those of rows
+// [qm, qe) of the reversed query.  fw / rv + boff receive the scores of
+// columns 0..Ts as split_sweep does for one segment.
+template <typename Buf>
+__device__ void packed_split_sweep(const GWAMD_LDS uint32_t* pat, int pat_words, int Q,
+                                   const GWAMD_LDS PackSeg* segs, int nseg, const GWAMD_LDS uint32_t* tcod, int lane,
+                                   Buf fw, Buf rv)
+{
+    // this lane's group
+    int g_ts = -1, g_tb = 0, g_te = 0, g_w = 0, g_m = 0, g_boff = 0, g_off = 0;
+    bool g_rev = false, is_start = false, is_last = false;
+    int lo = 0, tmax = 0;
+    for (int s = 0; s < nseg; s++)
+    {
+        const int qb = segs[s].qb, qm = segs[s].qm, qe = segs[s].qe, tb = segs[s].tb, te = segs[s].te;
+        const int mf = qm - qb, mr = qe - qm;
+        const int wf = (mf + kWordBits - 1) / kWordBits, wr = (mr + kWordBits - 1) / kWordBits;
+        tmax = max(tmax, te - tb);
+        if (lane >= lo && lane < lo + wf)
+        {
+            g_ts = te - tb, g_tb = tb, g_te = te, g_w = lane - lo, g_m = mf, g_boff = segs[s].boff;
+            g_rev = false, g_off = qb, is_start = lane == lo, is_last = lane == lo + wf - 1;
+        }
+        else if (lane >= lo + wf && lane < lo + wf + wr)
+        {
+            g_ts = te - tb, g_tb = tb, g_te = te, g_w = lane - lo - wf, g_m = mr, g_boff = segs[s].boff;
+            g_rev = true, g_off = Q - qe, is_start = lane == lo + wf, is_last = lane == lo + wf + wr - 1;
+        }
+        lo += wf + wr;
+    }
+    const bool valid  = g_ts >= 0;
+    const uint64_t act = __builtin_amdgcn_ballot_w64(valid);
+    // carries and shifted bits stop at group boundaries
+    const uint64_t cut = act & ~__builtin_amdgcn_ballot_w64(is_last);
+    const uint32_t start_bit = is_start ? 1u : 0u;
+    const uint32_t hisel     = lane >= 32 ? 1u : 0u;
+    uint32_t e[4];
+#pragma unroll
+    for (int L = 0; L < 4; L++)
+        e[L] = valid ? seg_pattern(pat, pat_words, g_off, g_w, (g_rev ? 4 : 0) + L) : 0u;
+    uint32_t pv = ~0u, mv = 0u;
+    const int hb = (g_m - 1) & (kWordBits - 1);
+    int score    = g_m;
+    Buf out      = g_rev ? rv : fw;
+    if (is_last)
+        out[g_boff] = uint16_t(score);
+    // the letter of column t for this lane, read one column ahead
+    auto code_of = [&](int t) -> int {
+        if (!valid || t > g_ts)
+            return 0;
+        return code_at(tcod, g_rev ? g_te - t : g_tb + t - 1);
+    };
+    int code = code_of(1);
+    tmax     = uni(tmax);
+    for (int t = 1; t <= tmax; t++)
+    {
+        const int next = code_of(t + 1);
+        const uint32_t l2 = (code & 1) ? e[1] : e[0];
+        const uint32_t h2 = (code & 1) ? e[3] : e[2];
+        const uint32_t eq = (code & 2) ? h2 : l2;
+        const uint32_t xv = eq | mv;
+        uint32_t sum;
+        const bool ov     = __builtin_add_overflow(eq & pv, pv, &sum);
+        const uint64_t G  = __builtin_amdgcn_ballot_w64(ov) & cut;
+        const uint64_t P  = __builtin_amdgcn_ballot_w64(sum == 0xffffffffu) & cut;
+        const uint64_t GP = G | P;
+        sum += mask_bit((GP + G) ^ GP ^ G, hisel, lane);
+        const uint32_t xh = (sum ^ pv) | eq;
+        uint32_t ph       = mv | ~(xh | pv);
+        uint32_t mh       = pv & xh;
+        score += int((ph >> hb) & 1u) - int((mh >> hb) & 1u);
+        const uint64_t PH = __builtin_amdgcn_ballot_w64((ph >> 31) != 0u) & cut;
+        const uint64_t MH = __builtin_amdgcn_ballot_w64((mh >> 31) != 0u) & cut;
+        // the top row enters every group with +1 (:327-331)
+        ph = (ph << 1) | mask_bit(PH << 1, hisel, lane) | start_bit;
+        mh = (mh << 1) | mask_bit(MH << 1, hisel, lane);
+        pv = mh | ~(xv | ph);
+        mv = ph & xv;
+        if (is_last && t <= g_ts)
+            out[g_boff + t] = uint16_t(score);
+        code = next;
+    }
+}
+
+// Base case of one frontier entry, emitted at path + len (end -> start).
+template <typename LeafFn>
+__device__ int emit_base(int kind, int qb, int qe, int tb, int te, const char* q, const char* tg, int8_t* path,
+                         int lane, LeafFn&& leaf)
+{
+    const int m  = qe - qb;
+    const int Ts = te - tb;
+    if (kind == 1)
+    {
+        for (int k = lane; k < m; k += kWave)
+            path[k] = kDeletion;
+        return m;
+    }
+    if (kind == 2)
+    {
+        for (int k = lane; k < Ts; k += kWave)
+            path[k] = kInsertion;
+        return Ts;
+    }
+    if (kind == 3)
+    {
+        // last target position equal to the query character (:477-508)
+        const char c = q[qb];
+        int found    = -1;
+        for (int k0 = 0; k0 < Ts && found < 0; k0 += kWave)
+        {
+            const int k       = k0 + lane;
+            const bool hit    = k < Ts && tg[te - 1 - k] == c; // raw characters
+            const uint64_t hm = __builtin_amdgcn_ballot_w64(hit);
+            if (hm != 0)
+                found = k0 + __builtin_ctzll(hm);
+        }
+        for (int k = lane; k < Ts; k += kWave)
+        {
+            int8_t st = k == found ? kMatch : kInsertion;
+            if (found < 0 && k == Ts - 1)
+                st = kMismatch;
+            path[k] = st;
+        }
+        return Ts;
+    }
+    return leaf(qb, qe, tb, te, path);
 }
 
 // ---------------------------------------------------------------------------
@@ -445,10 +615,14 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
     // split scores of segments up to kSplitLds columns (wider ones in HBM)
     GWAMD_LDS uint16_t* fwl         = (GWAMD_LDS uint16_t*)(scratch + kLeafCols * kLeafColBytes);
     GWAMD_LDS uint16_t* rvl         = fwl + kSplitLds;
-    GWAMD_LDS Range* stack          = (GWAMD_LDS Range*)(base + a.lds_stack_off);
+    GWAMD_LDS PackSeg* pack         = (GWAMD_LDS PackSeg*)(base + a.lds_stack_off);
     uint8_t* ws                     = a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes);
     uint16_t* fwg = reinterpret_cast<uint16_t*>(ws + ((int64_t(a.stride + 1) * kLeafColBytes + 15) & ~int64_t(15)));
-    uint16_t* rvg = fwg + (a.stride + 1);
+    uint16_t* rvg = fwg + (a.stride + 1 + kWave);
+    uint2* front[2];
+    front[0]      = reinterpret_cast<uint2*>(ws + a.ws_front_off);
+    front[1]      = front[0] + a.front_cap;
+    uint16_t* spl = reinterpret_cast<uint16_t*>(front[1] + a.front_cap); // split column per entry
 #ifdef GWAMD_ALN_PROFILE
     uint64_t pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -464,139 +638,169 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
         pack_target(tcod, tg, T, lane);
         build_patterns(pat, q, Q, lane);
         const int pat_words = (Q + kWordBits - 1) / kWordBits;
-        wave_sync();
-
-        int sp = 0;
         if (lane == 0)
-            put_range(stack, 0, Q, 0, T);
-        sp           = 1;
-        bool success = true;
-        int len      = 0;
-        while (success && sp > 0)
+            front[0][0] = seg_pack(0, Q, 0, T);
+        __threadfence_block();
+        wave_sync();
+        int cur = 0, nf = 1;
+        while (true)
         {
-            wave_sync();
-            --sp;
-            const Range e = Range{uni(stack[sp].qb), uni(stack[sp].qe), uni(stack[sp].tb), uni(stack[sp].te)};
-            wave_sync();
-            const int m  = e.qe - e.qb;
-            const int Ts = e.te - e.tb;
-            if (Ts == 0)
-            {
-                for (int k = lane; k < m; k += kWave)
-                    path[len + k] = kDeletion;
-                len += m;
-            }
-            else if (m == 0)
-            {
-                for (int k = lane; k < Ts; k += kWave)
-                    path[len + k] = kInsertion;
-                len += Ts;
-            }
-            else if (m == 1)
-            {
-                // last target position equal to the query character (:477-508)
-                const char c = q[e.qb];
-                int found    = -1;
-                for (int k0 = 0; k0 < Ts && found < 0; k0 += kWave)
+            // 1. split columns of this level's non-base segments
+            GWAMD_PROF_T0(t_rev);
+            int nsplit = 0, npk = 0, lanes_used = 0, boff = 0;
+            auto flush = [&]() {
+                if (npk == 0)
+                    return;
+                wave_sync();
+                packed_split_sweep(pat, pat_words, Q, pack, npk, tcod, lane, fwg, rvg);
+                __threadfence_block();
+                wave_sync();
+                for (int s = 0; s < npk; s++)
                 {
-                    const int k       = k0 + lane;
-                    const bool hit    = k < Ts && tg[e.te - 1 - k] == c; // raw characters
-                    const uint64_t hm = __builtin_amdgcn_ballot_w64(hit);
-                    if (hm != 0)
-                        found = k0 + __builtin_ctzll(hm);
+                    const int Ts = uni(pack[s].te) - uni(pack[s].tb);
+                    const int bo = uni(pack[s].boff);
+                    const int bt = split_argmin(fwg + bo, rvg + bo, Ts, lane);
+                    if (lane == 0)
+                        spl[uni(pack[s].f)] = uint16_t(bt);
                 }
-                for (int k = lane; k < Ts; k += kWave)
-                {
-                    int8_t st = k == found ? kMatch : kInsertion;
-                    if (found < 0 && k == Ts - 1)
-                        st = kMismatch;
-                    path[len + k] = st;
-                }
-                len += Ts;
-            }
-            else
+                wave_sync();
+                npk = 0, lanes_used = 0, boff = 0;
+            };
+            for (int f = 0; f < nf; f++)
             {
-                const int nw = (m + kWordBits - 1) / kWordBits;
-                if (m < kFullMyers && int64_t(Ts + 1) * nw <= a.max_matrix_elems)
+                const uint2 v  = front[cur][f];
+                const int qb   = uni(int(v.x & 0xffffu)), qe = uni(int(v.x >> 16));
+                const int tb   = uni(int(v.y & 0xffffu)), te = uni(int(v.y >> 16));
+                const int m    = qe - qb;
+                const int Ts   = te - tb;
+                if (base_kind(m, Ts, a.max_matrix_elems) != 0)
+                    continue;
+                nsplit++;
+                const int qm = qb + m / 2;
+                const int wf = (qm - qb + kWordBits - 1) / kWordBits;
+                const int wr = (qe - qm + kWordBits - 1) / kWordBits;
+                if (wf + wr <= kWave)
                 {
-                    GWAMD_PROF_T0(t_leaf);
-#ifdef GWAMD_ALN_PROFILE
-                    pr[5] += Ts;
-                    pr[6] += 1;
-#endif
-                    if (Ts + 1 <= kLeafCols)
+                    if (lanes_used + wf + wr > kWave || npk == 32 || boff + Ts + 1 > a.stride + 1 + kWave)
+                        flush();
+                    if (lane == 0)
                     {
-                        GWAMD_LDS uint64_t* lpv = (GWAMD_LDS uint64_t*)(scratch);
-                        GWAMD_LDS uint64_t* lmv = lpv + kLeafCols;
-                        GWAMD_LDS int32_t* lsc  = (GWAMD_LDS int32_t*)(lmv + kLeafCols);
-                        len += leaf_full_myers(pat, pat_words, e.qb, e.qe, tcod, e.tb, e.te, lpv, lmv, lsc, path + len,
-                                               lane);
+                        GWAMD_LDS PackSeg* ps = pack + npk;
+                        ps->qb = qb, ps->qm = qm, ps->qe = qe, ps->tb = tb, ps->te = te, ps->f = f, ps->boff = boff;
                     }
-                    else
-                    {
-                        uint64_t* lpv = reinterpret_cast<uint64_t*>(ws);
-                        uint64_t* lmv = lpv + (a.stride + 1);
-                        int32_t* lsc  = reinterpret_cast<int32_t*>(lmv + (a.stride + 1));
-                        len += leaf_full_myers(pat, pat_words, e.qb, e.qe, tcod, e.tb, e.te, lpv, lmv, lsc, path + len,
-                                               lane);
-                    }
-                    wave_sync();
-                    GWAMD_PROF_ADD(pr[2], t_leaf);
+                    npk++;
+                    lanes_used += wf + wr;
+                    boff += Ts + 1;
                     continue;
                 }
-                // split the query at its middle, the target at the best column:
-                // both halves swept together, then the minimum of fwd + rev
-                const int qm   = e.qb + m / 2;
-                const int nblk = uni(((max(qm - e.qb, e.qe - qm) + kWordBits - 1) / kWordBits + kWave - 1) / kWave);
+                // a segment too large to share a block: both sweeps over
+                // 1..4 blocks of 64 words (split_sweep)
+                const int nblk = uni(((max(wf, wr)) + kWave - 1) / kWave);
 #ifdef GWAMD_ALN_PROFILE
                 pr[4] += uint64_t(Ts) * nblk;
 #endif
-                GWAMD_PROF_T0(t_rev);
                 int bt;
                 if (Ts + 1 <= kSplitLds)
                 {
-                    run_split(nblk, pat, pat_words, Q, e.qb, qm, e.qe, tcod, e.tb, e.te, lane, fwl, rvl);
+                    run_split(nblk, pat, pat_words, Q, qb, qm, qe, tcod, tb, te, lane, fwl, rvl);
                     wave_sync();
-                    GWAMD_PROF_ADD(pr[0], t_rev);
-                    GWAMD_PROF_T0(t_fwd);
                     bt = split_argmin(fwl, rvl, Ts, lane);
-                    GWAMD_PROF_ADD(pr[1], t_fwd);
                 }
                 else
                 {
-                    run_split(nblk, pat, pat_words, Q, e.qb, qm, e.qe, tcod, e.tb, e.te, lane, fwg, rvg);
+                    run_split(nblk, pat, pat_words, Q, qb, qm, qe, tcod, tb, te, lane, fwg, rvg);
                     __threadfence_block();
                     wave_sync();
-                    GWAMD_PROF_ADD(pr[0], t_rev);
-                    GWAMD_PROF_T0(t_fwd);
                     bt = split_argmin(fwg, rvg, Ts, lane);
-                    GWAMD_PROF_ADD(pr[1], t_fwd);
                 }
-                const int tm = e.tb + bt;
+                if (lane == 0)
+                    spl[f] = uint16_t(bt);
                 wave_sync();
-                if (sp < kStackSize)
+            }
+            flush();
+            __threadfence_block();
+            wave_sync();
+            GWAMD_PROF_ADD(pr[0], t_rev);
+            if (nsplit == 0)
+                break;
+            // 2. next frontier: each split segment becomes its two halves, in order
+            GWAMD_PROF_T0(t_fwd);
+            int nn = 0;
+            for (int f0 = 0; f0 < nf; f0 += kWave)
+            {
+                const int f      = f0 + lane;
+                const bool in    = f < nf;
+                const uint2 v    = in ? front[cur][f] : make_uint2(0, 0);
+                const int qb     = int(v.x & 0xffffu), qe = int(v.x >> 16);
+                const int tb     = int(v.y & 0xffffu), te = int(v.y >> 16);
+                const bool split = in && base_kind(qe - qb, te - tb, a.max_matrix_elems) == 0;
+                const int cnt    = in ? (split ? 2 : 1) : 0;
+                // exclusive prefix sum of cnt over the lanes
+                int x = cnt;
+#pragma unroll
+                for (int d = 1; d < kWave; d <<= 1)
                 {
-                    if (lane == 0)
-                        put_range(stack + sp, e.qb, qm, e.tb, tm);
-                    ++sp;
+                    const int y = __shfl_up(x, d);
+                    x += lane >= d ? y : 0;
                 }
-                else
-                    success = false;
-                if (success)
+                const int pos = nn + x - cnt;
+                if (in)
                 {
-                    if (sp < kStackSize)
+                    if (split)
                     {
-                        if (lane == 0)
-                            put_range(stack + sp, qm, e.qe, tm, e.te);
-                        ++sp;
+                        const int qm = qb + (qe - qb) / 2;
+                        const int tm = tb + int(spl[f]);
+                        front[cur ^ 1][pos]     = seg_pack(qb, qm, tb, tm);
+                        front[cur ^ 1][pos + 1] = seg_pack(qm, qe, tm, te);
                     }
                     else
-                        success = false;
+                        front[cur ^ 1][pos] = v;
                 }
+                nn += uni(__shfl(x, kWave - 1));
             }
+            __threadfence_block();
+            wave_sync();
+            cur ^= 1;
+            nf = nn;
+            GWAMD_PROF_ADD(pr[1], t_fwd);
         }
+        // 3. base cases, from the last segment to the first
+        GWAMD_PROF_T0(t_leaf);
+        int len = 0;
+        for (int f = nf - 1; f >= 0; f--)
+        {
+            const uint2 v = front[cur][f];
+            const int qb  = uni(int(v.x & 0xffffu)), qe = uni(int(v.x >> 16));
+            const int tb  = uni(int(v.y & 0xffffu)), te = uni(int(v.y >> 16));
+            const int kind = base_kind(qe - qb, te - tb, a.max_matrix_elems);
+#ifdef GWAMD_ALN_PROFILE
+            if (kind == 4)
+            {
+                pr[5] += te - tb;
+                pr[6] += 1;
+            }
+#endif
+            len += emit_base(kind, qb, qe, tb, te, q, tg, path + len, lane,
+                             [&](int lqb, int lqe, int ltb, int lte, int8_t* p) -> int {
+                                 if (lte - ltb + 1 <= kLeafCols)
+                                 {
+                                     GWAMD_LDS uint64_t* lpv = (GWAMD_LDS uint64_t*)(scratch);
+                                     GWAMD_LDS uint64_t* lmv = lpv + kLeafCols;
+                                     GWAMD_LDS int32_t* lsc  = (GWAMD_LDS int32_t*)(lmv + kLeafCols);
+                                     return leaf_full_myers(pat, pat_words, lqb, lqe, tcod, ltb, lte, lpv, lmv, lsc, p,
+                                                            lane);
+                                 }
+                                 uint64_t* lpv = reinterpret_cast<uint64_t*>(ws);
+                                 uint64_t* lmv = lpv + (a.stride + 1);
+                                 int32_t* lsc  = reinterpret_cast<int32_t*>(lmv + (a.stride + 1));
+                                 return leaf_full_myers(pat, pat_words, lqb, lqe, tcod, ltb, lte, lpv, lmv, lsc, p,
+                                                        lane);
+                             });
+            wave_sync();
+        }
+        GWAMD_PROF_ADD(pr[2], t_leaf);
         if (lane == 0)
-            a.path_len[idx] = success ? len : 0;
+            a.path_len[idx] = len;
         wave_sync();
         GWAMD_PROF_ADD(pr[3], t_all);
     }

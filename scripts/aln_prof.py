@@ -33,7 +33,7 @@ b.synchronize()
 dt = time.perf_counter() - t0
 lib.gwamd_internal_aln_prof(buf, 1)
 v = list(buf)
-names = ["rev_sweep", "fwd_sweep", "base_cases", "total", "sweep_col_blocks", "leaf_cols", "leaves"]
+names = ["split_levels", "frontier", "base_cases", "total", "big_col_blocks", "leaf_cols", "leaves"]
 print("pairs", n, "grid", b.config()[0], "wall_ms", round(dt * 1e3, 1))
 for k, nm in enumerate(names):
     print("%-18s %14.0f per pair" % (nm, v[k] / n))
