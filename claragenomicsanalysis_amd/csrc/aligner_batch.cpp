@@ -18,6 +18,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 extern "C" hipError_t gwamd_internal_align_launch(const gwamd::aln::Args* a, int algo, int grid, hipStream_t stream);
@@ -273,16 +274,32 @@ public:
         ScopedDevice dev(device_id_);
         GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
         const int32_t n = int32_t(alignments_.size());
-        for (int32_t i = 0; i < n; i++)
+        auto fill       = [&](int32_t i0, int32_t i1) {
+            for (int32_t i = i0; i < i1; i++)
+            {
+                const int32_t len = h_plen_.as<int32_t>()[i];
+                const int8_t* p   = h_paths_.as<int8_t>() + size_t(i) * max_result_;
+                std::vector<AlignmentState> st(size_t(std::max(len, 0)));
+                for (int32_t k = 0; k < len; k++)
+                    st[size_t(len - 1 - k)] = static_cast<AlignmentState>(p[k]);
+                auto* a = static_cast<AlignmentImpl*>(alignments_[size_t(i)].get());
+                a->set_alignment(std::move(st));
+                a->set_status(StatusType::success);
+            }
+        };
+        // the alignments are independent: large batches are filled by a few
+        // host threads (each alignment object is touched by one thread)
+        const int32_t nth = n < 4096 ? 1 : int32_t(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+        if (nth <= 1)
+            fill(0, n);
+        else
         {
-            const int32_t len = h_plen_.as<int32_t>()[i];
-            const int8_t* p   = h_paths_.as<int8_t>() + size_t(i) * max_result_;
-            std::vector<AlignmentState> st(size_t(std::max(len, 0)));
-            for (int32_t k = 0; k < len; k++)
-                st[size_t(len - 1 - k)] = static_cast<AlignmentState>(p[k]);
-            auto* a = static_cast<AlignmentImpl*>(alignments_[size_t(i)].get());
-            a->set_alignment(std::move(st));
-            a->set_status(StatusType::success);
+            std::vector<std::thread> th;
+            const int32_t per = (n + nth - 1) / nth;
+            for (int32_t t = 0; t < nth; t++)
+                th.emplace_back(fill, std::min(n, t * per), std::min(n, (t + 1) * per));
+            for (auto& t : th)
+                t.join();
         }
         return StatusType::success;
     }
@@ -431,7 +448,12 @@ private:
             // of the target-only halves of a split)
             front_cap_  = 2 * (max_q_ + 2);
             front_off_  = a16(a16(int64_t(stride_ + 1) * kLeafColBytes) + int64_t(stride_ + 1 + kWave) * 4 + 64);
-            slot_bytes_ = a16(front_off_ + int64_t(front_cap_) * (2 * 8 + 2) + 64);
+            // per-lane base cases: columns of every segment (target + one per
+            // segment), (offset, length) per segment, paths (query + target)
+            leaf_cols_  = max_t_ + front_cap_ + 2;
+            leaf_off_   = a16(front_off_ + int64_t(front_cap_) * (2 * 8 + 2) + 64);
+            slot_bytes_ = a16(leaf_off_ + int64_t(leaf_cols_) * kLeafColBytes + 16 + int64_t(front_cap_) * 8 +
+                              max_q_ + max_t_ + 64);
         }
         else
         {
@@ -460,6 +482,8 @@ private:
         a.ws_slot_bytes    = slot_bytes_;
         a.ws_front_off     = front_off_;
         a.front_cap        = front_cap_;
+        a.ws_leaf_off      = leaf_off_;
+        a.leaf_cols        = leaf_cols_;
         a.lds_target_off   = lds_target_off_;
         a.lds_pat_off      = lds_pat_off_;
         a.lds_scratch_off  = lds_scratch_off_;
@@ -483,6 +507,8 @@ private:
     int32_t pat_words_ = 0, scratch_bytes_ = 0;
     int64_t front_off_ = 0;
     int32_t front_cap_ = 0;
+    int64_t leaf_off_  = 0;
+    int32_t leaf_cols_ = 0;
     int32_t lds_seq2_off_ = 0, lds_tile_off_ = 0, tile_bytes_ = 0;
     int32_t slots_ = 1;
     int64_t slot_bytes_ = 0, device_bytes_ = 0;

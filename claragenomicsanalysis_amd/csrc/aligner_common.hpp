@@ -53,6 +53,8 @@ struct Args
     int64_t ws_slot_bytes;
     int64_t ws_front_off;    // Hirschberg-Myers: frontier of the breadth-first recursion in the slot
     int32_t front_cap;       //   entries per frontier buffer (two buffers, then one u16 split column each)
+    int64_t ws_leaf_off;     //   per-lane base cases: columns (pv, mv, score) then paths
+    int32_t leaf_cols;       //   column capacity (target + one per segment)
     // LDS layout (bytes)
     int32_t lds_target_off;
     int32_t lds_pat_off;     // [pat_words][8] u32: forward A C T G, reverse A C T G

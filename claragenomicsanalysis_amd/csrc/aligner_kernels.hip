@@ -602,6 +602,101 @@ __device__ int emit_base(int kind, int qb, int qe, int tb, int te, const char* q
     return leaf(qb, qe, tb, te, path);
 }
 
+// Full-Myers base case run by ONE lane (each lane of the wave takes one base
+// case of the frontier): the same recurrence and backtrace as
+// leaf_full_myers, with the column state in the lane's own stretch of the
+// slot and the path (end -> start) in its own stretch of path scratch.
+__device__ int leaf_lane(const GWAMD_LDS uint32_t* pat, int pat_words, int qb, int qe,
+                         const GWAMD_LDS uint32_t* tcod, int tb, int te, uint64_t* lpv, uint64_t* lmv, int32_t* lsc,
+                         int8_t* path)
+{
+    const int m         = qe - qb;
+    const int T         = te - tb;
+    const uint64_t full = (uint64_t(1) << m) - 1;
+    uint64_t e[4];
+    {
+        const int k  = qb >> 5;
+        const int sh = qb & 31;
+#pragma unroll
+        for (int L = 0; L < 4; L++)
+        {
+            const uint64_t w0 = k < pat_words ? pat[k * 8 + L] : 0u;
+            const uint64_t w1 = k + 1 < pat_words ? pat[(k + 1) * 8 + L] : 0u;
+            const uint64_t w2 = k + 2 < pat_words ? pat[(k + 2) * 8 + L] : 0u;
+            uint64_t r        = (w0 | (w1 << 32)) >> sh;
+            if (sh != 0)
+                r |= w2 << (64 - sh);
+            e[L] = r & full;
+        }
+    }
+    uint64_t pv = full, mv = 0;
+    int score   = m;
+    lpv[0]      = pv;
+    lmv[0]      = mv;
+    lsc[0]      = score;
+    for (int t = 1; t <= T; t++)
+    {
+        const int code    = code_at(tcod, tb + t - 1);
+        const uint64_t lo = (code & 1) ? e[1] : e[0];
+        const uint64_t hi = (code & 1) ? e[3] : e[2];
+        const uint64_t eq = (code & 2) ? hi : lo;
+        const uint64_t xv = eq | mv;
+        const uint64_t xh = (((eq & pv) + pv) ^ pv) | eq;
+        uint64_t ph       = mv | ~(xh | pv);
+        uint64_t mh       = pv & xh;
+        score += int((ph >> (m - 1)) & 1u) - int((mh >> (m - 1)) & 1u);
+        ph     = (ph << 1) | 1u;
+        mh     = mh << 1;
+        pv     = (mh | ~(xv | ph)) & full;
+        mv     = (ph & xv) & full;
+        lpv[t] = pv;
+        lmv[t] = mv;
+        lsc[t] = score;
+    }
+    // D(i, j) = D(m, j) - sum of vertical deltas of rows i+1..m
+    auto D = [&](int i, int j) -> int {
+        if (i == 0)
+            return j;
+        const uint64_t hm = full & ~((uint64_t(1) << i) - 1);
+        return lsc[j] - __builtin_popcountll(lpv[j] & hm) + __builtin_popcountll(lmv[j] & hm);
+    };
+    int i = m, j = T, pos = 0;
+    int s = D(i, j);
+    while (i > 0 && j > 0)
+    {
+        const int above = D(i - 1, j);
+        const int diag  = D(i - 1, j - 1);
+        const int left  = D(i, j - 1);
+        int8_t r;
+        if (left + 1 == s) // insertion, then deletion, then diagonal (:118-160)
+        {
+            r = kInsertion;
+            s = left;
+            --j;
+        }
+        else if (above + 1 == s)
+        {
+            r = kDeletion;
+            s = above;
+            --i;
+        }
+        else
+        {
+            r = diag == s ? kMatch : kMismatch;
+            s = diag;
+            --i;
+            --j;
+        }
+        path[pos++] = r;
+    }
+    for (int k = 0; k < i; k++)
+        path[pos + k] = kDeletion;
+    pos += i;
+    for (int k = 0; k < j; k++)
+        path[pos + k] = kInsertion;
+    return pos + j;
+}
+
 // ---------------------------------------------------------------------------
 // Hirschberg + Myers (hirschberg_myers, :569-638), one wave per pair.
 __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
@@ -623,6 +718,13 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
     front[0]      = reinterpret_cast<uint2*>(ws + a.ws_front_off);
     front[1]      = front[0] + a.front_cap;
     uint16_t* spl = reinterpret_cast<uint16_t*>(front[1] + a.front_cap); // split column per entry
+    // per-lane base cases: column state (pv, mv, score) and paths; (path
+    // offset, length) per frontier entry
+    uint64_t* lcol_pv = reinterpret_cast<uint64_t*>(ws + a.ws_leaf_off);
+    uint64_t* lcol_mv = lcol_pv + a.leaf_cols;
+    int32_t* lcol_sc  = reinterpret_cast<int32_t*>(lcol_mv + a.leaf_cols);
+    int2* lmeta       = reinterpret_cast<int2*>(lcol_sc + ((a.leaf_cols + 3) & ~1));
+    int8_t* lpath     = reinterpret_cast<int8_t*>(lmeta + a.front_cap);
 #ifdef GWAMD_ALN_PROFILE
     uint64_t pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -764,8 +866,47 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
             nf = nn;
             GWAMD_PROF_ADD(pr[1], t_fwd);
         }
-        // 3. base cases, from the last segment to the first
+        // 3. base cases.  The full-Myers ones (all but a few) are computed
+        // one per lane, their paths into scratch; then every base case is
+        // emitted from the last segment to the first.
         GWAMD_PROF_T0(t_leaf);
+        {
+            int coff = 0, poff = 0;
+            for (int f0 = 0; f0 < nf; f0 += kWave)
+            {
+                const int f   = f0 + lane;
+                const bool in = f < nf;
+                const uint2 v = in ? front[cur][f] : make_uint2(0, 0);
+                const int qb = int(v.x & 0xffffu), qe = int(v.x >> 16);
+                const int tb = int(v.y & 0xffffu), te = int(v.y >> 16);
+                const bool full_myers = in && base_kind(qe - qb, te - tb, a.max_matrix_elems) == 4;
+                // scratch stretches: columns 0..Ts, path up to m + Ts states
+                int cc = full_myers ? te - tb + 1 : 0, pc = full_myers ? qe - qb + te - tb : 0;
+                int xc = cc, xp = pc;
+#pragma unroll
+                for (int d = 1; d < kWave; d <<= 1)
+                {
+                    const int yc = __shfl_up(xc, d), yp = __shfl_up(xp, d);
+                    xc += lane >= d ? yc : 0;
+                    xp += lane >= d ? yp : 0;
+                }
+                const int mc = coff + xc - cc, mp = poff + xp - pc;
+#ifdef GWAMD_ALN_PROFILE
+                pr[5] += uni(__shfl(xc, kWave - 1));
+                pr[6] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(full_myers));
+#endif
+                if (full_myers)
+                {
+                    const int n = leaf_lane(pat, pat_words, qb, qe, tcod, tb, te, lcol_pv + mc, lcol_mv + mc,
+                                            lcol_sc + mc, lpath + mp);
+                    lmeta[f] = make_int2(mp, n);
+                }
+                coff += uni(__shfl(xc, kWave - 1));
+                poff += uni(__shfl(xp, kWave - 1));
+            }
+        }
+        __threadfence_block();
+        wave_sync();
         int len = 0;
         for (int f = nf - 1; f >= 0; f--)
         {
@@ -773,31 +914,19 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
             const int qb  = uni(int(v.x & 0xffffu)), qe = uni(int(v.x >> 16));
             const int tb  = uni(int(v.y & 0xffffu)), te = uni(int(v.y >> 16));
             const int kind = base_kind(qe - qb, te - tb, a.max_matrix_elems);
-#ifdef GWAMD_ALN_PROFILE
             if (kind == 4)
             {
-                pr[5] += te - tb;
-                pr[6] += 1;
+                const int2 md = lmeta[f];
+                const int mp  = uni(md.x), n = uni(md.y);
+                for (int k = lane; k < n; k += kWave)
+                    path[len + k] = lpath[mp + k];
+                len += n;
             }
-#endif
-            len += emit_base(kind, qb, qe, tb, te, q, tg, path + len, lane,
-                             [&](int lqb, int lqe, int ltb, int lte, int8_t* p) -> int {
-                                 if (lte - ltb + 1 <= kLeafCols)
-                                 {
-                                     GWAMD_LDS uint64_t* lpv = (GWAMD_LDS uint64_t*)(scratch);
-                                     GWAMD_LDS uint64_t* lmv = lpv + kLeafCols;
-                                     GWAMD_LDS int32_t* lsc  = (GWAMD_LDS int32_t*)(lmv + kLeafCols);
-                                     return leaf_full_myers(pat, pat_words, lqb, lqe, tcod, ltb, lte, lpv, lmv, lsc, p,
-                                                            lane);
-                                 }
-                                 uint64_t* lpv = reinterpret_cast<uint64_t*>(ws);
-                                 uint64_t* lmv = lpv + (a.stride + 1);
-                                 int32_t* lsc  = reinterpret_cast<int32_t*>(lmv + (a.stride + 1));
-                                 return leaf_full_myers(pat, pat_words, lqb, lqe, tcod, ltb, lte, lpv, lmv, lsc, p,
-                                                        lane);
-                             });
-            wave_sync();
+            else
+                len += emit_base(kind, qb, qe, tb, te, q, tg, path + len, lane,
+                                 [&](int, int, int, int, int8_t*) -> int { return 0; });
         }
+        wave_sync();
         GWAMD_PROF_ADD(pr[2], t_leaf);
         if (lane == 0)
             a.path_len[idx] = len;
