@@ -489,7 +489,7 @@ def bench_poa(ctx, key, steps, warmup, args, with_cpu):
                    "windows_per_gpu": nwin, "batch_size": [cfg["max_seq"], cfg["reads"]],
                    "scores": [-8, -6, 8], "parallelism": "dp%d (windows sharded, RCCL gather)" % ctx.world,
                    "score_bits": score_bits, "size_bits": size_bits,
-                   "kernel_variant": ["", "global", "lds", "band"][batch.kernel_variant()],
+                   "kernel_variant": ["", "global", "lds", "band", "band_ad"][batch.kernel_variant()],
                    "grid_slots": slots, "resident_workgroups": resident,
                    "windows_ok": n_ok, "dp_cells_per_step": cells_total,
                    "gcups": round(cells_total / (kernel_ms / 1e3) / 1e9, 3),
@@ -499,7 +499,7 @@ def bench_poa(ctx, key, steps, warmup, args, with_cpu):
                    "phase_ms_mean_per_window": {name: round(float(ticks[:, i].mean()) / 1e5, 3)
                                                 for i, name in enumerate(batch.PHASES)}},
         "roofline": roofline(alg_bytes, kernel_ms, traffic, "poa_window_kernel_%s" %
-                             ["", "v1", "lds", "band"][batch.kernel_variant()], tsrc, load_sq("poa_" + key)),
+                             ["", "v1", "lds", "band", "band"][batch.kernel_variant()], tsrc, load_sq("poa_" + key)),
         "cpu_baseline": cpu,
         "parity": parity,
     }

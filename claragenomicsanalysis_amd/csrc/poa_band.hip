@@ -95,7 +95,7 @@ struct BandAux
 // phase slots, see the kernel epilogue).
 struct BandProf
 {
-    uint64_t v[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t v[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef GWAMD_BAND_PROFILE
     __device__ void add(int i, uint64_t x) { v[i] += x; }
     __device__ static uint64_t now() { return __builtin_amdgcn_s_memtime(); }
@@ -117,6 +117,10 @@ enum
     kBpRefill,       // traceback move-window refills
     kBpSlow,         // traceback steps through the general (non-window) step
     kBpAddSeq,       // reads added by the sequential add (parallel add declined)
+    kBpAdBlocks,     // anti-diagonal pass: row blocks
+    kBpAdSetup,      // anti-diagonal pass: cycles in block setup (records, slots, dispatch)
+    kBpAdLoop,       // anti-diagonal pass: cycles in the step loops
+    kBpAdSteps,      // anti-diagonal pass: steps
 };
 
 __device__ __forceinline__ BandAux as_global(BandAux X)
@@ -167,8 +171,8 @@ __device__ __forceinline__ int band_np2(WinGraph<SizeT> g, int r, uint32_t a, ui
 // reads the row from kBandRing or more rows later) are collected as LDS bytes
 // from the successor's side and folded into rec_a in a second pass.
 template <typename SizeT>
-__device__ __forceinline__ void band_row_program(WinGraph<SizeT> g, int V, const Band& B, BandAux X, int lane,
-                                 GWAMD_LDS uint8_t* flags)
+__device__ __forceinline__ int band_row_program(WinGraph<SizeT> g, int V, const Band& B, BandAux X, int lane,
+                                 GWAMD_LDS uint8_t* flags, int spill_dist)
 {
     X = as_global(X);
     g = as_global(g);
@@ -177,6 +181,7 @@ __device__ __forceinline__ void band_row_program(WinGraph<SizeT> g, int V, const
         flags[r] = 0;
     wave_sync();
     int xbase = 0;
+    int npmax = 0; // largest predecessor count (returned, wave-uniform)
     static_assert(kRP * kWave == kStageRows, "one row-program pass per staged block");
     for (int r0 = 1; r0 <= V; r0 += kRP * kWave)
     {
@@ -210,6 +215,7 @@ __device__ __forceinline__ void band_row_program(WinGraph<SizeT> g, int V, const
             const int r      = r0 + u * kWave + lane;
             const bool valid = r <= V;
             const int n      = valid ? np[u] : 0;
+            npmax            = max(npmax, n);
             int p2 = 0, p3 = 0;
             if (n >= 3 && n <= 4)
             {
@@ -232,21 +238,21 @@ __device__ __forceinline__ void band_row_program(WinGraph<SizeT> g, int V, const
                     if (n >= 1)
                     {
                         bw = uint32_t(r - p0[u]);
-                        if (r - p0[u] >= kBandRing)
+                        if (r - p0[u] >= spill_dist)
                             flags[p0[u]] = 1;
                     }
                     if (n >= 2)
                     {
                         bw |= uint32_t(r - p1[u]) << 16;
-                        if (r - p1[u] >= kBandRing)
+                        if (r - p1[u] >= spill_dist)
                             flags[p1[u]] = 1;
                     }
                     if (n >= 3)
                     {
                         X.recc[r] = uint32_t(r - p2) | (uint32_t(r - p3) << 16);
-                        if (r - p2 >= kBandRing)
+                        if (r - p2 >= spill_dist)
                             flags[p2] = 1;
-                        if (n == 4 && r - p3 >= kBandRing)
+                        if (n == 4 && r - p3 >= spill_dist)
                             flags[p3] = 1;
                     }
                 }
@@ -259,7 +265,7 @@ __device__ __forceinline__ void band_row_program(WinGraph<SizeT> g, int V, const
                         const int pk = k == 0 ? p0[u] : (k == 1 ? p1[u] : pred_row(g, node[u], k));
                         if (fit)
                             X.xl[off + k] = pk;
-                        if (r - pk >= kBandRing)
+                        if (r - pk >= spill_dist)
                             flags[pk] = 1;
                     }
                     a |= (fit ? uint32_t(n) : kNpEsc) << 8;
@@ -298,6 +304,7 @@ __device__ __forceinline__ void band_row_program(WinGraph<SizeT> g, int V, const
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     wave_sync();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    return uniform(wave_max(npmax));
 }
 
 // Predecessor values F(p, d + CPL*lane + c), c = 0..CPL (flat get_scores()
@@ -839,6 +846,8 @@ __device__ __forceinline__ int band_forward(WinGraph<SizeT> g, BandAux X, int V,
     return end_row;
 }
 
+#include "poa_band_ad.hpp"
+
 // get_score(row, col) semantics for the out-of-band traceback step.  Sets
 // known = false for an in-band value that was not stored: such a value is
 // not one of the T values, so no comparison with minv can match it.
@@ -1160,33 +1169,12 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
     return n;
 }
 
-template <typename ScoreT, typename SizeT, bool MSA, int CPL>
-__global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims d, Scores sc)
+// Per-window pointers of the banded kernel (graph by window, scratch by slot).
+template <typename ScoreT, typename SizeT>
+__device__ __forceinline__ void band_window_ptrs(const Buffers& b, const Dims& d, int w, size_t slot, int rowsz,
+                                                 WinGraph<SizeT>& g, BandAux& X, ScoreT*& spill)
 {
-    extern __shared__ __align__(16) uint8_t lds[];
-    __shared__ int sh_status;
-    __shared__ int sh_len;
-
-    __shared__ int sh_next;
-    if (int(blockIdx.x) >= b.num_windows)
-        return;
-    const int lane    = threadIdx.x;
-    const size_t slot = blockIdx.x; // scratch slot (grid <= slots)
-
-    uint8_t* lread          = lds;
-    GWAMD_LDS uint8_t* work = (GWAMD_LDS uint8_t*)(lds) + d.lds_ring_off;
-    GWAMD_LDS ScoreT* ring  = (GWAMD_LDS ScoreT*)(work);
-    GWAMD_LDS uint8_t* shb  = (GWAMD_LDS uint8_t*)(lds) + d.lds_sh_off;
-    GWAMD_LDS uint8_t* tile = work;
-    const int rowsz          = d.score_stride;
-    // row-record staging after the ring (planned by poa_batch.cpp)
-    GWAMD_LDS uint32_t* stage = (GWAMD_LDS uint32_t*)(work + ((kBandRing * rowsz * int(sizeof(ScoreT)) + 15) & ~15));
-
-    for (int idx = blockIdx.x; idx < b.num_windows;)
-    {
-    const int w     = b.order ? b.order[idx] : idx;
     const size_t mn = size_t(d.max_nodes);
-    WinGraph<SizeT> g;
     g.base      = b.base + w * mn;
     g.in_cnt    = b.in_cnt + w * mn;
     g.out_cnt   = b.out_cnt + w * mn;
@@ -1199,22 +1187,87 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
     g.sorted    = static_cast<SizeT*>(b.sorted) + w * mn;
     g.pos       = static_cast<SizeT*>(b.pos) + w * mn;
     g.max_nodes = d.max_nodes;
+    spill       = static_cast<ScoreT*>(b.scores) + slot * d.score_rows * size_t(rowsz);
+    uint8_t* aux = b.codes + slot * size_t(d.aux_stride);
+    X.codes  = aux;
+    X.reca   = reinterpret_cast<uint32_t*>(aux + d.aux_reca_off);
+    X.recb   = reinterpret_cast<uint32_t*>(aux + d.aux_recb_off);
+    X.recc   = reinterpret_cast<uint32_t*>(aux + d.aux_recc_off);
+    X.rece   = reinterpret_cast<uint32_t*>(aux + d.aux_rece_off);
+    X.col0   = reinterpret_cast<int32_t*>(aux + d.aux_col0_off);
+    X.flags  = aux + d.aux_flag_off;
+    X.xl     = reinterpret_cast<int32_t*>(aux + d.aux_xl_off);
+    X.bx     = reinterpret_cast<int32_t*>(aux + d.aux_bx_off);
+    X.xl_cap = d.aux_xl_cap;
+}
 
+// One window per workgroup.  Wave 0 runs the whole window; with the
+// anti-diagonal pass (d.band_ad) the workgroup has kAdMaxWaves waves and waves
+// 1.. only join the forward passes: wave 0 posts each pass in sh_job and both
+// sides meet at two barriers around it (sh_job[0] < 0: no more passes).
+template <typename ScoreT, typename SizeT, bool MSA, int CPL>
+__global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Buffers b, Dims d, Scores sc)
+{
+    extern __shared__ __align__(16) uint8_t lds[];
+    __shared__ int sh_status;
+    __shared__ int sh_len;
+    __shared__ AdShared ad_sh;
+    __shared__ int sh_job[4]; // window, V, L, gradient bits
+
+    __shared__ int sh_next;
+    if (int(blockIdx.x) >= b.num_windows)
+        return;
+    const int lane    = int(threadIdx.x) % kWave;
+    const int wave    = int(threadIdx.x) / kWave;
+    const int nw      = int(blockDim.x) / kWave;
+    const size_t slot = blockIdx.x; // scratch slot (grid <= slots)
+    GWAMD_LDS AdShared* adsh = (GWAMD_LDS AdShared*)(&ad_sh);
+
+    uint8_t* lread          = lds + kReadGuard; // guard: the anti-diagonal pass reads read[c-1] for c >= -63
+    GWAMD_LDS uint8_t* work = (GWAMD_LDS uint8_t*)(lds) + d.lds_ring_off;
+    GWAMD_LDS ScoreT* ring  = (GWAMD_LDS ScoreT*)(work);
+    GWAMD_LDS uint8_t* shb  = (GWAMD_LDS uint8_t*)(lds) + d.lds_sh_off;
+    GWAMD_LDS uint8_t* tile = work;
+    const int rowsz          = d.score_stride;
+    // row-record staging after the ring (planned by poa_batch.cpp)
+    GWAMD_LDS uint32_t* stage = (GWAMD_LDS uint32_t*)(work + ((kBandRing * rowsz * int(sizeof(ScoreT)) + 15) & ~15));
+
+    if (wave > 0)
+    {
+        // helper waves: forward passes posted by wave 0
+        while (true)
+        {
+            __syncthreads(); // pass posted
+            const int w = sh_job[0];
+            if (w < 0)
+                break;
+            WinGraph<SizeT> g;
+            BandAux X;
+            ScoreT* spill;
+            band_window_ptrs<ScoreT, SizeT>(b, d, w, slot, rowsz, g, X, spill);
+            Band B;
+            B.bw         = d.band_width;
+            B.stride     = d.band_width + kBandPad;
+            B.max_column = sh_job[2] + 1;
+            B.gradient   = __int_as_float(sh_job[3]);
+            BandProf bp;
+            band_forward_ad<ScoreT, SizeT, CPL>(g, X, sh_job[1], (GWAMD_LDS const uint8_t*)(lread), sh_job[2], B, sc,
+                                                ring, spill, rowsz, d.score_rows, lane, wave, nw, adsh, bp);
+            __syncthreads(); // pass done
+        }
+        return;
+    }
+
+    for (int idx = blockIdx.x; idx < b.num_windows;)
+    {
+    const int w     = b.order ? b.order[idx] : idx;
+    const size_t mn = size_t(d.max_nodes);
+    WinGraph<SizeT> g;
+    BandAux X;
+    ScoreT* spill;
+    band_window_ptrs<ScoreT, SizeT>(b, d, w, slot, rowsz, g, X, spill);
     SizeT* ag        = static_cast<SizeT*>(b.ag) + slot * d.aln_cap;
     SizeT* ar        = static_cast<SizeT*>(b.ar) + slot * d.aln_cap;
-    ScoreT* spill    = static_cast<ScoreT*>(b.scores) + slot * d.score_rows * size_t(rowsz);
-    uint8_t* aux     = b.codes + slot * size_t(d.aux_stride);
-    BandAux X;
-    X.codes          = aux;
-    X.reca           = reinterpret_cast<uint32_t*>(aux + d.aux_reca_off);
-    X.recb           = reinterpret_cast<uint32_t*>(aux + d.aux_recb_off);
-    X.recc           = reinterpret_cast<uint32_t*>(aux + d.aux_recc_off);
-    X.rece           = reinterpret_cast<uint32_t*>(aux + d.aux_rece_off);
-    X.col0           = reinterpret_cast<int32_t*>(aux + d.aux_col0_off);
-    X.flags          = aux + d.aux_flag_off;
-    X.xl             = reinterpret_cast<int32_t*>(aux + d.aux_xl_off);
-    X.bx             = reinterpret_cast<int32_t*>(aux + d.aux_bx_off);
-    X.xl_cap         = d.aux_xl_cap;
     int32_t* cscore  = b.cscore + slot * mn;
     SizeT* cpred     = static_cast<SizeT*>(b.cpred) + slot * mn * 4;
     uint16_t* ecov   = MSA ? b.edge_cov + w * mn * kMaxEdges * d.max_seqs : nullptr;
@@ -1259,13 +1312,36 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
             B.stride     = d.band_width + kBandPad;
             B.max_column = L + 1;
             B.gradient   = float(L + 1) / float(V + 1); // cudapoa_nw_banded.cuh:206
-            band_row_program<SizeT>(g, V, B, X, lane, work);
+            // spill rows for successors kBandRing or more rows later: enough for
+            // both forward passes (kAdSpillDist > kBandRing)
+            const int npmax = band_row_program<SizeT>(g, V, B, X, lane, work, kBandRing);
             wave_sync();
             ph.lap<kPhRowProg>();
             cells += int64_t(V + 1) * (d.band_width + kBandPad);
-            const int end_row =
-                band_forward<ScoreT, SizeT, CPL>(g, X, V, (GWAMD_LDS const uint8_t*)(lds), L, B, sc, ring, stage,
-                                                 spill, rowsz, lane, bp);
+            int end_row;
+            if (d.band_ad && npmax <= kAdMaxSlots)
+            {
+                band_ad_init<ScoreT, CPL>(ring, rowsz, d.band_width, int(band_min_value<ScoreT>(sc)), adsh, lane);
+                if (nw > 1)
+                {
+                    if (lane == 0)
+                    {
+                        sh_job[0] = w;
+                        sh_job[1] = V;
+                        sh_job[2] = L;
+                        sh_job[3] = __float_as_int(B.gradient);
+                    }
+                    __syncthreads(); // pass posted
+                }
+                band_forward_ad<ScoreT, SizeT, CPL>(g, X, V, (GWAMD_LDS const uint8_t*)(lread), L, B, sc, ring, spill,
+                                                    rowsz, d.score_rows, lane, 0, nw, adsh, bp);
+                if (nw > 1)
+                    __syncthreads(); // pass done
+                end_row = uniform(band_ad_end_row(adsh, nw));
+            }
+            else
+                end_row = band_forward<ScoreT, SizeT, CPL>(g, X, V, (GWAMD_LDS const uint8_t*)(lread), L, B, sc, ring,
+                                                           stage, spill, rowsz, lane, bp);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             wave_sync();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -1361,12 +1437,26 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
             // topsort: move-window refills, output: forward cycles, rowprog:
             // traceback steps, total: traceback cycles
             int64_t* ph8 = b.phase + size_t(w) * kPhases;
+            if (d.band_ad)
+            {
+                // anti-diagonal pass: general-step blocks, blocks, setup cycles,
+                // forward cycles, step-loop cycles, steps
+                ph8[kPhBackbone] = int64_t(bp.v[kBpMulti]);
+                ph8[kPhAdd]      = int64_t(bp.v[kBpAdBlocks]);
+                ph8[kPhTopsort]  = int64_t(bp.v[kBpAdSetup]);
+                ph8[kPhOutput]   = int64_t(bp.v[kBpFwdCyc]);
+                ph8[kPhRowProg]  = int64_t(bp.v[kBpAdLoop]);
+                ph8[kPhTotal]    = int64_t(bp.v[kBpAdSteps]);
+            }
+            else
+            {
             ph8[kPhBackbone] = int64_t(bp.v[kBpSlow]);
             ph8[kPhAdd]      = int64_t(bp.v[kBpAddSeq]);
             ph8[kPhTopsort]  = int64_t(bp.v[kBpRefill]);
             ph8[kPhOutput]   = int64_t(bp.v[kBpFwdCyc]);
             ph8[kPhRowProg]  = int64_t(bp.v[kBpSteps]);
             ph8[kPhTotal]    = int64_t(bp.v[kBpTbCyc]);
+            }
 #endif
         }
         b.final_nodes[w] = node_count;
@@ -1383,6 +1473,12 @@ __global__ void __launch_bounds__(kWave) poa_window_kernel_band(Buffers b, Dims 
     wave_sync();
     idx = uniform(sh_next);
     }
+    if (nw > 1)
+    {
+        if (lane == 0)
+            sh_job[0] = -1;
+        __syncthreads(); // release the helper waves
+    }
 }
 
 } // namespace poa
@@ -1394,7 +1490,7 @@ extern "C" hipError_t gwamd_internal_poa_band_launch(const gwamd::poa::Buffers* 
                                                      int msa, hipStream_t stream)
 {
     using namespace gwamd::poa;
-    const dim3 grid(b->head ? b->num_slots : b->num_windows), blk(kWave);
+    const dim3 grid(b->head ? b->num_slots : b->num_windows), blk(kWave * (d->band_ad ? d->band_ad : 1));
     const size_t lb = size_t(d->lds_bytes);
 #define GWAMD_BAND_LAUNCH(ST, ZT, MS, CPL)                                                                      \
     {                                                                                                         \
@@ -1447,7 +1543,8 @@ extern "C" int gwamd_internal_poa_band_blocks_per_cu(const gwamd::poa::Dims* d, 
                                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lb)) != hipSuccess) \
             return 0;                                                                                         \
         int n = 0;                                                                                            \
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kfn, kWave, lb) != hipSuccess)                   \
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kfn, kWave * (d->band_ad ? d->band_ad : 1), lb) !=      \
+            hipSuccess)                                                                                       \
             return 0;                                                                                         \
         return n;                                                                                             \
     }

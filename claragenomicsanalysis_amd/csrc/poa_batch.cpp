@@ -518,7 +518,10 @@ public:
     int32_t window_num_seqs(int32_t w) const { return h_win_.as<const gwamd::poa::WindowDesc>()[w].num_seqs; }
     int8_t output_mask() const { return output_mask_; }
     int64_t device_bytes() const { return int64_t(d_slab_.n + d_codes_.n + d_seqs_.n + d_wts_.n + d_len_.n + d_off_.n + d_win_.n); }
-    int32_t kernel_kind() const { return dims_.lds_kernel == 3 ? 3 : (dims_.lds_kernel ? 2 : 1); }
+    int32_t kernel_kind() const
+    {
+        return dims_.lds_kernel == 3 ? (dims_.band_ad ? 4 : 3) : (dims_.lds_kernel ? 2 : 1);
+    }
     int32_t max_poas() const { return max_poas_; }
     int32_t slots() const { return slots_; }
     int32_t resident_slots() const { return blocks_per_cu_; }
@@ -665,22 +668,32 @@ private:
         const int sbytes  = score_bits_ / 8;
         const int rowsz   = bw + gwamd::poa::kBandPad + cpl;
         const int64_t ms  = dims_.max_seq_len, mn = dims_.max_nodes;
-        const int64_t read_b  = a16(ms + bw + 48);
+        const int64_t read_b  = a16(gwamd::poa::kReadGuard + ms + bw + 48);
         const int64_t sh_b    = 64;
         const int64_t ring_b  = a16(int64_t(16) * rowsz * sbytes) + 4 * 256 * 4 + 1024 * 4; // + record staging
         const int64_t tile_b  = a16(int64_t(64) * bw + 512);
         const int64_t flags_b = a16(mn + 2);
         const int64_t add_b   = 5 * a16(ms + 16) + 2 * (mn + ms + 16) + 16;
-        const int64_t min_w   = std::max({ring_b, tile_b, flags_b});
+        // anti-diagonal forward pass (poa_band_ad.hpp): a kAdRing-row ring and
+        // one dummy word per lane.  Default: whenever the windows-per-CU
+        // choice below leaves room for it (large windows, one or two per CU);
+        // GWAMD_BAND_FWD=ad|row forces it on (planning for it) or off.
+        const int64_t ad_b    = a16(int64_t(gwamd::poa::kAdRing) * rowsz * sbytes + gwamd::poa::kWave * sbytes);
+        const char* fwd_env   = std::getenv("GWAMD_BAND_FWD");
+        const bool force_ad   = fwd_env && std::string(fwd_env) == "ad";
+        const bool no_ad      = fwd_env && std::string(fwd_env) == "row";
+        const int64_t min_w   = std::max({ring_b, tile_b, flags_b, force_ad ? ad_b : int64_t(0)});
         const int64_t want_w  = std::max(min_w, add_b);
-        const int64_t kStatic = 64; // static __shared__ words of the kernel
+        const int64_t kStatic = 256; // static __shared__ bytes of the kernel
         int64_t total         = 0;
+        int chosen_per_cu     = 1;
         for (int per_cu : {4, 2, 1})
         {
             const int64_t budget = (163840 / per_cu - kStatic) & ~int64_t(15);
-            if (read_b + want_w + sh_b <= budget || per_cu == 1)
+            if ((!force_ad && read_b + want_w + sh_b <= budget) || per_cu == 1)
             {
-                total = budget;
+                total         = budget;
+                chosen_per_cu = per_cu;
                 break;
             }
         }
@@ -688,6 +701,11 @@ private:
         if (work < min_w)
             return;
         dims_.lds_kernel     = 3;
+        // the pass runs kAdMaxWaves waves per window: one window per CU
+        int ad_waves = gwamd::poa::kAdMaxWaves;
+        if (const char* ev = std::getenv("GWAMD_BAND_AD_WAVES")) // diagnostic: fewer waves per window
+            ad_waves = std::max(1, std::min(gwamd::poa::kAdMaxWaves, std::atoi(ev)));
+        dims_.band_ad        = (!no_ad && chosen_per_cu == 1 && work >= ad_b) ? ad_waves : 0;
         dims_.lds_cpl        = cpl;
         dims_.lds_waves      = 1;
         dims_.lds_bytes      = int32_t(total);

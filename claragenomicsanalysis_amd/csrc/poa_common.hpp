@@ -20,6 +20,10 @@ constexpr int kBandPad       = 8;  // CUDAPOA_BANDED_MATRIX_RIGHT_PADDING (cudap
 constexpr int kWave          = 64; // CDNA wavefront
 constexpr int kCellsPerLane  = 8;  // full-mode DP: 8 consecutive columns per lane
 constexpr int kChunk         = kWave * kCellsPerLane; // 512 columns per wave pass
+constexpr int kAdRing        = 128; // LDS ring rows of the banded anti-diagonal pass (poa_band_ad.hpp)
+constexpr int kAdSpillDist   = kAdRing - kWave + 1; // successor distance that needs a spill row there
+constexpr int kReadGuard     = 64;  // banded kernel: LDS bytes in front of the staged read
+constexpr int kAdMaxWaves    = 4;   // waves of a banded workgroup running the anti-diagonal pass
 constexpr int kColShift      = 7;  // column j of a full-mode score row lives at index j + 7,
                                    // so each lane's 8 cells are one 16-B aligned group
 
@@ -86,6 +90,7 @@ struct Dims
     int32_t aux_bx_off;     //   | per-256-row-block predecessor-list offsets (i32)
     int32_t aux_recc_off;   //   | row records c (u32)
     int32_t aux_rece_off;   //   | row records e (u32)
+    int32_t band_ad;        // banded kernel: waves of the anti-diagonal forward pass (0: row-parallel pass)
 };
 
 // Small shared region of the LDS kernel (kShBytes(waves) at Dims::lds_sh_off):

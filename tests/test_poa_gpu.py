@@ -278,7 +278,7 @@ def test_banded_kernel_variants(variant, bw, monkeypatch):
                  b"GGGG" * 100, b"ACGTTGCA" * 20])
     wins.append([b"A" * 600, b"C" * 600, b"A" * 300 + b"C" * 300, b"ACGT"])
     b = run_gpu(wins, 800, 10, banded=True, bw=bw)
-    assert b.kernel_variant() == (1 if variant == "v1" else 3)
+    assert b.kernel_variant() in ((1,) if variant == "v1" else (3, 4))
     sbits = b.get_types()[0]
     cons, cov, st = b.get_consensus()
     for i, w in enumerate(wins):
@@ -290,11 +290,79 @@ def test_banded_kernel_msa_graph_int32(monkeypatch):
     monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
     wins = synth.poa_windows(701, 5, 900, 9, 45, 45, 45)
     b = run_gpu(wins, 4200, 9, banded=True, bw=256, output_type="msa")
-    assert b.kernel_variant() == 3 and b.get_types()[0] == 32
+    assert b.kernel_variant() in (3, 4) and b.get_types()[0] == 32
     msa, st = b.get_msa()
     for i, w in enumerate(wins):
         r = run_oracle(w, 4200, 9, banded=True, bw=256, msa=True, score_bits=32)
         assert (st[i], msa[i]) == (r.status, r.msa), i
+
+
+def _band_ad_windows(seed):
+    # uneven windows: long and short reads (gradient above and below 1), reads
+    # shorter than the band (every row starts at column 0), empty and one-base
+    # reads, repeats (many equal-score ties), and a 60-read window whose graph
+    # has nodes with many predecessors
+    wins = synth.poa_windows(seed, 4, 700, 10, 35, 35, 35)
+    wins += synth.poa_windows(seed + 100, 2, 1500, 6, 120, 120, 120)
+    wins += synth.poa_windows(seed + 200, 2, 90, 8, 6, 6, 6)
+    wins.append([b"ACGTTGCA" * 20, b"ACGTTGCA" * 80, b"", b"A", b"ACGTTGCA" * 40 + b"T" * 100,
+                 b"GGGG" * 100, b"ACGTTGCA" * 20])
+    wins.append([b"A" * 600, b"C" * 600, b"A" * 300 + b"C" * 300, b"ACGT"])
+    wins += synth.poa_windows(seed + 300, 1, 300, 60, 30, 30, 30)
+    return wins
+
+
+# Anti-diagonal forward pass of the banded kernel (poa_band_ad.hpp; default
+# for large windows, forced here with GWAMD_BAND_FWD=ad) against the oracle
+# and the row-parallel pass, 16- and 32-bit scores, both band widths,
+# consensus and MSA output, SPOA_ACCURATE sorts.
+@pytest.mark.parametrize("bw", [128, 256])
+@pytest.mark.parametrize("max_seq", [1700, 4200])
+@pytest.mark.parametrize("out", ["consensus", "msa"])
+def test_band_anti_diagonal(bw, max_seq, out, monkeypatch):
+    monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    wins = _band_ad_windows(1301)
+    msa = out == "msa"
+    res = {}
+    for fwd in ("ad", "row"):
+        monkeypatch.setenv("GWAMD_BAND_FWD", fwd)
+        b = run_gpu(wins, max_seq, 60, banded=True, bw=bw, output_type=out)
+        assert b.kernel_variant() == (4 if fwd == "ad" else 3)
+        res[fwd] = b.get_msa() if msa else b.get_consensus()
+        res[fwd + "_cells"] = b.get_stats()[0]
+        sbits = b.get_types()[0]
+    monkeypatch.delenv("GWAMD_BAND_FWD", raising=False)
+    assert res["ad"] == res["row"]
+    assert list(res["ad_cells"]) == list(res["row_cells"])
+    for i, w in enumerate(wins):
+        r = run_oracle(w, max_seq, 60, banded=True, bw=bw, msa=msa, score_bits=sbits)
+        if msa:
+            assert (res["ad"][1][i], res["ad"][0][i]) == (r.status, r.msa), i
+        else:
+            cons, cov, st = res["ad"]
+            assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), i
+
+
+@pytest.mark.parametrize("out", ["consensus", "msa"])
+def test_band_anti_diagonal_spoa_graph(out, monkeypatch):
+    monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    monkeypatch.setenv("GWAMD_BAND_FWD", "ad")
+    wins = synth.poa_windows(1401, 6, 400, 20, 20, 20, 20)
+    b = run_gpu(wins, 1000, 20, banded=True, bw=256, output_type=out, spoa_accurate=True)
+    assert b.kernel_variant() == 4
+    sbits = b.get_types()[0]
+    graphs, gst = b.get_graphs()
+    got = b.get_msa() if out == "msa" else b.get_consensus()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 1000, 20, banded=True, bw=256, msa=(out == "msa"), score_bits=sbits,
+                       want_graph=True, spoa_accurate=True)
+        if out == "msa":
+            assert (got[1][i], got[0][i]) == (r.status, r.msa), i
+        else:
+            assert (got[2][i], got[0][i], got[1][i]) == (r.status, r.consensus, r.coverage), i
+        g = graphs[i]
+        assert {(u, v): g.weight(u, v) for (u, v) in g.edges} == \
+            {(src, v): wt for v, ins in enumerate(r.graph["in"]) for (src, wt) in ins}, i
 
 
 @pytest.mark.parametrize("variant", ["v1", "fast"])
@@ -310,7 +378,7 @@ def test_spoa_accurate(variant, banded, out, monkeypatch):
         monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
     wins = synth.poa_windows(100, 16, 300, 20, 60, 60, 60)
     b = run_gpu(wins, 400, 20, banded=banded, bw=256, output_type=out, spoa_accurate=True)
-    assert b.kernel_variant() == (1 if variant == "v1" else (3 if banded else 2))
+    assert b.kernel_variant() in ((1,) if variant == "v1" else ((3, 4) if banded else (2,)))
     sbits = b.get_types()[0]
     if out == "msa":
         got, st = b.get_msa()
@@ -382,7 +450,7 @@ def test_persistent_grid_and_launch_order(mode, grid, monkeypatch):
     if mode == "v1":
         assert resident == 0 and b.kernel_variant() == 1
     else:
-        assert b.kernel_variant() == (3 if banded else 2)
+        assert b.kernel_variant() in ((3, 4) if banded else (2,))
         if "slots" in grid:
             assert slots < len(wins)
     sbits = b.get_types()[0]
