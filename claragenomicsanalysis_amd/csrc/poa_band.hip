@@ -1433,11 +1433,15 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
 #endif
 #ifdef GWAMD_BAND_PROFILE
             // counters over the phase slots (read raw: value = phase_ms * 1e5)
-            // backbone: traceback general steps, add: reads added sequentially,
+            // backbone: traceback tile-staging cycles, add: path-flush cycles,
             // topsort: move-window refills, output: forward cycles, rowprog:
             // traceback steps, total: traceback cycles
             int64_t* ph8 = b.phase + size_t(w) * kPhases;
+#ifdef GWAMD_BAND_PROFILE_AD
             if (d.band_ad)
+#else
+            if (false)
+#endif
             {
                 // anti-diagonal pass: general-step blocks, blocks, setup cycles,
                 // forward cycles, step-loop cycles, steps
@@ -1450,8 +1454,8 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
             }
             else
             {
-            ph8[kPhBackbone] = int64_t(bp.v[kBpSlow]);
-            ph8[kPhAdd]      = int64_t(bp.v[kBpAddSeq]);
+            ph8[kPhBackbone] = int64_t(bp.v[kBpTileCyc]);
+            ph8[kPhAdd]      = int64_t(bp.v[kBpFlushCyc]);
             ph8[kPhTopsort]  = int64_t(bp.v[kBpRefill]);
             ph8[kPhOutput]   = int64_t(bp.v[kBpFwdCyc]);
             ph8[kPhRowProg]  = int64_t(bp.v[kBpSteps]);
