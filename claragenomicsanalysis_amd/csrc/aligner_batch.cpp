@@ -21,6 +21,34 @@
 #include <thread>
 #include <vector>
 
+namespace gwamd
+{
+namespace host
+{
+// Length limits of this implementation (include/gwamd_cudaaligner.h).
+inline void aligner_max_lengths(int32_t algo, int32_t& max_query, int32_t& max_target)
+{
+    max_target = 65535; // 16-bit segment coordinates, LDS target codes
+    switch (algo)
+    {
+    case GWAMD_ALIGNER_HIRSCHBERG_MYERS: max_query = 16384; break; // register-resident Myers blocks
+    case GWAMD_ALIGNER_MYERS: max_query = 8192; break;
+    case GWAMD_ALIGNER_MYERS_BANDED: max_query = gwamd::aln::kBandChunks * gwamd::aln::kChunkWords * 32; break;
+    default:
+    {
+        // Ukkonen: (1 + int(0.1f * T) + 2p + 1) / 2 band rows, at most kUkChunks * 64
+        max_query = 65535;
+        int32_t t = 0;
+        while (t < 65535 && (1 + int32_t(float(t + 1) * 0.1f) + 2 * gwamd::aln::kUkkonenP + 1) / 2 <=
+                                gwamd::aln::kUkChunks * gwamd::aln::kWave)
+            t++;
+        max_target = t;
+    }
+    }
+}
+} // namespace host
+} // namespace gwamd
+
 extern "C" hipError_t gwamd_internal_align_launch(const gwamd::aln::Args* a, int algo, int grid, hipStream_t stream);
 extern "C" hipError_t gwamd_internal_align_occupancy(int algo, int lds_bytes, int* blocks_per_cu);
 extern "C" hipError_t gwamd_internal_banded_launch(const gwamd::aln::Args* a, int algo, int grid, hipStream_t stream);
@@ -180,18 +208,20 @@ public:
     {
         if (max_alignments < 1)
             throw std::runtime_error("Max alignments must be at least 1.");
-        // limits of this implementation: the Myers state of a query segment
-        // is held in 4 blocks of 64x32 bits; split scores are 16-bit in LDS
-        if (algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS && max_q_ > 16384)
-            throw std::invalid_argument("max_query_length above 16384 is not supported by this aligner.");
-        if (algo_ == GWAMD_ALIGNER_MYERS && max_q_ > 8192)
-            throw std::invalid_argument("max_query_length above 8192 is not supported by the full Myers aligner.");
-        if (algo_ == GWAMD_ALIGNER_MYERS_BANDED && max_q_ > gwamd::aln::kBandChunks * gwamd::aln::kChunkWords * 32)
-            throw std::invalid_argument("max_query_length above 8192 is not supported by the banded Myers aligner.");
+        // limits of this implementation (aligner_max_lengths; the reference has
+        // none): the Myers state of a query segment is register-resident
+        // (4 blocks of 64x32 bits), segment coordinates and split scores are
+        // 16-bit, the Ukkonen band has at most 512 diagonals
+        int32_t lim_q = 0, lim_t = 0;
+        gwamd::host::aligner_max_lengths(algo_, lim_q, lim_t);
+        if (max_q_ > lim_q)
+            throw std::invalid_argument("max_query_length above " + std::to_string(lim_q) +
+                                        " is not supported by this aligner.");
         if (algo_ == GWAMD_ALIGNER_UKKONEN && ukkonen_band_rows() > gwamd::aln::kUkChunks * gwamd::aln::kWave)
             throw std::invalid_argument("max_target_length too large for the Ukkonen aligner's band.");
-        if (max_t_ > 65535)
-            throw std::invalid_argument("max_target_length above 65535 is not supported by this aligner.");
+        if (max_t_ > lim_t)
+            throw std::invalid_argument("max_target_length above " + std::to_string(lim_t) +
+                                        " is not supported by this aligner.");
         stride_     = std::max(max_q_, max_t_);
         max_result_ = (max_q_ + max_t_ + 3) / 4 * 4; // calc_max_result_length (aligner_global.cpp:26-31)
         ScopedDevice dev(device_id_);
@@ -775,6 +805,18 @@ int32_t gwamd_aligner_get_config(const gwamd_aligner* a, int32_t* grid, int64_t*
 {
     *grid         = a->impl->grid();
     *device_bytes = a->impl->device_bytes();
+    return 0;
+}
+
+int32_t gwamd_aligner_max_lengths(int32_t algorithm, int32_t* max_query, int32_t* max_target)
+{
+    if (max_query == nullptr || max_target == nullptr || algorithm < GWAMD_ALIGNER_HIRSCHBERG_MYERS ||
+        algorithm > GWAMD_ALIGNER_UKKONEN)
+    {
+        gwamd::host::last_error() = "gwamd_aligner_max_lengths: bad algorithm or NULL output";
+        return GWAMD_E_INVALID_ARGUMENT;
+    }
+    gwamd::host::aligner_max_lengths(algorithm, *max_query, *max_target);
     return 0;
 }
 

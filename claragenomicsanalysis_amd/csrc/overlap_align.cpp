@@ -11,6 +11,7 @@
 #include <claraparabricks/genomeworks/cudamapper/overlap_alignment.hpp>
 #include <claraparabricks/genomeworks/io/fasta_parser.hpp>
 
+#include "../../include/gwamd_cudaaligner.h"
 #include "../../include/gwamd_cudamapper.h"
 #include "host_common.hpp"
 
@@ -152,11 +153,46 @@ struct Region
 
 using RegionFn = std::function<Region(int32_t)>;
 
-void run_engines(int32_t n, int32_t max_query_size, int32_t max_target_size, int32_t num_alignment_engines,
-                 const RegionFn& region, std::vector<std::string>& cigars)
+void run_engines_on(int32_t n, int32_t max_query_size, int32_t max_target_size, int32_t num_alignment_engines,
+                    const RegionFn& region, std::vector<std::string>& cigars);
+
+// Overlaps longer than the aligner's limits (gwamd_aligner_max_lengths; the
+// reference has none) are left without a CIGAR, with a warning on stderr, so
+// one long overlap does not fail the whole call; the others are aligned by an
+// aligner sized for them (main.cu:125-175 sizes it by the longest overlap).
+void run_engines(int32_t n, int32_t num_alignment_engines, const RegionFn& region, std::vector<std::string>& cigars)
 {
     if (num_alignment_engines < 1)
         throw std::runtime_error("num_alignment_engines must be at least 1");
+    int32_t lim_q = 0, lim_t = 0;
+    gwamd_aligner_max_lengths(GWAMD_ALIGNER_HIRSCHBERG_MYERS, &lim_q, &lim_t);
+    int32_t max_q = 0, max_t = 0;
+    std::vector<int32_t> kept;
+    kept.reserve(size_t(n));
+    for (int32_t i = 0; i < n; i++)
+    {
+        const Region r = region(i);
+        if (r.query_length > lim_q || r.target_length > lim_t)
+            continue;
+        kept.push_back(i);
+        max_q = std::max(max_q, r.query_length);
+        max_t = std::max(max_t, r.target_length);
+    }
+    if (int32_t(kept.size()) != n)
+        std::cerr << "align_overlaps: " << n - int32_t(kept.size())
+                  << " overlap(s) longer than the aligner's limits (query " << lim_q << ", target " << lim_t
+                  << " bases) left without a CIGAR" << std::endl;
+    std::vector<std::string> kept_cigars;
+    run_engines_on(int32_t(kept.size()), max_q, max_t, num_alignment_engines,
+                   [&](int32_t k) { return region(kept[size_t(k)]); }, kept_cigars);
+    cigars.assign(size_t(n), std::string());
+    for (size_t k = 0; k < kept.size(); k++)
+        cigars[size_t(kept[k])] = std::move(kept_cigars[k]);
+}
+
+void run_engines_on(int32_t n, int32_t max_query_size, int32_t max_target_size, int32_t num_alignment_engines,
+                    const RegionFn& region, std::vector<std::string>& cigars)
+{
     cigars.assign(size_t(n), std::string());
     if (n == 0)
         return;
@@ -274,7 +310,7 @@ std::string format_paf_impl(const std::vector<Overlap>& overlaps, const std::vec
                       int(o.target_start_position_in_read_), int(o.target_end_position_in_read_),
                       int(o.num_residues_ * uint32_t(kmer_size)), span, 255);
         out += buf;
-        if (!cigars.empty())
+        if (!cigars.empty() && !cigars[i].empty()) // no CIGAR: overlap not aligned
         {
             out += "\tcg:Z:";
             out += cigars[i];
@@ -290,19 +326,16 @@ void align_overlaps(DefaultDeviceAllocator /*allocator*/, std::vector<Overlap>& 
                     const io::FastaParser& query_parser, const io::FastaParser& target_parser,
                     int32_t num_alignment_engines, std::vector<std::string>& cigars)
 {
-    int32_t max_q = 0, max_t = 0;
+    if (overlaps.size() > size_t(INT32_MAX))
+        throw std::invalid_argument("too many overlaps for one call");
     for (const Overlap& o : overlaps)
     {
         check_range(o.query_start_position_in_read_, o.query_end_position_in_read_,
                     query_parser.get_sequence_by_id(o.query_read_id_).seq.size(), "query");
         check_range(o.target_start_position_in_read_, o.target_end_position_in_read_,
                     target_parser.get_sequence_by_id(o.target_read_id_).seq.size(), "target");
-        max_q = std::max<int32_t>(max_q, int32_t(o.query_end_position_in_read_ - o.query_start_position_in_read_));
-        max_t = std::max<int32_t>(max_t, int32_t(o.target_end_position_in_read_ - o.target_start_position_in_read_));
     }
-    if (overlaps.size() > size_t(INT32_MAX))
-        throw std::invalid_argument("too many overlaps for one call");
-    run_engines(int32_t(overlaps.size()), max_q, max_t, num_alignment_engines,
+    run_engines(int32_t(overlaps.size()), num_alignment_engines,
                 [&](int32_t i) {
                     const Overlap& o = overlaps[size_t(i)];
                     const std::string& q = query_parser.get_sequence_by_id(o.query_read_id_).seq;
@@ -414,7 +447,6 @@ int32_t gwamd_align_overlaps(const char* query_bases, const int64_t* query_offse
         check_offsets(query_offsets, num_queries, "queries");
         check_offsets(target_offsets, num_targets, "targets");
         std::vector<cm::Overlap> ov = to_overlaps(overlaps, num_overlaps);
-        int32_t max_q = 0, max_t = 0;
         for (const auto& o : ov)
         {
             if (o.query_read_id_ >= uint32_t(num_queries) || o.target_read_id_ >= uint32_t(num_targets))
@@ -426,9 +458,6 @@ int32_t gwamd_align_overlaps(const char* query_bases, const int64_t* query_offse
             if (o.target_start_position_in_read_ > o.target_end_position_in_read_ ||
                 o.target_end_position_in_read_ > tl)
                 throw std::invalid_argument("overlap target range outside its read");
-            max_q = std::max<int32_t>(max_q, int32_t(o.query_end_position_in_read_ - o.query_start_position_in_read_));
-            max_t = std::max<int32_t>(max_t,
-                                      int32_t(o.target_end_position_in_read_ - o.target_start_position_in_read_));
         }
         auto list = std::make_unique<gwamd_text_list>();
         if (num_overlaps == 0)
@@ -437,7 +466,7 @@ int32_t gwamd_align_overlaps(const char* query_bases, const int64_t* query_offse
             return 0;
         }
         gwamd::host::ScopedDevice dev(device_id);
-        cm::run_engines(num_overlaps, max_q, max_t, num_alignment_engines,
+        cm::run_engines(num_overlaps, num_alignment_engines,
                         [&](int32_t i) {
                             const cm::Overlap& o = ov[size_t(i)];
                             return cm::Region{query_bases + query_offsets[o.query_read_id_] +

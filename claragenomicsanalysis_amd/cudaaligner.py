@@ -46,7 +46,21 @@ def _declare(L):
     L.gwamd_aligner_get_paths.argtypes = [vp, P(vp), P(vp), P(i32)]
     L.gwamd_aligner_get_config.restype = i32
     L.gwamd_aligner_get_config.argtypes = [vp, P(i32), P(i64)]
+    L.gwamd_aligner_max_lengths.restype = i32
+    L.gwamd_aligner_max_lengths.argtypes = [i32, P(i32), P(i32)]
     del i8
+
+
+def max_lengths(algorithm="hirschberg_myers"):
+    """(max query length, max target length) this implementation's aligner
+    accepts (the reference has no limits; CudaAlignerBatch raises
+    ValueError above them, include/gwamd_cudaaligner.h)."""
+    from . import load_library
+    L = load_library()
+    _declare(L)
+    q, t = C.c_int32(), C.c_int32()
+    _check(L.gwamd_aligner_max_lengths(ALGORITHMS[algorithm], C.byref(q), C.byref(t)))
+    return q.value, t.value
 
 
 def status_to_str(status):

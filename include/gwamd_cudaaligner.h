@@ -21,6 +21,7 @@
  *   gwamd_alignment_format        Alignment::format_alignment              alignment.hpp:82-85
  *                                 (AlignmentImpl over given states,        alignment_impl.cpp:75-112)
  *   gwamd_alignment_cigar         Alignment::convert_to_cigar              alignment_impl.cpp:47-73
+ *   gwamd_aligner_max_lengths     (none: this implementation's length limits)
  *
  * Extra entry points (bench.py): split align_all into upload / launch /
  * download and read the raw device paths.
@@ -103,6 +104,15 @@ int32_t gwamd_aligner_get_paths(gwamd_aligner* aligner, const int8_t** paths, co
                                 int32_t* stride);
 /* Resident workgroups of the kernel (persistent grid) and device bytes. */
 int32_t gwamd_aligner_get_config(const gwamd_aligner* aligner, int32_t* grid, int64_t* device_bytes);
+
+/* Length limits of this implementation (the reference has none,
+ * aligner_global_hirschberg_myers.cpp:47-51): gwamd_aligner_create throws
+ * std::invalid_argument (GWAMD_E_INVALID_ARGUMENT) above them.  Hirschberg-
+ * Myers: query 16384, target 65535; full and banded Myers: query 8192;
+ * Ukkonen: target 65535 and a band of at most 512 diagonals.  *max_query and
+ * *max_target receive the query and target limits (Ukkonen: the largest
+ * target for which any query passes). */
+int32_t gwamd_aligner_max_lengths(int32_t algorithm, int32_t* max_query, int32_t* max_target);
 
 #ifdef __cplusplus
 }

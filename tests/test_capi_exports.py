@@ -72,3 +72,14 @@ def test_synthetic_generator_is_deterministic():
     assert a == b
     assert a[0][0] != a[1][0]
     assert len(a[0][0]) == 300
+
+
+def test_aligner_length_limits_are_queryable(built):
+    # this implementation's limits (the reference has none): documented in
+    # include/gwamd_cudaaligner.h, INTEGRATION.md and DESIGN.md
+    from claragenomicsanalysis_amd.cudaaligner import max_lengths
+    assert max_lengths("hirschberg_myers") == (16384, 65535)
+    assert max_lengths("myers") == (8192, 65535)
+    assert max_lengths("myers_banded") == (8192, 65535)
+    q, t = max_lengths("ukkonen")
+    assert q == 65535 and 8000 < t < 8300
