@@ -897,6 +897,8 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
     int ti0 = INT_MIN / 2;
     uint32_t ta = 0, tb = 0, tcw = 0; // row records of the tile rows, lane k: row ti0 + k
     static_assert(kBandTile == kWave, "tile records are held one per lane");
+    // per-row move-decode info of the tile rows, after the code tile
+    GWAMD_LDS v4i_t* rowinfo = reinterpret_cast<GWAMD_LDS v4i_t*>(tile + kBandTile * bw);
     int n = 0, loops = 0;
     const int bound = L + V + 2;
     int eg = 0, er = 0;
@@ -939,6 +941,19 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
             const int t = u * kWave + lane;
             *reinterpret_cast<GWAMD_LDS v4i_t*>(tile + (t / kPerRow) * bw + (t % kPerRow) * 16) = q[u];
         }
+        {
+            // per tile row (lane k: row ti0 + k), what a move decode needs:
+            // band start | no-predecessor flag (bit 30) | listed or escaped
+            // predecessors (bit 31), and the inline distances of slots 0-3
+            const int f       = ra_np(ta);
+            const bool listed = f == int(kNpEsc) || (tb >> 31);
+            v4i_t info;
+            info.x = int(uint32_t(ra_bs(ta)) | (f == 0 ? (1u << 30) : 0u) | (listed ? (1u << 31) : 0u));
+            info.y = int(tb);
+            info.z = int(tcw);
+            info.w = 0;
+            rowinfo[lane] = info;
+        }
         wave_sync();
         bp.add(kBpTileCyc, BandProf::now() - tt0);
     };
@@ -955,38 +970,25 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
     const bool win_ok       = V < 65535 && L < 65535;
     int wi0 = -1, wj0 = -1;
     uint32_t wpk0 = kSlow, wpk1 = kSlow;
+    // branch-free: the row's info from the LDS table, then its code byte
     auto decode_cell = [&](int t) -> uint32_t {
-        const int r   = wi0 - t / kWinC;
-        const int c   = wj0 - t % kWinC;
-        const int src = min(max(r - ti0, 0), kWave - 1);
-        const uint32_t a  = uint32_t(__builtin_amdgcn_ds_bpermute(src * 4, int(ta)));
-        const uint32_t b  = uint32_t(__builtin_amdgcn_ds_bpermute(src * 4, int(tb)));
-        const uint32_t cw = uint32_t(__builtin_amdgcn_ds_bpermute(src * 4, int(tcw)));
-        uint32_t res = kSlow;
-        const int bs = ra_bs(a);
-        if (r >= 1 && c >= 1 && r >= ti0 && r < ti0 + kBandTile && c >= bs + 1 && c <= bs + bw)
-        {
-            const int code = int(tile[(r - ti0) * bw + (c - bs - 1)]);
-            const int dir  = code & 3;
-            if (dir == 2)
-                res = (uint32_t(r) << 16) | uint32_t(c - 1);
-            else if (dir != 3)
-            {
-                const int f = ra_np(a);
-                int p       = -1;
-                if (f == 0)
-                    p = 0;
-                else if (f != int(kNpEsc) && !(b >> 31))
-                {
-                    const int k      = code >> 2;
-                    const uint32_t w = k < 2 ? b : cw;
-                    p                = r - int((k & 1) ? (w >> 16) : (w & 0xffffu));
-                }
-                if (p >= 0)
-                    res = (uint32_t(p) << 16) | uint32_t(dir == 0 ? c - 1 : c);
-            }
-        }
-        return res;
+        const int r      = wi0 - t / kWinC;
+        const int c      = wj0 - t % kWinC;
+        const int k      = min(max(r - ti0, 0), kWave - 1);
+        const v4i_t info = rowinfo[k];
+        const uint32_t x = uint32_t(info.x);
+        const int bs     = int(x & 0x3fffffffu);
+        const int idx    = c - bs - 1;
+        const bool ok    = r >= 1 && c >= 1 && r >= ti0 && r < ti0 + kBandTile && uint32_t(idx) < uint32_t(bw);
+        const int code   = int(tile[k * bw + min(max(idx, 0), bw - 1)]);
+        const int dir    = code & 3;
+        const int slot   = code >> 2;
+        const uint32_t w = uint32_t(slot < 2 ? info.y : info.z);
+        const int p      = (x & (1u << 30)) ? 0 : r - int((slot & 1) ? (w >> 16) : (w & 0xffffu));
+        const uint32_t mv = dir == 2 ? ((uint32_t(r) << 16) | uint32_t(c - 1))
+                                     : ((uint32_t(p) << 16) | uint32_t(dir == 0 ? c - 1 : c));
+        const bool slow = !ok || dir == 3 || (dir != 2 && (x >> 31) != 0);
+        return slow ? kSlow : mv;
     };
     while (!(i == 0 && j == 0) && loops < bound)
     {

@@ -671,7 +671,7 @@ private:
         const int64_t read_b  = a16(gwamd::poa::kReadGuard + ms + bw + 48);
         const int64_t sh_b    = 64;
         const int64_t ring_b  = a16(int64_t(16) * rowsz * sbytes) + 4 * 256 * 4 + 1024 * 4; // + record staging
-        const int64_t tile_b  = a16(int64_t(64) * bw + 512);
+        const int64_t tile_b  = a16(int64_t(64) * bw + 64 * 16 + 512); // codes + per-row decode info
         const int64_t flags_b = a16(mn + 2);
         const int64_t add_b   = 5 * a16(ms + 16) + 2 * (mn + ms + 16) + 16;
         // anti-diagonal forward pass (poa_band_ad.hpp): a kAdRing-row ring and
