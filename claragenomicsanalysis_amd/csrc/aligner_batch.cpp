@@ -197,8 +197,15 @@ private:
 class AlignerGlobalHip : public Aligner
 {
 public:
+    // device_budget: the caller's DefaultDeviceAllocator caching budget in
+    // bytes (-1: all available memory, allocator.hpp:282-298).  The reference
+    // serves every device buffer of the aligner from that pool; here the
+    // fixed buffers (sequences, paths, lengths) come first and the workspace
+    // gets as many persistent-grid slots as the rest of the budget holds; a
+    // budget below the fixed buffers plus one slot throws, as the reference's
+    // pool does when an allocation does not fit.
     AlignerGlobalHip(int32_t max_query_length, int32_t max_target_length, int32_t max_alignments, int algorithm,
-                     hipStream_t stream, int32_t device_id)
+                     hipStream_t stream, int32_t device_id, int64_t device_budget = -1)
         : max_q_(throw_on_negative(max_query_length, "max_query_length must be non-negative."))
         , max_t_(throw_on_negative(max_target_length, "max_target_length must be non-negative."))
         , max_n_(throw_on_negative(max_alignments, "max_alignments must be non-negative."))
@@ -226,6 +233,17 @@ public:
         max_result_ = (max_q_ + max_t_ + 3) / 4 * 4; // calc_max_result_length (aligner_global.cpp:26-31)
         ScopedDevice dev(device_id_);
         plan();
+        if (device_budget >= 0)
+        {
+            const int64_t fixed = int64_t(2) * stride_ * max_n_ + 16 + int64_t(2) * max_n_ * 4 +
+                                  int64_t(max_result_) * max_n_ + 16 + int64_t(max_n_) * 4;
+            const int64_t room  = (device_budget - fixed) / std::max<int64_t>(1, slot_bytes_);
+            if (room < 1)
+                throw std::runtime_error("The aligner needs " + std::to_string(fixed + slot_bytes_) +
+                                         " device bytes, more than max_device_memory_allocator_caching_size (" +
+                                         std::to_string(device_budget) + ").");
+            slots_ = int32_t(std::min<int64_t>(slots_, room));
+        }
         auto dalloc = [&](void** p, size_t bytes, bool zero = true) {
             GWAMD_HIP_CHECK(hipMalloc(p, std::max<size_t>(bytes, 16)));
             if (zero)
@@ -555,11 +573,11 @@ std::unique_ptr<Aligner> create_aligner(int32_t max_query_length, int32_t max_ta
                                         AlignmentType type, DefaultDeviceAllocator allocator, hipStream_t stream,
                                         int32_t device_id)
 {
-    (void)allocator;
     // aligner.cpp:30-38
     if (type == AlignmentType::global_alignment)
         return std::make_unique<AlignerGlobalHip>(max_query_length, max_target_length, max_alignments,
-                                                  GWAMD_ALIGNER_HIRSCHBERG_MYERS, stream, device_id);
+                                                  GWAMD_ALIGNER_HIRSCHBERG_MYERS, stream, device_id,
+                                                  allocator.max_cached_bytes());
     throw std::runtime_error("Aligner for specified type not implemented yet.");
 }
 
@@ -646,7 +664,8 @@ int32_t gwamd_aligner_create(gwamd_aligner** out, int32_t max_query_length, int3
             throw std::invalid_argument("unknown aligner algorithm");
         auto h  = std::make_unique<gwamd_aligner>();
         h->impl = std::make_unique<ca::AlignerGlobalHip>(max_query_length, max_target_length, max_alignments,
-                                                         algorithm, static_cast<hipStream_t>(stream), device_id);
+                                                         algorithm, static_cast<hipStream_t>(stream), device_id,
+                                                         max_caching);
         *out    = h.release();
         return int32_t(0);
     });

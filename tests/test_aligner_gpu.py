@@ -215,3 +215,28 @@ def test_ukkonen_add_alignment_status_codes():
     assert b.num_alignments() == case["final_count"]
     b.align_all()
     assert [a.cigar for a in b.get_alignments()] == [oracle.cigar(oracle.align("ATCG", "TACG", 3))] * 5
+
+
+def test_caching_budget_caps_the_workspace():
+    # max_device_memory_allocator_caching_size (aligner.hpp:103): the
+    # reference serves the aligner's device buffers from a pool of that size;
+    # here the workspace gets as many persistent-grid slots as the budget
+    # holds after the fixed buffers, and a budget below one slot throws
+    from oracle import oracle
+    free = CudaAlignerBatch(5000, 5000, 64)
+    grid_free, dev_free = free.config()
+    slot = (dev_free - 2 * 5000 * 64 - 16 - 2 * 64 * 4 - 10000 * 64 - 16 - 64 * 4) // grid_free
+    budget = dev_free - (grid_free - 3) * slot
+    b = CudaAlignerBatch(5000, 5000, 64, max_device_memory_allocator_caching_size=budget)
+    grid, dev = b.config()
+    assert grid == 3 and dev <= budget
+    rng = random.Random(3)
+    pairs = [("".join(rng.choice("ACGT") for _ in range(rng.randint(1, 5000))),
+              "".join(rng.choice("ACGT") for _ in range(rng.randint(1, 5000)))) for _ in range(20)]
+    for q, t in pairs:
+        assert b.add_alignment(q, t) == 0
+    b.align_all()
+    for (q, t), a in zip(pairs, b.get_alignments()):
+        assert a.cigar == oracle.cigar(oracle.align(q, t, oracle.ALIGN_HM, 5000))
+    with pytest.raises(RuntimeError):
+        CudaAlignerBatch(5000, 5000, 64, max_device_memory_allocator_caching_size=1 << 20)
