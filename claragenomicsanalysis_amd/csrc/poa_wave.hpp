@@ -499,20 +499,53 @@ __device__ __forceinline__ int add_alignment_parallel(WinGraph<SizeT> g, int& no
 // *ncols.  Returns false when the marks and a useful stack do not fit in the
 // scratch, or when the stack outgrows it (after a partial sort): the caller
 // then runs topsort_racon, which rewrites everything.
-template <typename SizeT>
-__device__ __forceinline__ bool topsort_racon_lds(WinGraph<SizeT> g, int n, GWAMD_LDS uint8_t* scratch,
-                                                  int scratch_bytes, int lane, SizeT* mpos, int* ncols)
+// CSR: when they fit next to the marks and a stack of at least kRaconCsrStack
+// entries, the predecessor and aligned-node lists are first copied to LDS
+// (per node one word: list offset | in-degree << 20 | aligned count << 26;
+// entries u16, predecessors then aligned nodes), so a DFS step reads no HBM.
+constexpr int kRaconCsrStack = 4096;
+
+template <typename SizeT, bool CSR>
+__device__ __forceinline__ bool topsort_racon_lds_impl(WinGraph<SizeT> g, int n, GWAMD_LDS uint8_t* scratch,
+                                                       int scratch_bytes, int lane, SizeT* mpos, int* ncols,
+                                                       int list_total)
 {
     g = as_global(g);
     n                 = uniform(n);
     const int marks_b = (n + 15) & ~15;
-    const int cap     = scratch_bytes > marks_b ? (scratch_bytes - marks_b) / 2 : 0;
+    const int info_b  = CSR ? n * 4 : 0;
+    const int list_b  = CSR ? ((list_total * 2 + 15) & ~15) : 0;
+    const int used    = marks_b + info_b + list_b;
+    const int cap     = scratch_bytes > used ? (scratch_bytes - used) / 2 : 0;
     if (scratch == nullptr || n <= 0 || n > 65535 || cap < 4 * kWave)
         return false;
     GWAMD_LDS uint8_t* marks  = scratch;
-    GWAMD_LDS uint16_t* stack = (GWAMD_LDS uint16_t*)(scratch + marks_b);
+    GWAMD_LDS uint32_t* info  = (GWAMD_LDS uint32_t*)(scratch + marks_b);
+    GWAMD_LDS uint16_t* lists = (GWAMD_LDS uint16_t*)(scratch + marks_b + info_b);
+    GWAMD_LDS uint16_t* stack = (GWAMD_LDS uint16_t*)(scratch + used);
     for (int v = lane; v < n; v += kWave)
         marks[v] = 4; // mark 0, check_aligned_nodes = true
+    if constexpr (CSR)
+    {
+        int base = 0;
+        for (int v0 = 0; v0 < n; v0 += kWave)
+        {
+            const int v  = v0 + lane;
+            const int ic = v < n ? int(g.in_cnt[v]) : 0;
+            const int ac = v < n ? int(g.aln_cnt[v]) : 0;
+            int total    = 0;
+            const int o  = base + wave_excl_sum(ic + ac, lane, total);
+            if (v < n)
+            {
+                info[v] = uint32_t(o) | (uint32_t(ic) << 20) | (uint32_t(ac) << 26);
+                for (int e = 0; e < ic; e++)
+                    lists[o + e] = uint16_t(int(g.in_e[v * kMaxEdges + e]));
+                for (int e = 0; e < ac; e++)
+                    lists[o + ic + e] = uint16_t(int(g.aln[v * kMaxAlignments + e]));
+            }
+            base += total;
+        }
+    }
     wave_sync();
     int k = 0, col = 0;
     for (int v0 = 0; v0 < n; v0++)
@@ -532,10 +565,23 @@ __device__ __forceinline__ bool topsort_racon_lds(WinGraph<SizeT> g, int n, GWAM
             bool valid  = true;
             if ((m & 3) != 2)
             {
-                const int ic      = uniform(int(g.in_cnt[id]));
-                const int ac      = (m & 4) ? uniform(int(g.aln_cnt[id])) : 0;
-                const int bl      = lane < ic ? int(g.in_e[id * kMaxEdges + lane]) : 0;
-                const int al      = lane < ac ? int(g.aln[id * kMaxAlignments + lane]) : 0;
+                int ic, ac, bl, al;
+                if constexpr (CSR)
+                {
+                    const uint32_t w = uint32_t(uniform(int(info[id])));
+                    const int o      = int(w & 0xfffffu);
+                    ic               = int((w >> 20) & 63u);
+                    ac               = (m & 4) ? int(w >> 26) : 0;
+                    bl               = lane < ic ? int(lists[o + lane]) : 0;
+                    al               = lane < ac ? int(lists[o + ic + lane]) : 0;
+                }
+                else
+                {
+                    ic = uniform(int(g.in_cnt[id]));
+                    ac = (m & 4) ? uniform(int(g.aln_cnt[id])) : 0;
+                    bl = lane < ic ? int(g.in_e[id * kMaxEdges + lane]) : 0;
+                    al = lane < ac ? int(g.aln[id * kMaxAlignments + lane]) : 0;
+                }
                 const int mb      = lane < ic ? int(marks[bl]) : 2;
                 const int ma      = lane < ac ? int(marks[al]) : 2;
                 const bool nb     = lane < ic && (mb & 3) != 2;
@@ -601,6 +647,30 @@ __device__ __forceinline__ bool topsort_racon_lds(WinGraph<SizeT> g, int n, GWAM
     if (ncols)
         *ncols = col;
     return true;
+}
+
+template <typename SizeT>
+__device__ __forceinline__ bool topsort_racon_lds(WinGraph<SizeT> g, int n, GWAMD_LDS uint8_t* scratch,
+                                                  int scratch_bytes, int lane, SizeT* mpos, int* ncols)
+{
+    g = as_global(g);
+    n = uniform(n);
+    if (scratch == nullptr || n <= 0 || n > 65535)
+        return false;
+    // list entries of the CSR copy
+    int total = 0;
+    for (int v0 = 0; v0 < n; v0 += kWave)
+    {
+        const int v = v0 + lane;
+        int t       = 0;
+        wave_excl_sum(v < n ? int(g.in_cnt[v]) + int(g.aln_cnt[v]) : 0, lane, t);
+        total += t;
+    }
+    total = uniform(total);
+    const int need = ((n + 15) & ~15) + n * 4 + ((total * 2 + 15) & ~15) + 2 * kRaconCsrStack;
+    if (total < (1 << 20) && need <= scratch_bytes)
+        return topsort_racon_lds_impl<SizeT, true>(g, n, scratch, scratch_bytes, lane, mpos, ncols, total);
+    return topsort_racon_lds_impl<SizeT, false>(g, n, scratch, scratch_bytes, lane, mpos, ncols, 0);
 }
 
 // SPOA_ACCURATE per-read sort (cudapoa_kernels.cuh:324-337): the LDS racon
