@@ -879,7 +879,7 @@ template <typename ScoreT, typename SizeT, int CPL>
 __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int V, const uint8_t* read, int L,
                               int end_row, const Band& B, const Scores sc, const ScoreT* spill, int rowsz,
                               GWAMD_LDS uint8_t* tile, SizeT* ag, SizeT* ar, int aln_cap,
-                              int lane, BandProf& bp)
+                              int lane, BandProf& bp, bool rank)
 {
     X = as_global(X);
     spill = glb(spill);
@@ -1016,6 +1016,10 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
             }
             // walk the window: every value here is wave-uniform (SGPRs)
             int ci = i, cj = j, cn = n, cl = loops;
+            if (rank)
+                walk_window_ranked<kWinR, kWinC, 1>(wpk0, wpk1, wi0, wj0, ci, cj, cn, cl, bound, lane, eg, er,
+                                                    tile + kBandTile * bw + kWave * 16 + 512, flush);
+            else
             while (true)
             {
                 const int idx     = (wi0 - ci) * kWinC + (wj0 - cj);
@@ -1349,7 +1353,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             ph.lap<kPhForward>();
             const int alen = band_traceback<ScoreT, SizeT, CPL>(g, X, V, lread, L, end_row, B, sc, spill, rowsz, tile,
-                                                                ag, ar, d.aln_cap, lane, bp);
+                                                                ag, ar, d.aln_cap, lane, bp, d.tb_rank != 0);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             wave_sync();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");

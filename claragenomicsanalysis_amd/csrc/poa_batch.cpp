@@ -615,7 +615,7 @@ private:
             }
         }
         const int64_t add_b  = 5 * a16(dims_.max_seq_len + 16) + 2 * (int64_t(dims_.max_nodes) + dims_.max_seq_len);
-        const int64_t tile_b = int64_t(gwamd::poa::kTileRows) * gwamd::poa::kTileCols;
+        const int64_t tile_b = int64_t(gwamd::poa::kTileRows) * gwamd::poa::kTileCols + gwamd::poa::kTbRankBytes;
         const int64_t ring_b = a16(std::max<int64_t>({int64_t(ring_rows) * dims_.score_stride * 2, tile_b, add_b}));
         const int64_t rec_b  = a16(int64_t(dims_.max_nodes + 2) * 4);
         const int64_t sh_b   = a16(gwamd::poa::kShBytes(nw));
@@ -630,6 +630,7 @@ private:
         if (total > 65536)
             return;
         dims_.lds_kernel    = 1;
+        dims_.tb_rank       = tb_rank_default();
         dims_.lds_ring_off  = int32_t(read_b);
         dims_.lds_ring_rows = ring_rows;
         dims_.lds_rec_off   = int32_t(read_b + ring_b);
@@ -653,6 +654,14 @@ private:
     // traceback tile, the add-alignment scratch; the topological sort also
     // reuses the read) | shared words.  Windows per CU: 4, 2 or 1, the most
     // that leave room for the work region at this batch's maximum sizes.
+    // traceback move-window walk: pointer doubling (default) or the scalar
+    // walk (GWAMD_TB_WALK=scalar, for parity tests and diagnostics)
+    static int tb_rank_default()
+    {
+        const char* ev = std::getenv("GWAMD_TB_WALK");
+        return (ev && std::string(ev) == "scalar") ? 0 : 1;
+    }
+
     void plan_band_kernel()
     {
         if (!banded_ || dims_.lds_kernel)
@@ -671,7 +680,8 @@ private:
         const int64_t read_b  = a16(gwamd::poa::kReadGuard + ms + bw + 48);
         const int64_t sh_b    = 64;
         const int64_t ring_b  = a16(int64_t(16) * rowsz * sbytes) + 4 * 256 * 4 + 1024 * 4; // + record staging
-        const int64_t tile_b  = a16(int64_t(64) * bw + 64 * 16 + 512); // codes + per-row decode info
+        const int64_t tile_b  = a16(int64_t(64) * bw + 64 * 16 + 512 + gwamd::poa::kTbRankBytes); // codes +
+                                                                      // per-row decode info + walk tables
         const int64_t flags_b = a16(mn + 2);
         const int64_t add_b   = 5 * a16(ms + 16) + 2 * (mn + ms + 16) + 16;
         // anti-diagonal forward pass (poa_band_ad.hpp): a kAdRing-row ring and
@@ -706,6 +716,7 @@ private:
         if (const char* ev = std::getenv("GWAMD_BAND_AD_WAVES")) // diagnostic: fewer waves per window
             ad_waves = std::max(1, std::min(gwamd::poa::kAdMaxWaves, std::atoi(ev)));
         dims_.band_ad        = (!no_ad && chosen_per_cu == 1 && work >= ad_b) ? ad_waves : 0;
+        dims_.tb_rank        = tb_rank_default();
         dims_.lds_cpl        = cpl;
         dims_.lds_waves      = 1;
         dims_.lds_bytes      = int32_t(total);

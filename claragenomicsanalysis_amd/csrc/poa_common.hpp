@@ -91,7 +91,11 @@ struct Dims
     int32_t aux_recc_off;   //   | row records c (u32)
     int32_t aux_rece_off;   //   | row records e (u32)
     int32_t band_ad;        // banded kernel: waves of the anti-diagonal forward pass (0: row-parallel pass)
+    int32_t tb_rank;        // traceback move windows walked by pointer doubling (0: scalar walk)
 };
+
+// LDS bytes of the pointer-doubling traceback walk (walk_window_ranked)
+constexpr int kTbRankBytes = 5 * 144 + 128 * 4;
 
 // Small shared region of the LDS kernel (kShBytes(waves) at Dims::lds_sh_off):
 // control ints, per-wave channel progress, the end-row slot, the per-span

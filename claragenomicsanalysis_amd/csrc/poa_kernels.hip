@@ -925,7 +925,7 @@ __device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, con
 template <typename SizeT>
 __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L, int end_row,
                                const uint8_t* codes, int code_stride, uint8_t* tile, SizeT* ag, SizeT* ar,
-                               int aln_cap, int lane)
+                               int aln_cap, int lane, bool rank)
 {
     g = as_global(g);
 
@@ -1040,6 +1040,10 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
             }
             // walk the window: every value here is wave-uniform (SGPRs)
             int ci = i, cj = j, cn = n, cl = loops;
+            if (rank)
+                walk_window_ranked<kWinR, kWinC, 0>(wpk0, wpk1, wi0, wj0, ci, cj, cn, cl, bound, lane, eg, er,
+                                                    (GWAMD_LDS uint8_t*)(tile + kTileRows * kTileCols), flush);
+            else
             while (true)
             {
                 const int idx     = (wi0 - ci) * kWinC + (wj0 - cj);
@@ -1240,7 +1244,7 @@ __global__ void __launch_bounds__(kWave * NW, NW >= 4 ? 4 : 1) poa_window_kernel
             if (wave == 0)
             {
                 const int alen_w = traceback_codes<SizeT>(g, P, V, L, end_row, codes, d.code_stride, tile, ag, ar,
-                                                          d.aln_cap, lane);
+                                                          d.aln_cap, lane, d.tb_rank != 0);
                 if (lane == 0)
                     sh_len = alen_w;
             }

@@ -938,5 +938,91 @@ __device__ __forceinline__ bool topsort_lds_big(WinGraph<SizeT> g, int n, GWAMD_
     return true;
 }
 
+// ---------------------------------------------------------------------------
+// Traceback move-window walk by pointer doubling.  The window holds the moves
+// of kWinR x kWinC = 128 cells (cell t: row wi0 - t / kWinC, column
+// wj0 - t % kWinC), two per lane (wpk0: cell lane, wpk1: cell lane + 64),
+// packed (row << 16 | column) or kSlow when the general step must decide.
+// The scalar walk takes one cell per iteration (~350 cycles of dependent
+// scalar code); here every lane finds the cell of one path step at once:
+// J0 maps a cell to the next cell in the window (kX: the move leaves the
+// window, a slow cell maps to itself), J1..J4 = J^2, J^4, J^8, J^16 are built
+// in LDS, and lane L follows step k = (L - cn) mod 64 by the binary digits of
+// k.  A path inside the window has at most kWinR + kWinC - 1 < 32 steps.  The
+// steps taken are a prefix in k; each lane writes its own (eg, er) entry
+// exactly as the scalar walk would have, with the flush at the 64-entry
+// boundary in between.  Updates (ci, cj) to the cell after the last step, cn
+// (entries) and cl (loop count, capped at bound).  kCmin: the smallest column
+// that stays in the window (0 full mode, 1 banded).  Same results as the
+// scalar walk by construction; parity is tested with both (GWAMD_TB_WALK).
+template <int kWinR, int kWinC, int kCmin, typename Flush>
+__device__ __forceinline__ void walk_window_ranked(uint32_t wpk0, uint32_t wpk1, int wi0, int wj0, int& ci, int& cj,
+                                                   int& cn, int& cl, int bound, int lane, int& eg, int& er,
+                                                   GWAMD_LDS uint8_t* scratch, Flush&& flush)
+{
+    static_assert(kWinR * kWinC == 2 * kWave, "two window cells per lane");
+    static_assert(kWinR + kWinC - 1 < 32, "paths inside the window need at most 5 doubling levels");
+    constexpr uint32_t kSlow = 0xffffffffu;
+    constexpr int kX         = 2 * kWave;
+    constexpr int kS         = 144; // level stride (129 entries: index kX maps to itself)
+    GWAMD_LDS uint8_t* J     = scratch;
+    GWAMD_LDS uint32_t* W    = (GWAMD_LDS uint32_t*)(scratch + 5 * kS);
+    auto next_cell = [&](int t, uint32_t nx) -> int {
+        const int pi  = int(nx >> 16), pj = int(nx & 0xffffu);
+        const bool in = pi >= 1 && pj >= kCmin && pi <= wi0 && pi > wi0 - kWinR && pj <= wj0 && pj > wj0 - kWinC;
+        return nx == kSlow ? t : (in ? (wi0 - pi) * kWinC + (wj0 - pj) : kX);
+    };
+    int ja = next_cell(lane, wpk0), jb = next_cell(lane + kWave, wpk1);
+    wave_sync(); // the previous walk's readers are done with the tables
+    J[lane]         = uint8_t(ja);
+    J[lane + kWave] = uint8_t(jb);
+    W[lane]         = wpk0;
+    W[lane + kWave] = wpk1;
+    if (lane < 5)
+        J[lane * kS + kX] = uint8_t(kX);
+#pragma unroll
+    for (int m = 1; m < 5; m++)
+    {
+        wave_sync();
+        ja = int(J[(m - 1) * kS + ja]);
+        jb = int(J[(m - 1) * kS + jb]);
+        J[m * kS + lane]         = uint8_t(ja);
+        J[m * kS + lane + kWave] = uint8_t(jb);
+    }
+    wave_sync();
+    const int k = (lane - cn) & (kWave - 1);
+    int c       = (wi0 - ci) * kWinC + (wj0 - cj);
+#pragma unroll
+    for (int m = 0; m < 5; m++)
+    {
+        const int c2 = int(J[m * kS + c]);
+        c            = ((k >> m) & 1) ? c2 : c;
+    }
+    const uint32_t nx = c < kX ? W[c] : kSlow;
+    const bool taken  = k < 32 && nx != kSlow && cl + k < bound;
+    const int steps   = __popcll(__builtin_amdgcn_ballot_w64(taken));
+    if (steps == 0)
+        return;
+    const int r = wi0 - c / kWinC, col = wj0 - c % kWinC;
+    const int pi = int(nx >> 16), pj = int(nx & 0xffffu);
+    const int neg = r == pi ? -1 : r;
+    const int ner = col == pj ? -1 : col - 1;
+    const int e   = cn + k;
+    const int B   = (cn | (kWave - 1)) + 1; // next 64-entry flush boundary
+    if (taken && e < B)
+        eg = neg, er = ner;
+    if (cn + steps >= B)
+    {
+        flush(B);
+        if (taken && e >= B)
+            eg = neg, er = ner;
+    }
+    const int last = (cn + steps - 1) & (kWave - 1);
+    ci             = __builtin_amdgcn_readlane(pi, last);
+    cj             = __builtin_amdgcn_readlane(pj, last);
+    cn += steps;
+    cl += steps;
+}
+
 } // namespace poa
 } // namespace gwamd

@@ -470,3 +470,39 @@ def test_persistent_grid_and_launch_order(mode, grid, monkeypatch):
             assert (st[i], got[i]) == (r.status, want), (mode, grid, rep, i)
             expect = {(src, v): wt for v, ins in enumerate(r.graph["in"]) for (src, wt) in ins}
             assert {(u, v): graphs[i].weight(u, v) for (u, v) in graphs[i].edges} == expect, (mode, grid, rep, i)
+
+
+# Traceback move-window walk: pointer doubling (default) and the scalar walk
+# (GWAMD_TB_WALK=scalar) give identical alignments, so identical outputs, on
+# the full-mode LDS kernel and the banded kernel (row-parallel and
+# anti-diagonal forward), consensus and MSA, against the oracle; the windows
+# include repeats, empty/one-base reads and reads shorter than the band.
+@pytest.mark.parametrize("mode", ["full", "band_row", "band_ad"])
+@pytest.mark.parametrize("out", ["consensus", "msa"])
+def test_traceback_walk_modes(mode, out, monkeypatch):
+    monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    banded = mode != "full"
+    if banded:
+        monkeypatch.setenv("GWAMD_BAND_FWD", "ad" if mode == "band_ad" else "row")
+    wins = _band_ad_windows(1501)
+    # full mode: the LDS kernel's shape (config B's 1,100-base windows)
+    ms = 1700 if banded else 1100
+    wins = [w for w in wins if max(len(r) for r in w) < ms - 60]
+    msa = out == "msa"
+    res = {}
+    for walk in ("rank", "scalar"):
+        monkeypatch.setenv("GWAMD_TB_WALK", walk)
+        b = run_gpu(wins, ms, 60, banded=banded, bw=256, output_type=out)
+        assert b.kernel_variant() == {"full": 2, "band_row": 3, "band_ad": 4}[mode]
+        res[walk] = b.get_msa() if msa else b.get_consensus()
+        sbits = b.get_types()[0]
+    monkeypatch.delenv("GWAMD_TB_WALK", raising=False)
+    monkeypatch.delenv("GWAMD_BAND_FWD", raising=False)
+    assert res["rank"] == res["scalar"]
+    for i, w in enumerate(wins):
+        r = run_oracle(w, ms, 60, banded=banded, bw=256, msa=msa, score_bits=sbits)
+        if msa:
+            assert (res["rank"][1][i], res["rank"][0][i]) == (r.status, r.msa), i
+        else:
+            cons, cov, st = res["rank"]
+            assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), i
