@@ -448,7 +448,7 @@ def bench_poa(ctx, key, steps, warmup, args, with_cpu):
     cpu = None
     if with_cpu and ctx.world == 1:
         th = cpu_threads()
-        ns = args.cpu_sample or min(nwin, max(th * (1 if msa else 8), 16 if msa else 64))
+        ns = args.cpu_sample or min(nwin, max(th * (4 if msa else 8), 64))
         tc = time.perf_counter()
         res = oracle.poa_batch(windows[:ns], nthreads=th, banded=cfg["banded"], band_width=cfg["bw"],
                                score_bits=score_bits, max_nodes=mn, max_consensus=2 * cfg["max_seq"],
