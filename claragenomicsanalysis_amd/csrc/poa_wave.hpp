@@ -8,6 +8,7 @@
 
 #include <climits>
 #include <cstdint>
+#include <type_traits>
 
 #include "poa_device.hpp"
 
@@ -789,8 +790,10 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
 #ifdef GWAMD_TOPSORT_PROFILE
     const uint64_t tp1 = __builtin_amdgcn_s_memtime();
 #endif
-    {
-        // FIFO (cudapoa_topsort.cuh:58-85)
+    // FIFO (cudapoa_topsort.cuh:58-85), instantiated with and without the
+    // queued info words so the loop carries no per-node mode test
+    auto fifo = [&](auto useq_tag) -> int {
+        constexpr bool kUseQ = decltype(useq_tag)::value;
         int tail       = uniform(k);
         int q          = 0;
         uint32_t vinfo = tail > 0 ? uint32_t(uniform(int(info[int(queue[0])]))) : 0u;
@@ -798,26 +801,56 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
         {
             // the loop state is wave-uniform; saying so keeps it in SGPRs with
             // scalar branches whatever the caller's control flow looks like
-            tail                = uniform(tail);
-            q                   = uniform(q);
-            vinfo               = uint32_t(uniform(int(vinfo)));
-            const int deg       = int((vinfo >> 16) & 63u);
-            const int qtail     = tail; // entries pushed by this step start here
-            uint32_t first_info = 0;
+            tail    = uniform(tail);
+            q       = uniform(q);
+            vinfo   = uint32_t(uniform(int(vinfo)));
+            int deg = int((vinfo >> 16) & 63u);
             if (deg == 1)
             {
-                const int o       = int(vinfo & 0xffffu);
-                const uint32_t oi = uint32_t(uniform(int(info[o]))) - (1u << 24);
-                info[o]           = oi;
-                if ((oi >> 24) == 0u)
+                // single-successor run: one dependent LDS read per node.  A
+                // released node's word is not written back (nothing decrements
+                // it again and a pop uses only its degree and successor bits),
+                // and one popped next comes from the register, not the queue.
+                bool more = true;
+                do
                 {
-                    first_info = oi;
-                    if (use_q)
-                        qinfo[tail] = oi;
-                    queue[tail++] = uint16_t(o);
-                }
+                    const int o       = int(vinfo & 0xffffu);
+                    const uint32_t oi = uint32_t(uniform(int(info[o]))) - (1u << 24);
+                    q++;
+                    if ((oi >> 24) == 0u)
+                    {
+                        queue[tail] = uint16_t(o);
+                        if (q == tail)
+                        {
+                            tail++;
+                            vinfo = oi;
+                        }
+                        else
+                        {
+                            if (kUseQ)
+                                qinfo[tail] = oi;
+                            tail++;
+                            vinfo = uint32_t(uniform(int(kUseQ ? qinfo[q] : info[int(queue[q])])));
+                        }
+                    }
+                    else
+                    {
+                        info[o] = oi;
+                        if (q < tail)
+                            vinfo = uint32_t(uniform(int(kUseQ ? qinfo[q] : info[int(queue[q])])));
+                        else
+                            more = false;
+                    }
+                    q     = uniform(q);
+                    tail  = uniform(tail);
+                    vinfo = uint32_t(uniform(int(vinfo)));
+                    deg   = int((vinfo >> 16) & 63u);
+                } while (more && deg == 1);
+                continue;
             }
-            else if (deg >= 2)
+            const int qtail     = tail; // entries pushed by this step start here
+            uint32_t first_info = 0;
+            if (deg >= 2)
             {
                 // all successors at once, one per lane: children are distinct,
                 // so the decrements are independent; ready ones are queued in
@@ -836,7 +869,7 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
                     if (rdy)
                     {
                         queue[tail + before] = uint16_t(o);
-                        if (use_q)
+                        if (kUseQ)
                             qinfo[tail + before] = oi;
                     }
                     first_info = uint32_t(__builtin_amdgcn_readlane(int(oi), __builtin_ctzll(ready)));
@@ -846,8 +879,12 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
             q++;
             if (q < tail)
                 vinfo = (q == qtail) ? first_info
-                                     : uint32_t(uniform(int(use_q ? qinfo[q] : info[int(queue[q])])));
+                                     : uint32_t(uniform(int(kUseQ ? qinfo[q] : info[int(queue[q])])));
         }
+        return tail;
+    };
+    {
+        const int tail = use_q ? fifo(std::integral_constant<bool, true>{}) : fifo(std::integral_constant<bool, false>{});
         if (lane == 0)
             sh[0] = tail;
     }
