@@ -811,8 +811,7 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
                 // released node's word is not written back (nothing decrements
                 // it again and a pop uses only its degree and successor bits),
                 // and one popped next comes from the register, not the queue.
-                bool more = true;
-                do
+                for (;;)
                 {
                     const int o       = int(vinfo & 0xffffu);
                     const uint32_t oi = uint32_t(uniform(int(info[o]))) - (1u << 24);
@@ -824,28 +823,24 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
                         {
                             tail++;
                             vinfo = oi;
+                            if (((oi >> 16) & 63u) == 1u)
+                                continue;
+                            break;
                         }
-                        else
-                        {
-                            if (kUseQ)
-                                qinfo[tail] = oi;
-                            tail++;
-                            vinfo = uint32_t(uniform(int(kUseQ ? qinfo[q] : info[int(queue[q])])));
-                        }
+                        if (kUseQ)
+                            qinfo[tail] = oi;
+                        tail++;
                     }
                     else
                     {
                         info[o] = oi;
-                        if (q < tail)
-                            vinfo = uint32_t(uniform(int(kUseQ ? qinfo[q] : info[int(queue[q])])));
-                        else
-                            more = false;
+                        if (q >= tail)
+                            break;
                     }
-                    q     = uniform(q);
-                    tail  = uniform(tail);
-                    vinfo = uint32_t(uniform(int(vinfo)));
-                    deg   = int((vinfo >> 16) & 63u);
-                } while (more && deg == 1);
+                    vinfo = uint32_t(uniform(int(kUseQ ? qinfo[q] : info[int(queue[q])])));
+                    if (((vinfo >> 16) & 63u) != 1u)
+                        break;
+                }
                 continue;
             }
             const int qtail     = tail; // entries pushed by this step start here
