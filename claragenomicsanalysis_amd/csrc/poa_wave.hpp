@@ -767,7 +767,13 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
     // queued nodes' final info words next to the queue when they fit: a pop is
     // then one LDS read instead of two dependent ones
     const int qinfo_off          = (head_bytes + ebase * 2 + 15) & ~15;
-    const bool use_q             = uniform(int(qinfo_off + n * 4 <= scratch_bytes)) != 0;
+    // (all n of them, or for graphs too large for that a ring of the last
+    // kQRing pushes: a pop at q reads the ring while tail - q <= kQRing, the
+    // node word otherwise; the queue holds about the graph's width)
+    constexpr int kQRing = 1024;
+    const int q_mode     = uniform(qinfo_off + n * 4 <= scratch_bytes ? 1 : (qinfo_off + kQRing * 4 <= scratch_bytes ? 2 : 0));
+    const bool use_q     = q_mode != 0;
+    const uint32_t qmask = q_mode == 2 ? uint32_t(kQRing - 1) : 0xffffffffu;
     GWAMD_LDS uint32_t* qinfo    = (GWAMD_LDS uint32_t*)(scratch + qinfo_off);
     // sources in id order
     int k = 0;
@@ -782,7 +788,7 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
         {
             queue[k + ex] = uint16_t(v);
             if (use_q)
-                qinfo[k + ex] = vi;
+                qinfo[uint32_t(k + ex) & qmask] = vi;
         }
         k += total;
     }
@@ -793,7 +799,12 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
     // FIFO (cudapoa_topsort.cuh:58-85), instantiated with and without the
     // queued info words so the loop carries no per-node mode test
     auto fifo = [&](auto useq_tag) -> int {
-        constexpr bool kUseQ = decltype(useq_tag)::value;
+        constexpr int kMode = decltype(useq_tag)::value; // 0 node words, 1 all queued words, 2 ring
+        auto pop_info = [&](int qq, int tl) -> uint32_t {
+            if (kMode == 1 || (kMode == 2 && tl - qq <= kQRing))
+                return uint32_t(uniform(int(qinfo[uint32_t(qq) & (kMode == 2 ? uint32_t(kQRing - 1) : 0xffffffffu)])));
+            return uint32_t(uniform(int(info[int(queue[qq])])));
+        };
         int tail       = uniform(k);
         int q          = 0;
         uint32_t vinfo = tail > 0 ? uint32_t(uniform(int(info[int(queue[0])]))) : 0u;
@@ -827,8 +838,8 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
                                 continue;
                             break;
                         }
-                        if (kUseQ)
-                            qinfo[tail] = oi;
+                        if (kMode != 0)
+                            qinfo[uint32_t(tail) & qmask] = oi;
                         tail++;
                     }
                     else
@@ -837,7 +848,7 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
                         if (q >= tail)
                             break;
                     }
-                    vinfo = uint32_t(uniform(int(kUseQ ? qinfo[q] : info[int(queue[q])])));
+                    vinfo = pop_info(q, tail);
                     if (((vinfo >> 16) & 63u) != 1u)
                         break;
                 }
@@ -864,8 +875,8 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
                     if (rdy)
                     {
                         queue[tail + before] = uint16_t(o);
-                        if (kUseQ)
-                            qinfo[tail + before] = oi;
+                        if (kMode != 0)
+                            qinfo[uint32_t(tail + before) & qmask] = oi;
                     }
                     first_info = uint32_t(__builtin_amdgcn_readlane(int(oi), __builtin_ctzll(ready)));
                     tail += __popcll(ready);
@@ -874,12 +885,14 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
             q++;
             if (q < tail)
                 vinfo = (q == qtail) ? first_info
-                                     : uint32_t(uniform(int(kUseQ ? qinfo[q] : info[int(queue[q])])));
+                                     : pop_info(q, tail);
         }
         return tail;
     };
     {
-        const int tail = use_q ? fifo(std::integral_constant<bool, true>{}) : fifo(std::integral_constant<bool, false>{});
+        const int tail = q_mode == 1 ? fifo(std::integral_constant<int, 1>{})
+                                     : (q_mode == 2 ? fifo(std::integral_constant<int, 2>{})
+                                                    : fifo(std::integral_constant<int, 0>{}));
         if (lane == 0)
             sh[0] = tail;
     }
