@@ -95,7 +95,7 @@ struct Dims
 };
 
 // LDS bytes of the pointer-doubling traceback walk (walk_window_ranked)
-constexpr int kTbRankBytes = 5 * 144 + 128 * 4;
+constexpr int kTbRankBytes = 7 * 144 + 128 * 4;
 
 // Small shared region of the LDS kernel (kShBytes(waves) at Dims::lds_sh_off):
 // control ints, per-wave channel progress, the end-row slot, the per-span

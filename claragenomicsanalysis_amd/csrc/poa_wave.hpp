@@ -991,9 +991,10 @@ __device__ __forceinline__ bool topsort_lds_big(WinGraph<SizeT> g, int n, GWAMD_
 // The scalar walk takes one cell per iteration (~350 cycles of dependent
 // scalar code); here every lane finds the cell of one path step at once:
 // J0 maps a cell to the next cell in the window (kX: the move leaves the
-// window, a slow cell maps to itself), J1..J4 = J^2, J^4, J^8, J^16 are built
-// in LDS, and lane L follows step k = (L - cn) mod 64 by the binary digits of
-// k.  A path inside the window has at most kWinR + kWinC - 1 < 32 steps.  The
+// window, a slow cell maps to itself), J^2, J^3, J^4, J^8, J^12 and J^16 are
+// built in LDS (4 dependent rounds), and lane L follows step
+// k = (L - cn) mod 64 by the base-4 digits of k (3 dependent reads).  A path
+// inside the window has at most kWinR + kWinC - 1 < 32 steps.  The
 // steps taken are a prefix in k; each lane writes its own (eg, er) entry
 // exactly as the scalar walk would have, with the flush at the 64-entry
 // boundary in between.  Updates (ci, cj) to the cell after the last step, cn
@@ -1006,42 +1007,61 @@ __device__ __forceinline__ void walk_window_ranked(uint32_t wpk0, uint32_t wpk1,
                                                    GWAMD_LDS uint8_t* scratch, Flush&& flush)
 {
     static_assert(kWinR * kWinC == 2 * kWave, "two window cells per lane");
-    static_assert(kWinR + kWinC - 1 < 32, "paths inside the window need at most 5 doubling levels");
+    static_assert(kWinR + kWinC - 1 < 32, "paths inside the window have fewer than 32 steps");
     constexpr uint32_t kSlow = 0xffffffffu;
     constexpr int kX         = 2 * kWave;
-    constexpr int kS         = 144; // level stride (129 entries: index kX maps to itself)
+    constexpr int kS         = 144; // table stride (129 entries: index kX maps to itself)
+    // tables: 0 J, 1 J^2, 2 J^3, 3 J^4, 4 J^8, 5 J^12, 6 J^16
     GWAMD_LDS uint8_t* J     = scratch;
-    GWAMD_LDS uint32_t* W    = (GWAMD_LDS uint32_t*)(scratch + 5 * kS);
+    GWAMD_LDS uint32_t* W    = (GWAMD_LDS uint32_t*)(scratch + 7 * kS);
     auto next_cell = [&](int t, uint32_t nx) -> int {
         const int pi  = int(nx >> 16), pj = int(nx & 0xffffu);
         const bool in = pi >= 1 && pj >= kCmin && pi <= wi0 && pi > wi0 - kWinR && pj <= wj0 && pj > wj0 - kWinC;
         return nx == kSlow ? t : (in ? (wi0 - pi) * kWinC + (wj0 - pj) : kX);
     };
-    int ja = next_cell(lane, wpk0), jb = next_cell(lane + kWave, wpk1);
+    auto put = [&](int tab, int va, int vb) {
+        J[tab * kS + lane]         = uint8_t(va);
+        J[tab * kS + lane + kWave] = uint8_t(vb);
+    };
+    const int ja = next_cell(lane, wpk0), jb = next_cell(lane + kWave, wpk1);
     wave_sync(); // the previous walk's readers are done with the tables
-    J[lane]         = uint8_t(ja);
-    J[lane + kWave] = uint8_t(jb);
+    put(0, ja, jb);
     W[lane]         = wpk0;
     W[lane + kWave] = wpk1;
-    if (lane < 5)
+    if (lane < 7)
         J[lane * kS + kX] = uint8_t(kX);
-#pragma unroll
-    for (int m = 1; m < 5; m++)
-    {
-        wave_sync();
-        ja = int(J[(m - 1) * kS + ja]);
-        jb = int(J[(m - 1) * kS + jb]);
-        J[m * kS + lane]         = uint8_t(ja);
-        J[m * kS + lane + kWave] = uint8_t(jb);
-    }
     wave_sync();
-    const int k = (lane - cn) & (kWave - 1);
-    int c       = (wi0 - ci) * kWinC + (wj0 - cj);
-#pragma unroll
-    for (int m = 0; m < 5; m++)
+    const int a2 = int(J[ja]), b2 = int(J[jb]);
+    put(1, a2, b2);
+    wave_sync();
+    const int a3 = int(J[a2]), b3 = int(J[b2]);
+    const int a4 = int(J[kS + a2]), b4 = int(J[kS + b2]);
+    put(2, a3, b3);
+    put(3, a4, b4);
+    wave_sync();
+    const int a8 = int(J[3 * kS + a4]), b8 = int(J[3 * kS + b4]);
+    put(4, a8, b8);
+    wave_sync();
+    const int a12 = int(J[3 * kS + a8]), b12 = int(J[3 * kS + b8]);
+    const int a16 = int(J[4 * kS + a8]), b16 = int(J[4 * kS + b8]);
+    put(5, a12, b12);
+    put(6, a16, b16);
+    wave_sync();
+    // step k = d0 + 4 d1 + 16 d2: three dependent reads
+    const int k  = (lane - cn) & (kWave - 1);
+    const int d0 = k & 3, d1 = (k >> 2) & 3, d2 = (k >> 4) & 1;
+    int c        = (wi0 - ci) * kWinC + (wj0 - cj);
     {
-        const int c2 = int(J[m * kS + c]);
-        c            = ((k >> m) & 1) ? c2 : c;
+        const int c2 = int(J[max(d0 - 1, 0) * kS + c]);
+        c            = d0 ? c2 : c;
+    }
+    {
+        const int c2 = int(J[(d1 + 2) * kS + c]);
+        c            = d1 ? c2 : c;
+    }
+    {
+        const int c2 = int(J[6 * kS + c]);
+        c            = d2 ? c2 : c;
     }
     const uint32_t nx = c < kX ? W[c] : kSlow;
     const bool taken  = k < 32 && nx != kSlow && cl + k < bound;
