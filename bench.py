@@ -107,8 +107,12 @@ def parse():
     p.add_argument("--secondary-steps", type=int, default=3, help="timed steps of the D object")
     p.add_argument("--stream-batches", type=int, default=2, help="E: concurrent batches (streams + host threads)")
     p.add_argument("--stream-batch-windows", type=int, default=4096, help="E: windows per batch")
-    p.add_argument("--traffic-file", default=None,
-                   help="PMC HBM bytes per launch (default profiles/traffic_poa_<config>.json)")
+    p.add_argument("--stream-step-windows", type=int, default=None,
+                   help="E: windows per step (default %d; 20 steps = 125k windows per GPU)" % E_STEP_WINDOWS)
+    p.add_argument("--secondary-c-steps", type=int, default=3, help="timed steps of the default run's C object")
+    p.add_argument("--dry-run", action="store_true",
+                   help="CPU rehearsal of the multi-rank launch (gloo): config E with stand-in rows instead of the "
+                        "GPU engine; prints a line marked dry_run that is not a measurement")
     return p.parse_args()
 
 
@@ -180,23 +184,44 @@ def load_sq(key):
 
 
 class Ctx:
-    def __init__(self):
+    """One process per GPU (torch.distributed.run sets RANK / LOCAL_RANK /
+    WORLD_SIZE); RCCL ("nccl") between the ranks.  dry: gloo on CPU, no GPU."""
+
+    def __init__(self, dry=False):
+        self.dry = dry
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if dry:
+            if self.world > 1:
+                dist.init_process_group("gloo")
+            self.dev = None
+            self.device = "cpu"
+            return
         if self.world > 1:
             dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
         torch.cuda.set_device(self.local_rank)
         self.dev = self.local_rank
+        self.device = "cuda"
 
     def barrier(self):
         if self.world > 1:
             dist.barrier()
 
+    def sync(self):
+        if not self.dry:
+            torch.cuda.synchronize()
+
     def max_over_ranks(self, v):
-        t = torch.tensor([v], dtype=torch.float64, device="cuda")
+        t = torch.tensor([v], dtype=torch.float64, device=self.device)
         if self.world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(self, v):
+        t = torch.tensor([v], dtype=torch.float64, device=self.device)
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return float(t.item())
 
 
@@ -214,6 +239,11 @@ def roofline(alg_bytes, kernel_ms, traffic, kernel, source=None, sq=None):
         r["traffic_source"] = source
     if sq:
         r["sq"] = sq
+        if sq.get("valu_issue_util") is not None:
+            # the kernels are issue-bound: VALU issue slots used / available (SQ
+            # counters of the committed profile, scripts/sq_summary.py)
+            r["valu_issue_frac"] = sq["valu_issue_util"]
+            r["valu_issue_source"] = sq.get("source")
     return r
 
 
@@ -508,60 +538,110 @@ def bench_poa(ctx, key, steps, warmup, args, with_cpu):
 # ---------------------------------------------------------------------------
 # config E: the multi-batch streaming driver, step = E_STEP_WINDOWS windows
 # ---------------------------------------------------------------------------
+def busy_union_ms(start, stop):
+    """Time during which at least one of the launches [start_i, stop_i) ran."""
+    tot, cur_a, cur_b = 0.0, None, None
+    for a, b in sorted(zip(start.tolist(), stop.tolist())):
+        if cur_b is None or a > cur_b:
+            if cur_b is not None:
+                tot += cur_b - cur_a
+            cur_a, cur_b = a, b
+        else:
+            cur_b = max(cur_b, b)
+    if cur_b is not None:
+        tot += cur_b - cur_a
+    return tot
+
+
+def dry_rows(first_seed, n, width):
+    """Dry run stand-in for the GPU engine's output: a deterministic function of
+    each window's global seed (status 0, length, bytes, coverage), so rank 0
+    can check the gathered rows window by window."""
+    seeds = np.arange(first_seed, first_seed + n, dtype=np.int64)
+    clen = (1 + seeds % (width - 1)).astype(np.int32)
+    col = np.arange(width, dtype=np.int64)[None, :]
+    live = col < clen[:, None]
+    cons = np.where(live, np.array(list(b"ACGT"), np.uint8)[(seeds[:, None] + col) % 4], 0).astype(np.uint8)
+    cov = np.where(live, (seeds[:, None] * 7 + col) % 65521, 0).astype(np.uint16)
+    return np.zeros(n, np.int32), clen, cons, cov
+
+
 def bench_stream(ctx, key, steps, warmup, args, with_cpu):
     cfg = dict(STREAM_CONFIGS[key])
     from claragenomicsanalysis_amd import synth
-    from claragenomicsanalysis_amd.cudapoa import CudaPoaMultiBatch, estimate_max_poas
+    from claragenomicsanalysis_amd.shard import stream_window_range, gather_rows
 
-    from claragenomicsanalysis_amd.shard import stream_window_range
-    per_step = cfg["windows_per_step"]
+    per_step = args.stream_step_windows or cfg["windows_per_step"]
     first_seed, nwin = stream_window_range(ctx.rank, steps, per_step)
     t0 = time.time()
-    bases, lens = synth.poa_windows_packed(first_seed, nwin, cfg["backbone"], cfg["reads"], cfg["err"], cfg["err"],
-                                           cfg["err"])
+    if ctx.dry:
+        bases = np.zeros(0, np.uint8)
+        lens = np.zeros((nwin, cfg["reads"]), np.int32)
+    else:
+        bases, lens = synth.poa_windows_packed(first_seed, nwin, cfg["backbone"], cfg["reads"], cfg["err"],
+                                               cfg["err"], cfg["err"])
     gen_s = time.time() - t0
     read_lens = lens.ravel()
     rpw = np.full(nwin, cfg["reads"], np.int64)
-    # device bytes per batch so that a batch holds stream_batch_windows windows
-    # by the reference's own capacity rule (BatchBlock::estimate_max_poas)
-    probe = 64 << 30
-    per_window = probe / max(1, estimate_max_poas(cfg["max_seq"], cfg["reads"], cfg["bw"], banded=cfg["banded"],
-                                                  msa=False, free_device_memory=probe,
-                                                  gpu_memory_usage_quota=1.0))
-    mem = int(per_window * args.stream_batch_windows) + (64 << 20)
-    mb = CudaPoaMultiBatch(cfg["reads"], cfg["max_seq"], num_batches=args.stream_batches, mem_per_batch=mem,
-                           device_id=ctx.dev, cuda_banded_alignment=cfg["banded"], alignment_band_width=cfg["bw"])
-    stride = mb.stride
-    out = (np.zeros(nwin, np.int32), np.zeros(nwin, np.int32), np.zeros((nwin, stride), np.uint8),
-           np.zeros((nwin, stride), np.uint16))
-    for a in out:  # touch the pages outside the timed region
-        a.fill(0)
-    if warmup > 0:  # untimed pass over this rank's first warmup x step windows
-        wn = min(nwin, warmup * per_step)
-        nb = int(read_lens[:wn * cfg["reads"]].sum())
-        mb.process_packed(bases[:nb], read_lens[:wn * cfg["reads"]], rpw[:wn])
-    ctx.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    mb.process_packed(bases, read_lens, rpw, out=out)
-    torch.cuda.synchronize()
-    ctx.barrier()
-    wall = time.perf_counter() - t_start
+    launches = None
+    nb_used = per_batch = rounds = mem = None
+    if ctx.dry:
+        stride = 2 * cfg["max_seq"]
+        ctx.barrier()
+        t_start = time.perf_counter()
+        status, clen, cons, cov = dry_rows(first_seed, nwin, stride)
+        ctx.barrier()
+        wall = time.perf_counter() - t_start
+    else:
+        from claragenomicsanalysis_amd.cudapoa import CudaPoaMultiBatch, estimate_max_poas
+        # device bytes per batch so that a batch holds stream_batch_windows windows
+        # by the reference's own capacity rule (BatchBlock::estimate_max_poas)
+        probe = 64 << 30
+        per_window = probe / max(1, estimate_max_poas(cfg["max_seq"], cfg["reads"], cfg["bw"], banded=cfg["banded"],
+                                                      msa=False, free_device_memory=probe,
+                                                      gpu_memory_usage_quota=1.0))
+        mem = int(per_window * args.stream_batch_windows) + (64 << 20)
+        mb = CudaPoaMultiBatch(cfg["reads"], cfg["max_seq"], num_batches=args.stream_batches, mem_per_batch=mem,
+                               device_id=ctx.dev, cuda_banded_alignment=cfg["banded"],
+                               alignment_band_width=cfg["bw"])
+        stride = mb.stride
+        out = (np.zeros(nwin, np.int32), np.zeros(nwin, np.int32), np.zeros((nwin, stride), np.uint8),
+               np.zeros((nwin, stride), np.uint16))
+        for arr in out:  # touch the pages outside the timed region
+            arr.fill(0)
+        if warmup > 0:  # untimed pass over this rank's first warmup x step windows
+            wn = min(nwin, warmup * per_step)
+            nb = int(read_lens[:wn * cfg["reads"]].sum())
+            mb.process_packed(bases[:nb], read_lens[:wn * cfg["reads"]], rpw[:wn])
+        # HIP events around every kernel launch, on each batch's own stream
+        mb.set_launch_timing(True)
+        ctx.barrier()
+        ctx.sync()
+        t_start = time.perf_counter()
+        mb.process_packed(bases, read_lens, rpw, out=out)
+        ctx.sync()
+        ctx.barrier()
+        wall = time.perf_counter() - t_start
+        launches = mb.launches()
+        status, clen, cons, cov = out
+        nb_used, per_batch, rounds = mb.info()
     wall_max = ctx.max_over_ranks(wall)
-    status, clen, cons, cov = out
-    nb_used, per_batch, rounds = mb.info()
     n_ok = int((status == 0).sum())
 
+    # Final gather (SURVEY.md 8(e)): every rank's [len | status | consensus |
+    # coverage] rows to rank 0 over RCCL, one dist.gather, rows trimmed to the
+    # longest consensus of the job.
     gather_ms = None
     gathered = None
-    if ctx.world > 1:  # every rank's consensus rows to rank 0 over RCCL
-        from claragenomicsanalysis_amd.shard import gather_rows
-        torch.cuda.synchronize()
+    width = None
+    if ctx.world > 1:
+        width = int(ctx.max_over_ranks(float(clen.max() if nwin else 0)))
+        ctx.sync()
         tg = time.perf_counter()
-        rows = np.concatenate([clen.view(np.uint8).reshape(nwin, 4), status.view(np.uint8).reshape(nwin, 4), cons],
-                              axis=1)
-        gathered = gather_rows(rows, device="cuda")
-        torch.cuda.synchronize()
+        rows = np.concatenate([clen.view(np.uint8).reshape(nwin, 4), status.view(np.uint8).reshape(nwin, 4),
+                               cons[:, :width], np.ascontiguousarray(cov[:, :width]).view(np.uint8)], axis=1)
+        gathered = gather_rows(rows, device=ctx.device)
+        ctx.sync()
         gather_ms = (time.perf_counter() - tg) * 1e3
     if ctx.rank != 0:
         return None
@@ -569,25 +649,92 @@ def bench_stream(ctx, key, steps, warmup, args, with_cpu):
     if gathered is not None:
         glen = gathered[:, :4].copy().view(np.int32).ravel()
         gst = gathered[:, 4:8].copy().view(np.int32).ravel()
+        gcons = gathered[:, 8:8 + width]
+        gcov = gathered[:, 8 + width:].copy().view(np.uint16)
         parity["gathered_windows"] = int(gathered.shape[0])
+        parity["gathered_bytes"] = int(gathered.nbytes)
         parity["gathered_all_status_ok"] = bool((gst == 0).all() and (glen > 0).all())
         parity["gathered_rank0_rows_equal_local"] = bool(
-            np.array_equal(gathered[:nwin, 8:], cons) and np.array_equal(glen[:nwin], clen))
-    # oracle check of a sample spread over the rank's stream (windows from every batch round)
+            np.array_equal(gcons[:nwin], cons[:, :width]) and np.array_equal(gcov[:nwin], cov[:, :width]) and
+            np.array_equal(glen[:nwin], clen))
+    if ctx.dry:
+        if gathered is not None:
+            es, el, ec, ev = dry_rows(1, nwin * ctx.world, stride)
+            parity["gathered_rows_equal_expected"] = bool(
+                np.array_equal(gst, es) and np.array_equal(glen, el) and np.array_equal(gcons, ec[:, :width]) and
+                np.array_equal(gcov, ev[:, :width]))
+        return {"metric": "POA windows/sec (consensus)", "value": None, "unit": "windows/s", "dry_run": True,
+                "n_gpus": ctx.world, "steps": steps, "warmup": warmup, "ms_per_step": None,
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16",
+                "data": "dry run on CPU (gloo): stand-in rows, no GPU, not a measurement",
+                "config": {"workload": "config E rehearsal", "config_key": key, "windows_per_gpu": nwin,
+                           "gather_width": width, "gather_ms": gather_ms,
+                           "parallelism": "dp%d (windows sharded, gloo gather)" % ctx.world},
+                "roofline": None, "cpu_baseline": None, "parity": parity}
+
+    # oracle check of a sample spread over the rank's stream (windows from every
+    # batch round) and, at N > 1, of windows the other ranks computed
     from oracle import oracle
-    idx = sorted(set(np.linspace(0, nwin - 1, 12).astype(int).tolist()))
     starts = np.concatenate([[0], np.cumsum(read_lens)])
-    samp = []
-    for i in idx:
+
+    def window_reads(i):
         r0 = i * cfg["reads"]
-        samp.append([bases[starts[r]:starts[r + 1]].tobytes() for r in range(r0, r0 + cfg["reads"])])
+        return [bases[starts[r]:starts[r + 1]].tobytes() for r in range(r0, r0 + cfg["reads"])]
+
+    idx = sorted(set(np.linspace(0, nwin - 1, 12).astype(int).tolist()))
     mn = 3 * cfg["max_seq"]
-    rcons, rst, rcov, _, used = oracle.poa_batch(samp, nthreads=cpu_threads(), max_nodes=mn,
-                                                 max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"],
-                                                 coverage=True)
+    rcons, rst, rcov, _, used = oracle.poa_batch([window_reads(i) for i in idx], nthreads=cpu_threads(),
+                                                 max_nodes=mn, max_consensus=2 * cfg["max_seq"],
+                                                 max_seqs=cfg["reads"], coverage=True)
     ok = all(rst[j] == status[i] and rcons[j] == cons[i, :clen[i]].tobytes().decode() and
              list(rcov[j]) == cov[i, :clen[i]].tolist() for j, i in enumerate(idx))
     parity.update({"windows_checked": len(idx), "bit_exact_vs_oracle": bool(ok)})
+    if gathered is not None:
+        # two windows of every other rank, regenerated here from their seeds
+        gidx = [r * nwin + k for r in range(1, ctx.world) for k in (0, nwin - 1)]
+        wins = []
+        for g in gidx:
+            b1, l1 = synth.poa_windows_packed(1 + g, 1, cfg["backbone"], cfg["reads"], cfg["err"], cfg["err"],
+                                              cfg["err"])
+            wins.append(windows_from_packed(b1, l1)[0])
+        gc, gs, gv, _, _ = oracle.poa_batch(wins, nthreads=cpu_threads(), max_nodes=mn,
+                                            max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"], coverage=True)
+        parity["gathered_other_ranks_checked"] = len(gidx)
+        parity["gathered_other_ranks_bit_exact_vs_oracle"] = bool(all(
+            gs[j] == gst[g] and gc[j] == gcons[g, :glen[g]].tobytes().decode() and
+            list(gv[j]) == gcov[g, :glen[g]].tolist() for j, g in enumerate(gidx)))
+
+    # roofline of the streamed kernels: SURVEY 8(d) priced bytes of every launch
+    # (4 B per int16 DP cell + inputs + outputs) over the time the GPU ran at
+    # least one of them (the batches' kernels overlap on their two streams)
+    cells_total = int(launches["cells"].sum())
+    alg_bytes = cells_total * 2 * 2 + 2 * int(read_lens.sum()) + 3 * int(clen.sum())
+    busy_ms = busy_union_ms(launches["start_ms"], launches["stop_ms"])
+    durations = launches["stop_ms"] - launches["start_ms"]
+    traffic, tsrc = load_traffic("poa", key, nwin)
+    roof = roofline(alg_bytes, busy_ms, traffic, "poa_window_kernel_lds", tsrc, load_sq("poa_" + key))
+    roof.update({"launches": int(len(durations)), "kernel_ms_sum": round(float(durations.sum()), 3),
+                 "kernel_busy_ms": round(busy_ms, 3), "kernel_ms_mean_per_launch": round(float(durations.mean()), 3),
+                 "windows_per_launch_mean": round(float(launches["windows"].mean()), 1),
+                 "timing": "HIP events on each batch's stream around every launch, one clock; kernel_ms = the "
+                           "union of the launch intervals (the kernels of the two batches overlap)"})
+    cpu = None
+    if with_cpu and ctx.world == 1:
+        th = cpu_threads()
+        ns = args.cpu_sample or min(nwin, max(th * 8, 64))
+        sidx = sorted(set(np.linspace(0, nwin - 1, ns).astype(int).tolist()))
+        tc = time.perf_counter()
+        cc, cs, cv, _, cused = oracle.poa_batch([window_reads(i) for i in sidx], nthreads=th, max_nodes=mn,
+                                                max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"],
+                                                coverage=True)
+        cpu_s = time.perf_counter() - tc
+        match = all(cs[j] == status[i] and cc[j] == cons[i, :clen[i]].tobytes().decode() and
+                    list(cv[j]) == cov[i, :clen[i]].tolist() for j, i in enumerate(sidx))
+        cpu = dict({"value": round(len(sidx) / cpu_s, 3), "unit": "windows/s", "kind": "port",
+                    "sample": "%d windows spread evenly over the same stream, oracle/poa_oracle.cpp "
+                              "(reference-algorithm C++ restatement, not SPOA), OpenMP one window per thread, "
+                              "%.1f s wall" % (len(sidx), cpu_s),
+                    "matches_gpu": bool(match), "compared": "status, consensus, coverage"}, **cpu_fields(th, cused))
     total = nwin * ctx.world
     return {
         "metric": "POA windows/sec (consensus)",
@@ -604,12 +751,15 @@ def bench_stream(ctx, key, steps, warmup, args, with_cpu):
                    "config_key": key,
                    "step": "%d windows through MultiBatch::process_batches (fill + H2D + kernel + D2H timed, "
                            "multi_batch.hpp:64-171)" % per_step,
-                   "windows_per_gpu": nwin, "batches": nb_used, "windows_per_batch": per_batch,
-                   "batch_rounds": rounds, "mem_per_batch": mem, "batch_size": [cfg["max_seq"], cfg["reads"]],
-                   "scores": [-8, -6, 8], "parallelism": "dp%d (windows sharded, RCCL gather)" % ctx.world,
-                   "windows_ok": n_ok, "gather_ms": gather_ms, "input_gen_s": round(gen_s, 2)},
-        "roofline": None,
-        "cpu_baseline": None,
+                   "windows_per_gpu": nwin, "windows_total": total, "batches": nb_used,
+                   "windows_per_batch": per_batch, "batch_rounds": rounds, "mem_per_batch": mem,
+                   "batch_size": [cfg["max_seq"], cfg["reads"]], "scores": [-8, -6, 8],
+                   "parallelism": "dp%d (windows sharded, RCCL gather)" % ctx.world,
+                   "windows_ok": n_ok, "dp_cells": cells_total,
+                   "gcups": round(cells_total / (busy_ms / 1e3) / 1e9, 3),
+                   "gather_ms": gather_ms, "gather_width": width, "input_gen_s": round(gen_s, 2)},
+        "roofline": roof,
+        "cpu_baseline": cpu,
         "parity": parity,
     }
 
@@ -620,17 +770,47 @@ RUNNERS.update({k: bench_aligner for k in ALIGNER_CONFIGS})
 RUNNERS.update({k: bench_stream for k in STREAM_CONFIGS})
 
 
+def free_port():
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def relaunch(args):
+    """--gpus N > 1 outside torch.distributed.run: start N ranks (one process
+    per GPU, the reference's one worker per device, cudamapper/src/main.cu:488-
+    513) as a child torch.distributed.run and return its exit code.  Runs
+    before anything touches the GPU; the child is a subprocess, not an exec."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", str(max(1, cpu_threads() // args.gpus)))
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
-    ctx = Ctx()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(args))
+    ctx = Ctx(dry=args.dry_run)
+    if args.gpus > 1 and ctx.world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, ctx.world))
     default = args.config is None
     key = args.config or ("B" if ctx.world == 1 else "E")
+    if ctx.dry and key != "E":
+        raise SystemExit("--dry-run rehearses config E only")
     line = RUNNERS[key](ctx, key, args.steps, args.warmup, args, not args.no_cpu)
-    if default and ctx.world == 1 and not args.no_secondary:
-        # the metric's second half and the streaming driver, in the same run
+    if default and ctx.world == 1 and not args.no_secondary and not ctx.dry:
+        # the metric's second half, the MSA config and the streaming driver, in the same run
         sec = {}
         sec["D"] = bench_aligner(ctx, "D", max(1, args.secondary_steps), 1, args, not args.no_cpu)
-        sec["E"] = bench_stream(ctx, "E", args.steps, min(args.warmup, 1), args, False)
+        sec["C"] = bench_poa(ctx, "C", max(1, args.secondary_c_steps), 1, args, not args.no_cpu)
+        sec["E"] = bench_stream(ctx, "E", args.steps, min(args.warmup, 1), args, not args.no_cpu)
         if line is not None:
             line["secondary"] = sec
     if ctx.rank == 0 and line is not None:

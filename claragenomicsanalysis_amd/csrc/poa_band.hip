@@ -1344,6 +1344,11 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
                 if (nw > 1)
                     __syncthreads(); // pass done
                 end_row = uniform(band_ad_end_row(adsh, nw));
+                if (uniform(__hip_atomic_load(&adsh->stalled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+                {
+                    status = kGenericError; // a progress wait ran out: the scores are not trustworthy
+                    break;
+                }
             }
             else
                 end_row = band_forward<ScoreT, SizeT, CPL>(g, X, V, (GWAMD_LDS const uint8_t*)(lread), L, B, sc, ring,

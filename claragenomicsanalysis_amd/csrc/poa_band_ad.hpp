@@ -64,6 +64,7 @@ struct AdShared
     int prog[kAdProg];        // (block & 0x7ff) << 20 | completed steps (kAdDone: complete)
     int best[kAdMaxWaves];    // per wave: greatest sink value in its blocks
     int end_row[kAdMaxWaves]; // per wave: first row with it
+    int stalled;              // a progress wait ran out (set by ad_wait, read by wave 0 after the pass)
 };
 
 // Per-block context shared by the step loops.
@@ -104,13 +105,19 @@ __device__ __forceinline__ void ad_wait(GWAMD_LDS AdShared* sh, int blk, uint32_
 {
     GWAMD_LDS int* p     = &sh->prog[blk % kAdProg];
     const uint32_t want  = min(need, kAdDone);
-    // bounded: a broken hand-over must not hang the device (outputs would be
-    // wrong, and the parity tests catch that)
-    for (int spin = 0; spin < (1 << 26); spin++)
+    // bounded: a broken hand-over must not hang the device; if the wait runs
+    // out the pass carries on with values that may not be final, so the flag
+    // turns the window into a generic_error instead of a silently wrong result
+    for (int spin = 0;; spin++)
     {
         const uint32_t v = uint32_t(uniform(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)));
         if ((v >> 20) == uint32_t(blk & 0x7ff) && (v & kAdDone) >= want)
             break;
+        if (spin == (1 << 26))
+        {
+            __hip_atomic_store(&sh->stalled, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            break;
+        }
         __builtin_amdgcn_s_sleep(1);
     }
     ad_compiler_fence();
@@ -356,6 +363,8 @@ __device__ __forceinline__ void band_ad_init(GWAMD_LDS ScoreT* ring, int rowsz, 
             ring[k] = ScoreT(minv);
     if (lane < kAdProg)
         sh->prog[lane] = -1;
+    if (lane == 0)
+        sh->stalled = 0;
     wave_sync();
 }
 

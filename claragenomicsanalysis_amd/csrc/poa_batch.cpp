@@ -13,6 +13,7 @@
 
 #include "gwamd_cudapoa.h"
 #include "host_common.hpp"
+#include "poa_batch_internal.hpp"
 #include "poa_common.hpp"
 
 #include <hip/hip_runtime.h>
@@ -329,9 +330,33 @@ public:
             GWAMD_HIP_CHECK(hipMemsetAsync(b.head, 0, sizeof(int32_t), stream_));
         gwamd::poa::Scores sc{gap_, mismatch_, match_};
         const bool msa = (output_mask_ & OutputType::msa) != 0;
+        if (ev_start_)
+            GWAMD_HIP_CHECK(hipEventRecord(ev_start_, stream_));
         GWAMD_HIP_CHECK(gwamd_internal_poa_launch(&b, &dims_, &sc, score_bits_, size_bits_, banded_ ? 1 : 0, msa ? 1 : 0,
                                          stream_));
+        if (ev_stop_)
+            GWAMD_HIP_CHECK(hipEventRecord(ev_stop_, stream_));
         generated_ = true;
+    }
+
+    // instrumentation for the multi-batch driver (poa_batch_internal.hpp)
+    void set_launch_events(hipEvent_t start, hipEvent_t stop)
+    {
+        ev_start_ = start;
+        ev_stop_  = stop;
+    }
+
+    int64_t last_launch_cells()
+    {
+        if (poa_count_ == 0 || !generated_)
+            return 0;
+        std::vector<int64_t> cells(static_cast<size_t>(poa_count_));
+        std::vector<int32_t> fn(static_cast<size_t>(poa_count_));
+        get_stats(cells.data(), fn.data());
+        int64_t s = 0;
+        for (int64_t c : cells)
+            s += c;
+        return s;
     }
 
     void synchronize()
@@ -523,6 +548,7 @@ public:
         return dims_.lds_kernel == 3 ? (dims_.band_ad ? 4 : 3) : (dims_.lds_kernel ? 2 : 1);
     }
     int32_t max_poas() const { return max_poas_; }
+    int32_t max_sequence_size() const { return bs_.max_sequence_size; }
     int32_t slots() const { return slots_; }
     int32_t resident_slots() const { return blocks_per_cu_; }
     void set_spoa_accurate(bool on) { dims_.spoa_accurate = on ? 1 : 0; }
@@ -948,6 +974,7 @@ private:
     size_t num_bases_   = 0;
     bool generated_     = false;
     int32_t bid_        = 0;
+    hipEvent_t ev_start_ = nullptr, ev_stop_ = nullptr; // set_launch_events (multi-batch driver)
     gwamd::poa::Dims dims_{};
     PinnedBuf h_order_; // workgroup -> window (plan_launch_order)
     gwamd::poa::Buffers bufs_{};
@@ -1085,6 +1112,18 @@ std::unique_ptr<Batch> create_batch(int32_t device_id, hipStream_t stream, size_
     return std::unique_ptr<Batch>(new PoaBatch(device_id, stream, max_mem, output_mask, batch_size, gap_score,
                                                mismatch_score, match_score, cuda_banded_alignment));
 }
+
+namespace detail
+{
+void set_launch_events(Batch* batch, hipEvent_t start, hipEvent_t stop)
+{
+    static_cast<PoaBatch*>(batch)->set_launch_events(start, stop);
+}
+
+int64_t last_launch_cells(Batch* batch) { return static_cast<PoaBatch*>(batch)->last_launch_cells(); }
+
+int32_t max_sequence_size(const Batch* batch) { return static_cast<const PoaBatch*>(batch)->max_sequence_size(); }
+} // namespace detail
 
 } // namespace cudapoa
 } // namespace genomeworks

@@ -12,6 +12,7 @@
 
 #include "gwamd_cudapoa.h"
 #include "host_common.hpp"
+#include "poa_batch_internal.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -99,24 +100,108 @@ void MultiBatch::process_batches()
         consensus_.assign(size_t(count), std::string());
         coverages_.assign(size_t(count), std::vector<uint16_t>());
     }
+    else
+    {
+        // a window that never reaches a batch (the threads stopped on an
+        // error) must not keep the caller's earlier status / length
+        for (int32_t w = 0; w < count; w++)
+        {
+            if (sink_.status)
+                sink_.status[w] = int32_t(StatusType::generic_error);
+            if (sink_.len)
+                sink_.len[w] = 0;
+        }
+    }
     status_.assign(size_t(count), StatusType::generic_error);
     rounds_   = 0;
     max_poas_ = 0;
+    skipped_  = 0;
+    launches_.clear();
 
     std::mutex mutex_windows;
     int32_t next_window_index = 0;
 
-    // multi_batch.hpp:79-115: reset, then add windows until the batch is full
+    // Launch timing (set_launch_timing): one start/stop event pair per batch
+    // and a reference event, so every launch becomes an interval on one clock.
+    const size_t nb = batches_.size();
+    std::vector<hipEvent_t> ev_start(nb, nullptr), ev_stop(nb, nullptr);
+    hipEvent_t ev_ref = nullptr;
+    struct EventGuard
+    {
+        std::vector<hipEvent_t>* a;
+        std::vector<hipEvent_t>* b;
+        hipEvent_t* r;
+        std::vector<std::unique_ptr<Batch>>* batches;
+        ~EventGuard()
+        {
+            for (auto& bt : *batches)
+                detail::set_launch_events(bt.get(), nullptr, nullptr);
+            for (auto* v : {a, b})
+                for (hipEvent_t e : *v)
+                    if (e)
+                        (void)hipEventDestroy(e);
+            if (*r)
+                (void)hipEventDestroy(*r);
+        }
+    } guard_events{&ev_start, &ev_stop, &ev_ref, &batches_};
+    if (time_launches_)
+    {
+        ScopedDevice dev(device_id_);
+        for (size_t b = 0; b < nb; b++)
+        {
+            GWAMD_HIP_CHECK(hipEventCreate(&ev_start[b]));
+            GWAMD_HIP_CHECK(hipEventCreate(&ev_stop[b]));
+            detail::set_launch_events(batches_[b].get(), ev_start[b], ev_stop[b]);
+        }
+        GWAMD_HIP_CHECK(hipEventCreate(&ev_ref));
+        GWAMD_HIP_CHECK(hipEventRecord(ev_ref, static_cast<hipStream_t>(streams_[0])));
+        GWAMD_HIP_CHECK(hipEventSynchronize(ev_ref));
+    }
+    std::mutex mutex_launches;
+
+    // multi_batch.hpp:79-115: reset, then add windows until the batch is full.
+    // A window that does not fit an empty batch (a read longer than the
+    // batch's max_sequence_size, too many reads) would stop every thread in
+    // the reference, leaving the rest of the windows unprocessed; here it
+    // gets its add_poa_group status and the batch moves past it.
     auto fill_next_batch = [&](Batch* batch) -> std::pair<int32_t, int32_t> {
         batch->reset();
         std::lock_guard<std::mutex> guard(mutex_windows);
-        const int32_t initial = next_window_index;
+        int32_t initial = next_window_index;
         std::vector<StatusType> s;
         while (next_window_index < count)
         {
-            if (batch->add_poa_group(s, groups_[size_t(next_window_index)]) != StatusType::success)
+            const StatusType st = batch->add_poa_group(s, groups_[size_t(next_window_index)]);
+            if (st == StatusType::success)
+            {
+                next_window_index++;
+                continue;
+            }
+            if (batch->get_total_poas() > 0)
                 break;
-            next_window_index++;
+            // nothing fits an empty batch: this window cannot be processed
+            StatusType why = st;
+            for (const StatusType e : s)
+                if (e != StatusType::success)
+                {
+                    why = e;
+                    break;
+                }
+            if (why == StatusType::exceeded_maximum_poas)
+            {
+                int32_t longest = 0;
+                for (const auto& e : groups_[size_t(next_window_index)])
+                    longest = std::max(longest, e.length);
+                if (longest > detail::max_sequence_size(batch))
+                    why = StatusType::exceeded_maximum_sequence_size;
+            }
+            const size_t w = size_t(next_window_index);
+            status_[w]     = why;
+            if (use_sink_ && sink_.status)
+                sink_.status[w] = int32_t(why);
+            skipped_++;
+            batch->reset();
+            initial = ++next_window_index;
         }
         if (next_window_index > initial)
         {
@@ -127,7 +212,8 @@ void MultiBatch::process_batches()
     };
 
     // multi_batch.hpp:118-155
-    auto process_batch = [&](Batch* batch) {
+    auto process_batch = [&](size_t b) {
+        Batch* batch = batches_[b].get();
         std::vector<std::string> cons;
         std::vector<std::vector<uint16_t>> cov;
         std::vector<StatusType> st;
@@ -144,6 +230,17 @@ void MultiBatch::process_batches()
             const int32_t n = range.second - range.first;
             if (int32_t(cons.size()) != n || int32_t(cov.size()) != n)
                 throw std::runtime_error("Consensus processed doesn't match range of windows passed to batch");
+            if (time_launches_)
+            {
+                LaunchRecord rec;
+                GWAMD_HIP_CHECK(hipEventElapsedTime(&rec.start_ms, ev_ref, ev_start[b]));
+                GWAMD_HIP_CHECK(hipEventElapsedTime(&rec.stop_ms, ev_ref, ev_stop[b]));
+                rec.cells   = detail::last_launch_cells(batch);
+                rec.windows = n;
+                rec.batch   = int32_t(b);
+                std::lock_guard<std::mutex> g(mutex_launches);
+                launches_.push_back(rec);
+            }
             for (int32_t i = 0; i < n; i++)
             {
                 const size_t w = size_t(range.first + i);
@@ -178,7 +275,7 @@ void MultiBatch::process_batches()
             try
             {
                 ScopedDevice dev(device_id_);
-                process_batch(batches_[b].get());
+                process_batch(b);
             }
             catch (...)
             {
@@ -194,6 +291,8 @@ void MultiBatch::process_batches()
     for (auto& e : errors)
         if (e)
             std::rethrow_exception(e);
+    std::sort(launches_.begin(), launches_.end(),
+              [](const LaunchRecord& a, const LaunchRecord& b) { return a.start_ms < b.start_ms; });
 }
 
 // multi_batch.hpp:176-207
@@ -337,6 +436,36 @@ int32_t gwamd_poa_multibatch_info(const gwamd_poa_multibatch* mb, int32_t* num_b
     *rounds             = mb->impl->rounds();
     return 0;
 }
+
+int32_t gwamd_poa_multibatch_set_launch_timing(gwamd_poa_multibatch* mb, int32_t on)
+{
+    const int32_t was = mb->impl->launch_timing() ? 1 : 0;
+    mb->impl->set_launch_timing(on != 0);
+    return was;
+}
+
+int32_t gwamd_poa_multibatch_launches(const gwamd_poa_multibatch* mb, float* start_ms, float* stop_ms, int64_t* cells,
+                                      int32_t* windows, int32_t* batch, int32_t capacity)
+{
+    const auto& l = mb->impl->launches();
+    const int32_t n = int32_t(l.size());
+    for (int32_t i = 0; i < std::min(n, capacity); i++)
+    {
+        if (start_ms)
+            start_ms[i] = l[size_t(i)].start_ms;
+        if (stop_ms)
+            stop_ms[i] = l[size_t(i)].stop_ms;
+        if (cells)
+            cells[i] = l[size_t(i)].cells;
+        if (windows)
+            windows[i] = l[size_t(i)].windows;
+        if (batch)
+            batch[i] = l[size_t(i)].batch;
+    }
+    return n;
+}
+
+int32_t gwamd_poa_multibatch_skipped(const gwamd_poa_multibatch* mb) { return mb->impl->skipped_windows(); }
 
 int32_t gwamd_poa_multibatch_run_file(const char* filename, int32_t num_batches, int32_t total_windows,
                                       char* assembly, int64_t capacity, int64_t* length)

@@ -364,12 +364,20 @@ class CudaPoaMultiBatch:
         read_lens = np.ascontiguousarray(read_lens, dtype=np.int32).ravel()
         rpw = np.asarray(reads_per_window, dtype=np.int64).ravel()
         n = len(rpw)
+        if (rpw < 0).any() or (read_lens < 0).any():
+            raise ValueError("negative read count or read length")
         first = np.zeros(n + 1, np.int64)
         np.cumsum(rpw, out=first[1:])
+        if first[-1] != len(read_lens):
+            raise ValueError("reads_per_window sums to %d, but %d read lengths were given"
+                             % (int(first[-1]), len(read_lens)))
         off = np.zeros(len(read_lens), np.int64)
         if len(read_lens) > 1:
             np.cumsum(read_lens[:-1], out=off[1:])
-        bases = np.ascontiguousarray(bases, dtype=np.uint8)
+        bases = np.ascontiguousarray(bases, dtype=np.uint8).ravel()
+        if int(read_lens.sum(dtype=np.int64)) > len(bases):
+            raise ValueError("read lengths sum to %d bases, but only %d were given"
+                             % (int(read_lens.sum(dtype=np.int64)), len(bases)))
         if out is None:
             out = (np.zeros(n, np.int32), np.zeros(n, np.int32), np.zeros((n, self.stride), np.uint8),
                    np.zeros((n, self.stride), np.uint16))
@@ -390,6 +398,28 @@ class CudaPoaMultiBatch:
         cs = [cons[i, :ln[i]].tobytes().decode() for i in range(len(data))]
         cv = [cov[i, :ln[i]].tolist() for i in range(len(data))]
         return cs, cv, status.tolist()
+
+    def set_launch_timing(self, on=True):
+        """Record HIP events around every kernel launch of the next process calls
+        (bench.py config E roofline).  Returns the previous setting."""
+        return bool(self._lib.gwamd_poa_multibatch_set_launch_timing(self._handle, int(bool(on))))
+
+    def launches(self):
+        """Kernel launches of the last process (launch timing on), sorted by start:
+        dict of arrays start_ms, stop_ms (ms after the call began, one clock for
+        all streams), cells (DP cells), windows, batch."""
+        n = self._lib.gwamd_poa_multibatch_launches(self._handle, None, None, None, None, None, 0)
+        out = {"start_ms": np.zeros(n, np.float32), "stop_ms": np.zeros(n, np.float32),
+               "cells": np.zeros(n, np.int64), "windows": np.zeros(n, np.int32), "batch": np.zeros(n, np.int32)}
+        self._lib.gwamd_poa_multibatch_launches(self._handle, out["start_ms"].ctypes.data, out["stop_ms"].ctypes.data,
+                                                out["cells"].ctypes.data, out["windows"].ctypes.data,
+                                                out["batch"].ctypes.data, n)
+        return out
+
+    def skipped(self):
+        """Windows of the last process that fit no empty batch (they carry their
+        add_poa_group status, e.g. exceeded_maximum_sequence_size)."""
+        return int(self._lib.gwamd_poa_multibatch_skipped(self._handle))
 
     def info(self):
         """(batches, the most windows one batch took, generate_poa calls) of the last process."""
@@ -424,6 +454,12 @@ def _declare_multibatch(L):
     L.gwamd_poa_multibatch_process.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, i32]
     L.gwamd_poa_multibatch_info.restype = i32
     L.gwamd_poa_multibatch_info.argtypes = [vp, P(i32), P(i32), P(i32)]
+    L.gwamd_poa_multibatch_set_launch_timing.restype = i32
+    L.gwamd_poa_multibatch_set_launch_timing.argtypes = [vp, i32]
+    L.gwamd_poa_multibatch_launches.restype = i32
+    L.gwamd_poa_multibatch_launches.argtypes = [vp, vp, vp, vp, vp, vp, i32]
+    L.gwamd_poa_multibatch_skipped.restype = i32
+    L.gwamd_poa_multibatch_skipped.argtypes = [vp]
     L.gwamd_poa_multibatch_run_file.restype = i32
     L.gwamd_poa_multibatch_run_file.argtypes = [C.c_char_p, i32, i32, vp, i64, P(i64)]
     L._mb_declared = True

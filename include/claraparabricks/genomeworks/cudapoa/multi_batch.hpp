@@ -82,6 +82,24 @@ public:
     int32_t max_poas_per_batch() const { return max_poas_; }
     /// generate_poa calls of the last process_batches (all batches together).
     int32_t rounds() const { return rounds_; }
+    /// Windows of the last process_batches that fit no empty batch (they keep
+    /// the add_poa_group status; the reference stops every thread there).
+    int32_t skipped_windows() const { return skipped_; }
+
+    /// Kernel launch records of the last process_batches when launch timing is
+    /// on: start / stop of each batch's kernel in ms after the call began (HIP
+    /// events on the batch's stream), the DP cells and the windows it ran.
+    struct LaunchRecord
+    {
+        float start_ms  = 0.f;
+        float stop_ms   = 0.f;
+        int64_t cells   = 0;
+        int32_t windows = 0;
+        int32_t batch   = 0;
+    };
+    void set_launch_timing(bool on) { time_launches_ = on; }
+    bool launch_timing() const { return time_launches_; }
+    const std::vector<LaunchRecord>& launches() const { return launches_; }
 
 private:
     void create(int32_t num_batches, int32_t device_id, size_t mem_per_batch, int8_t output_mask,
@@ -100,6 +118,9 @@ private:
     bool use_sink_   = false;
     int32_t max_poas_ = 0;
     int32_t rounds_   = 0;
+    int32_t skipped_  = 0;
+    bool time_launches_ = false;
+    std::vector<LaunchRecord> launches_;
 };
 
 } // namespace cudapoa

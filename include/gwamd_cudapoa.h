@@ -179,6 +179,18 @@ int32_t gwamd_poa_multibatch_process(gwamd_poa_multibatch* mb, const char* bases
 /* Batches, the most windows one batch took, generate_poa calls of the last process. */
 int32_t gwamd_poa_multibatch_info(const gwamd_poa_multibatch* mb, int32_t* num_batches, int32_t* max_poas_per_batch,
                                   int32_t* rounds);
+/* Extra (no reference counterpart; bench.py config E roofline): when on,
+ * process records HIP events around every kernel launch.  Returns the previous
+ * setting. */
+int32_t gwamd_poa_multibatch_set_launch_timing(gwamd_poa_multibatch* mb, int32_t on);
+/* Launch records of the last process (sorted by start): kernel start / stop in
+ * ms after the call began, DP cells, windows, batch index.  Fills at most
+ * capacity entries (NULL arrays skipped); returns the number of launches. */
+int32_t gwamd_poa_multibatch_launches(const gwamd_poa_multibatch* mb, float* start_ms, float* stop_ms, int64_t* cells,
+                                      int32_t* windows, int32_t* batch, int32_t capacity);
+/* Windows of the last process that fit no empty batch (status = the
+ * add_poa_group status, e.g. exceeded_maximum_sequence_size). */
+int32_t gwamd_poa_multibatch_skipped(const gwamd_poa_multibatch* mb);
 /* The reference's end-to-end flow: MultiBatch(num_batches, filename,
  * total_windows), process_batches(), assembly().  Writes up to capacity bytes
  * of the assembly and its full length to *length. */

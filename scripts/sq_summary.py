@@ -9,6 +9,7 @@ count quad-cycles).  Derived:
   wait_frac        = SQ_WAIT_ANY / SQ_WAVE_CYCLES       (parked at s_waitcnt / barrier)
   active_valu_frac = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES
   salu_per_valu    = SQ_INSTS_SALU / SQ_INSTS_VALU
+  sq_busy_frac     = SQ_BUSY_CYCLES / (kernel ns x 2.4 GHz x 32 SQs)  (cycles, summed over the 32 SEs)
 Usage: python scripts/sq_summary.py <pmc dir> <profile name> <config key> <kernel substring> <kernel avg ns>
 """
 import csv
@@ -20,6 +21,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLOCK_GHZ = 2.4
 SIMDS = 1024
+SQ_INSTANCES = 32  # one SQ per shader engine (MI355X_MICROARCH.md: 32 SEs); SQ_BUSY_CYCLES sums them
 
 
 def main(src, name, config, kernel, avg_ns):
@@ -47,7 +49,7 @@ def main(src, name, config, kernel, avg_ns):
     if g("SQ_INSTS_SALU") and g("SQ_INSTS_VALU"):
         out["salu_per_valu"] = round(g("SQ_INSTS_SALU") / g("SQ_INSTS_VALU"), 3)
     if g("SQ_BUSY_CYCLES") and avg_ns:
-        out["sq_busy_frac"] = round(g("SQ_BUSY_CYCLES") / (avg_ns * CLOCK_GHZ), 4)
+        out["sq_busy_frac"] = round(g("SQ_BUSY_CYCLES") / (avg_ns * CLOCK_GHZ * SQ_INSTANCES), 4)
     out["note"] = ("rocprofv3 --pmc, one pass per counter group (scripts/pmc_sq.sh); SQ_* summed over the "
                    "dispatch; quad-cycle units for *_CYCLES / WAIT / ACTIVE; valu_issue_util assumes 2 cycles "
                    "per wave64 VALU instruction at %.1f GHz on %d SIMDs" % (CLOCK_GHZ, SIMDS))

@@ -421,10 +421,17 @@ def test_serialize_graph_case(banded):
 # scratch; GWAMD_LAUNCH_ORDER_CUS plans the snake order for a 2-CU device, so
 # batches far smaller than the real CU count run reordered.  Every output stays
 # bit-exact per window, and a second generate (dequeue counter reset) repeats it.
-@pytest.mark.parametrize("mode", ["full", "full_msa", "banded", "banded_msa", "v1", "full_spoa"])
+@pytest.mark.parametrize("mode", ["full", "full_msa", "banded", "banded_msa", "banded_ad", "banded_ad_msa", "v1",
+                                  "full_spoa"])
 @pytest.mark.parametrize("grid", ["slots3", "cus2", "slots5_cus2"])
 def test_persistent_grid_and_launch_order(mode, grid, monkeypatch):
     monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    # banded_ad: the anti-diagonal forward pass (helper waves, progress words,
+    # ring) on a persistent grid whose workgroups reuse their slot across windows
+    if "_ad" in mode:
+        monkeypatch.setenv("GWAMD_BAND_FWD", "ad")
+    else:
+        monkeypatch.delenv("GWAMD_BAND_FWD", raising=False)
     if "slots" in grid:
         monkeypatch.setenv("GWAMD_POA_SLOTS", grid.split("_")[0][5:])
     else:
@@ -449,6 +456,8 @@ def test_persistent_grid_and_launch_order(mode, grid, monkeypatch):
     slots, resident = b.get_grid()
     if mode == "v1":
         assert resident == 0 and b.kernel_variant() == 1
+    elif "_ad" in mode:
+        assert b.kernel_variant() == 4
     else:
         assert b.kernel_variant() in ((3, 4) if banded else (2,))
         if "slots" in grid:

@@ -67,6 +67,51 @@ def test_multibatch_config_b_shape_sample():
         assert rcov[j] == cov[i, :clen[i]].tolist(), i
 
 
+def test_multibatch_overlong_window_is_skipped_not_stale():
+    # a window whose read exceeds max_sequence_size fits no empty batch; the
+    # reference's loop stops every thread there.  Here the window gets
+    # exceeded_maximum_sequence_size, the rest are processed, and output
+    # arrays reused from an earlier call never keep stale rows.
+    wins = synth.poa_windows(4001, 30, 150, 6, 6, 6, 6)
+    wins.insert(11, [b"ACGT" * 100, b"ACGT" * 99])  # 400 > 300
+    mb = CudaPoaMultiBatch(8, 300, num_batches=2, mem_per_batch=mem_for(300, 8, 7))
+    flat = [r for w in wins for r in w]
+    bases = np.frombuffer(b"".join(flat), np.uint8)
+    lens = np.array([len(r) for r in flat], np.int32)
+    rpw = [len(w) for w in wins]
+    n = len(wins)
+    stale = (np.full(n, 0, np.int32), np.full(n, 77, np.int32), np.full((n, mb.stride), 65, np.uint8),
+             np.full((n, mb.stride), 9, np.uint16))
+    mb.set_launch_timing(True)
+    status, clen, cons, cov = mb.process_packed(bases, lens, rpw, out=stale)
+    assert mb.skipped() == 1
+    assert status[11] == 2 and clen[11] == 0  # exceeded_maximum_sequence_size
+    rest = [w for i, w in enumerate(wins) if i != 11]
+    rc, rst, rcov, _, _ = oracle.poa_batch(rest, max_nodes=900, max_consensus=600, max_seqs=8, coverage=True)
+    j = 0
+    for i in range(n):
+        if i == 11:
+            continue
+        assert status[i] == rst[j] and cons[i, :clen[i]].tobytes().decode() == rc[j], i
+        assert cov[i, :clen[i]].tolist() == rcov[j], i
+        j += 1
+    # launch records: every processed window is in exactly one launch, on one clock
+    L = mb.launches()
+    assert int(L["windows"].sum()) == n - 1
+    assert (L["stop_ms"] >= L["start_ms"]).all() and (L["cells"] > 0).all()
+    assert set(L["batch"].tolist()) <= {0, 1}
+
+
+def test_multibatch_rejects_inconsistent_inputs():
+    mb = CudaPoaMultiBatch(4, 100, num_batches=1, mem_per_batch=mem_for(100, 4, 4))
+    with pytest.raises(ValueError):
+        mb.process_packed(np.zeros(10, np.uint8), np.array([5, 5], np.int32), [3])
+    with pytest.raises(ValueError):
+        mb.process_packed(np.zeros(9, np.uint8), np.array([5, 5], np.int32), [2])
+    with pytest.raises(ValueError):
+        mb.process_packed(np.zeros(10, np.uint8), np.array([5, 5], np.int32), [-1, 3])
+
+
 @pytest.mark.skipif(not os.environ.get("GWAMD_SAMPLE_WINDOWS"),
                     reason="cudapoa/data/sample-windows.txt is not in the reference snapshot "
                            "(.MISSING_LARGE_BLOBS); set GWAMD_SAMPLE_WINDOWS to a copy to run")
