@@ -952,9 +952,15 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
     GWAMD_LDS uint8_t* tgt  = base + a.lds_target_off;
     GWAMD_LDS uint32_t* pat = (GWAMD_LDS uint32_t*)(base + a.lds_pat_off);
     uint8_t* ws             = a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes);
+#ifdef GWAMD_ALN_PROFILE
+    // [0] forward (score matrix) cycles, [1] backtrace cycles, [3] total,
+    // [4] column-blocks, [5] backtrace steps
+    uint64_t pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
 
     for (int idx = blockIdx.x; idx < a.n; idx += gridDim.x)
     {
+        GWAMD_PROF_T0(t_all);
         const char* q  = a.seqs + size_t(2 * idx) * a.stride;
         const char* tg = a.seqs + size_t(2 * idx + 1) * a.stride;
         const int Q    = uni(a.lens[2 * idx]);
@@ -968,6 +974,7 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
         uint32_t* wpv = reinterpret_cast<uint32_t*>(ws);
         uint32_t* wmv = wpv + size_t(nw) * (T + 1);
         int32_t* wsc  = reinterpret_cast<int32_t*>(wmv + size_t(nw) * (T + 1));
+        GWAMD_PROF_T0(t_fwd);
         if (Q > 0)
         {
             const int nch           = uni((nw + kWave - 1) / kWave);
@@ -1031,6 +1038,11 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
         }
         __threadfence_block();
         wave_sync();
+        GWAMD_PROF_ADD(pr[0], t_fwd);
+#ifdef GWAMD_ALN_PROFILE
+        pr[4] += uint64_t(T) * uint64_t((nw + kWave - 1) / kWave);
+#endif
+        GWAMD_PROF_T0(t_bt);
         // backtrace (myers_backtrace, myers_gpu.cu:181-245)
         const uint32_t last_mask = (Q % kWordBits) != 0 ? (1u << (Q % kWordBits)) - 1u : ~0u;
         auto gms                 = [&](int i, int j) -> int {
@@ -1081,10 +1093,20 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
         for (int k = lane; k < j; k += kWave)
             path[pos + k] = kInsertion;
         pos += j;
+        GWAMD_PROF_ADD(pr[1], t_bt);
+#ifdef GWAMD_ALN_PROFILE
+        pr[5] += uint64_t(pos);
+#endif
         if (lane == 0)
             a.path_len[idx] = pos;
         wave_sync();
+        GWAMD_PROF_ADD(pr[3], t_all);
     }
+#ifdef GWAMD_ALN_PROFILE
+    if (lane == 0)
+        for (int k = 0; k < 8; k++)
+            atomicAdd(&gwamd_aln_prof[k], (unsigned long long)pr[k]);
+#endif
 }
 
 } // namespace aln
