@@ -47,6 +47,14 @@ ALIGNER_CONFIGS = {
     # the reference's other global aligners on the same pairs (secondary rows)
     "D_banded": dict(pairs=100000, length=5000, algorithm="myers_banded"),
     "D_ukkonen": dict(pairs=100000, length=5000, algorithm="ukkonen"),
+    # BM_SingleAlignment at its largest size (cudaaligner/benchmarks/main.cpp:33-60,
+    # 135-138): one pair, query = generate_random_genome(100000, minstd_rand(1)),
+    # target = generate_random_sequence(query, 100000/30 x 3), default aligner
+    "D_100k": dict(pairs=1, length=100000, algorithm="hirschberg_myers", recipe="BM_SingleAlignment"),
+    # BM_SingleBatchAlignment<AlignerGlobalMyers / MyersBanded> at 65,536 bp
+    # (main.cpp:85-124, 140-158): per-pair seeds here, target truncated to 65,536
+    "D_myers_64k": dict(pairs=32, length=65536, algorithm="myers", recipe="BM_SingleBatchAlignment"),
+    "D_banded_64k": dict(pairs=32, length=65536, algorithm="myers_banded", recipe="BM_SingleBatchAlignment"),
 }
 
 # per algorithm: oracle id, dominant kernel
@@ -67,6 +75,18 @@ CONFIGS = {
 }
 # the config-B generator, seeds 1..1e6, 125k per GPU
 STREAM_CONFIGS = {"E": dict(CONFIGS["B"], windows_per_step=E_STEP_WINDOWS)}
+
+
+def golden_long(recipe, size, algorithm):
+    """The tests/golden/aligner_long.json case of a reference benchmark pair, if any."""
+    try:
+        gl = json.load(open(os.path.join(ROOT, "tests", "golden", "aligner_long.json")))
+    except (OSError, ValueError):
+        return None
+    for c in gl["cases"]:
+        if c["recipe"] == recipe and c["size"] == size and c["algorithm"] == algorithm:
+            return c
+    return None
 
 
 def aligner_alg_bytes(algorithm, q, t):
@@ -259,10 +279,20 @@ def bench_aligner(ctx, key, steps, warmup, args, with_cpu):
 
     n, L = cfg["pairs"], cfg["length"]
     t0 = time.time()
-    qs, ts = synth.pairs(1 + ctx.rank * n, n, L, L, 166, 166, 166)
+    recipe = cfg.get("recipe")
+    if recipe:
+        # the reference benchmark's pair: query = the random genome, target =
+        # its 10 %-difference copy (L/30 substitutions, insertions, deletions)
+        e = L // 30
+        muts, genomes = synth.pairs(1 + ctx.rank * n, n, L, L if recipe == "BM_SingleBatchAlignment" else L + e + 1,
+                                    e, e, e)
+        qs, ts = genomes, muts
+    else:
+        qs, ts = synth.pairs(1 + ctx.rank * n, n, L, L, 166, 166, 166)
     gen_s = time.time() - t0
     stream = torch.cuda.Stream()
-    b = CudaAlignerBatch(L, L, n, stream=stream, algorithm=cfg["algorithm"])
+    mq, mt = max(len(q) for q in qs), max(len(t) for t in ts)
+    b = CudaAlignerBatch(mq, mt, n, stream=stream, algorithm=cfg["algorithm"])
     for q, t in zip(qs, ts):
         if b.add_alignment(q, t) != 0:
             raise RuntimeError("add_alignment failed")
@@ -292,10 +322,20 @@ def bench_aligner(ctx, key, steps, warmup, args, with_cpu):
     from oracle import oracle
     cells = sum(len(q) * len(t) for q, t in zip(qs, ts))
     alg_bytes = sum(aligner_alg_bytes(cfg["algorithm"], q, t) for q, t in zip(qs, ts))
-    k = min(8, n)
+    k = min(8 if L <= 20000 else 1, n)
     algo = ALIGNER_ALGOS[cfg["algorithm"]][0]
-    ok = all(paths[i, :plen[i]][::-1].tolist() == oracle.align(qs[i], ts[i], algo, L) for i in range(k))
-    parity = {"pairs_checked": k, "bit_exact_vs_oracle": bool(ok)}
+    gold = golden_long(recipe, L, cfg["algorithm"]) if recipe else None
+    if gold is not None:
+        # the first pair against tests/golden/aligner_long.json (oracle output,
+        # make_aligner_long.py): a 100 kb oracle run takes ~40 s
+        import hashlib
+        p0 = paths[0, :plen[0]][::-1].tobytes()
+        ok = int(plen[0]) == gold["path_length"] and hashlib.sha256(p0).hexdigest() == gold["path_sha256"]
+        parity = {"pairs_checked": 1, "bit_exact_vs_oracle": bool(ok),
+                  "pinned_by": "tests/golden/aligner_long.json: " + gold["name"]}
+    else:
+        ok = all(paths[i, :plen[i]][::-1].tolist() == oracle.align(qs[i], ts[i], algo, mq) for i in range(k))
+        parity = {"pairs_checked": k, "bit_exact_vs_oracle": bool(ok)}
     # size-independent check over every pair: a global alignment consumes the
     # whole query (match/mismatch + deletion) and the whole target (match/
     # mismatch + insertion; cudaaligner.hpp:46-52)
@@ -319,9 +359,9 @@ def bench_aligner(ctx, key, steps, warmup, args, with_cpu):
     cpu = None
     if with_cpu and ctx.world == 1:
         th = cpu_threads()
-        ns = args.cpu_sample or min(n, max(th * 12, 64))
+        ns = args.cpu_sample or min(n, max(th * 12, 64) if L <= 20000 else th)
         tc = time.perf_counter()
-        cres, used = oracle.align_batch(list(zip(qs[:ns], ts[:ns])), algo, L, th)
+        cres, used = oracle.align_batch(list(zip(qs[:ns], ts[:ns])), algo, mq, th)
         cpu_s = time.perf_counter() - tc
         match = all(cres[i] == paths[i, :plen[i]][::-1].tolist() for i in range(ns))
         cpu = dict({"value": round(ns / cpu_s, 3), "unit": "alignments/s", "kind": "port",
@@ -339,8 +379,8 @@ def bench_aligner(ctx, key, steps, warmup, args, with_cpu):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "int16" if cfg["algorithm"] == "ukkonen" else "u32 bit-vectors",
         "data": "synthetic (reference genomeutils generators, seeds 1..N)",
-        "config": {"workload": "cudaaligner global, %d pairs/GPU x %d bp, ~10%% difference, %s"
-                               % (n, L, cfg["algorithm"]),
+        "config": {"workload": "cudaaligner global, %d pairs/GPU x %d bp, ~10%% difference, %s%s"
+                               % (n, L, cfg["algorithm"], (", %s recipe" % recipe) if recipe else ""),
                    "config_key": key, "step": "align_all() + sync_alignments() (aligner_global.cpp:131-191)",
                    "pairs_per_gpu": n, "length": L, "algorithm": cfg["algorithm"], "grid": grid,
                    "device_bytes": dev_bytes, "gcups": round(cells / (kernel_ms / 1e3) / 1e9, 3),

@@ -315,13 +315,18 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
             else
             {
                 // wider bands: chunk c (words 32c..32c+31) in lanes 0..31 in turn,
-                // its state in LDS between columns
+                // its state in LDS between columns; bands wider than the LDS
+                // region (long queries) read the previous column's state back
+                // from the band matrix in HBM, with a workgroup fence per column
+                const bool lds_state = nwb <= TLE;
                 for (int w = lane; w < nwb; w += kWave)
                 {
                     const BandEntry e0{~0u, 0u, min((w + 1) * kWordBits, bw), 0};
-                    lds_put(reg + w, e0);
+                    if (lds_state)
+                        lds_put(reg + w, e0);
                     E[w] = e0;
                 }
+                __threadfence_block();
                 wave_sync();
                 for (int t = 1; t <= T; t++)
                 {
@@ -334,7 +339,11 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                         const int w        = c * kChunkWords + lane;
                         const bool valid   = lane < kChunkWords && w < nwb;
                         const uint64_t act = ballot(valid);
-                        const BandEntry e  = lds_get(reg + (valid ? w : 0));
+                        BandEntry e;
+                        if (lds_state)
+                            e = lds_get(reg + (valid ? w : 0));
+                        else
+                            e = E[size_t(t - 1) * nwb + (valid ? w : 0)];
                         uint32_t pv = e.pv, mv = e.mv;
                         int sc            = e.sc;
                         const uint32_t eq = band_pattern(patL, pw_stride, nwq, off, w, code);
@@ -356,7 +365,8 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                             {
                                 // word 31 takes bit 0 of the next chunk's first word,
                                 // still the previous column's (:567-573)
-                                const BandEntry nx = lds_get(reg + (c + 1) * kChunkWords);
+                                const BandEntry nx = lds_state ? lds_get(reg + (c + 1) * kChunkWords)
+                                                               : E[size_t(t - 1) * nwb + (c + 1) * kChunkWords];
                                 if (lane == kChunkWords - 1)
                                 {
                                     p2 |= (nx.pv & 1u) << 31;
@@ -382,13 +392,21 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                         if (valid)
                         {
                             const BandEntry o{pv, mv, sc, 0};
-                            lds_put(reg + w, o);
+                            if (lds_state)
+                                lds_put(reg + w, o);
                             E[size_t(t) * nwb + w] = o;
                         }
                     }
+                    if (!lds_state)
+                    {
+                        // this column's entries before the next column reads them
+                        __threadfence_block();
+                        wave_sync();
+                    }
                 }
+                __threadfence_block();
                 wave_sync();
-                ed = uni(lds_get(reg + lastw).sc);
+                ed = lds_state ? uni(lds_get(reg + lastw).sc) : uni(E[size_t(T) * nwb + lastw].sc);
             }
             if (ed <= est || bw == Q)
                 break;

@@ -25,15 +25,40 @@ namespace gwamd
 {
 namespace host
 {
+// long mode: target letter codes in LDS up to kHmLdsTarget bases, in HBM beyond
+constexpr int32_t kHmMaxQuery  = 1 << 24;
+constexpr int32_t kHmMaxTarget = 1 << 24;
+constexpr int32_t kHmLdsTarget = 131072;
+// full Myers: one pair's (word, column) state (0.375 B per cell) per slot
+constexpr int64_t kMyersMaxSlot   = int64_t(32) << 30;
+constexpr int64_t kMyersWorkspace = int64_t(48) << 30; // resident slots within 48 GiB of the 288 GB HBM
+// Hirschberg-Myers takes the LDS-resident kernel (hm_kernel<false>, patterns in
+// LDS, register-resident sweeps of up to 4 blocks per half) up to these sizes
+constexpr int32_t kHmShortQuery  = 16384;
+constexpr int32_t kHmShortTarget = 65535;
 // Length limits of this implementation (include/gwamd_cudaaligner.h).
 inline void aligner_max_lengths(int32_t algo, int32_t& max_query, int32_t& max_target)
 {
     max_target = 65535; // 16-bit segment coordinates, LDS target codes
     switch (algo)
     {
-    case GWAMD_ALIGNER_HIRSCHBERG_MYERS: max_query = 16384; break; // register-resident Myers blocks
-    case GWAMD_ALIGNER_MYERS: max_query = 8192; break;
-    case GWAMD_ALIGNER_MYERS_BANDED: max_query = gwamd::aln::kBandChunks * gwamd::aln::kChunkWords * 32; break;
+    case GWAMD_ALIGNER_HIRSCHBERG_MYERS:
+        // long mode (hm_kernel<true>): query patterns in HBM, striped sweeps;
+        // the target's 2-bit letter codes stay in LDS
+        max_query  = kHmMaxQuery;
+        max_target = kHmMaxTarget;
+        break;
+    case GWAMD_ALIGNER_MYERS:
+        // stripes of 8,192 rows; the (word, column) state of the largest pair
+        // must fit one workspace slot (kMyersMaxSlot)
+        max_query  = kHmMaxQuery;
+        max_target = kHmMaxTarget;
+        break;
+    case GWAMD_ALIGNER_MYERS_BANDED:
+        // patterns (Q / 2 bytes) and target codes (T / 4 bytes) in LDS
+        max_query  = 65536;
+        max_target = 65536;
+        break;
     default:
     {
         // Ukkonen: (1 + int(0.1f * T) + 2p + 1) / 2 band rows, at most kUkChunks * 64
@@ -435,7 +460,16 @@ private:
             lds_target_off_  = 0;
             lds_pat_off_     = int32_t(a16((max_t_ + 15) / 16 * 4 + 16));
             lds_tile_off_    = int32_t(lds_pat_off_ + a16(int64_t(pat_words) * 16 + 16));
-            tile_bytes_      = 4096; // 256 16-byte band entries: two columns of 128 words, or 256 chunk words
+            // at least 256 16-byte band entries (two columns of 128 words, or
+            // 256 chunk words); up to the whole band's chunk state while it
+            // fits 48 KiB of LDS (wider bands keep it in HBM)
+            tile_bytes_      = 4096;
+            int64_t want     = std::min<int64_t>(a16(int64_t(pat_words) * 16), int64_t(48) << 10);
+            want             = std::min<int64_t>(want, (65536 - lds_tile_off_) & ~int64_t(511));
+            if (const char* tb = std::getenv("GWAMD_BAND_TILE_BYTES")) // parity tests: HBM chunk state
+                want = std::atoi(tb);
+            if (want > tile_bytes_)
+                tile_bytes_ = int32_t(want);
             lds_bytes_       = lds_tile_off_ + tile_bytes_;
             // band entries (pv, mv, score, pad) of the widest band (the whole query)
             slot_bytes_ = a16(int64_t(pat_words) * (max_t_ + 1) * 16 + 64);
@@ -471,44 +505,75 @@ private:
             return;
         }
         const int pat_words = (max_q_ + kWordBits - 1) / kWordBits;
+        const bool hm       = algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS;
+        // long mode: patterns in HBM, target codes through a generic pointer;
+        // full Myers takes it past 8,192 x 65,535 (its stripes work either way)
+        long_mode_ = hm ? (max_q_ > gwamd::host::kHmShortQuery || max_t_ > gwamd::host::kHmShortTarget)
+                        : (max_q_ > 8192 || max_t_ > gwamd::host::kHmShortTarget);
+        // GWAMD_HM_STRIPE_BLOCKS=1..4 (parity tests): long mode at any size, with
+        // stripes of that many blocks, so short pairs take the striped sweeps
+        stripe_blocks_ = kMaxChunks;
+        if (const char* sb = std::getenv("GWAMD_HM_STRIPE_BLOCKS"))
+            if (hm && std::atoi(sb) >= 1 && std::atoi(sb) <= kMaxChunks)
+            {
+                stripe_blocks_ = std::atoi(sb);
+                long_mode_     = true;
+            }
+        const int sc_bytes  = long_mode_ ? 4 : 2; // split scores
         lds_target_off_     = 0;
-        // Hirschberg-Myers: target as 2-bit letter codes; full Myers: bytes
-        lds_pat_off_        = int32_t(algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS ? a16((max_t_ + 15) / 16 * 4 + 16)
-                                                                              : a16(max_t_ + 16));
-        lds_scratch_off_    = int32_t(lds_pat_off_ + a16(int64_t(pat_words) * 32 + 16));
+        // target as 2-bit letter codes (long mode: in HBM past kHmLdsTarget)
+        tcod_hbm_           = long_mode_ && max_t_ > gwamd::host::kHmLdsTarget;
+        lds_pat_off_        = int32_t(tcod_hbm_ ? 0 : a16((max_t_ + 15) / 16 * 4 + 16));
+        // long mode: the patterns live in the HBM slot
+        lds_scratch_off_    = int32_t(lds_pat_off_ + (long_mode_ ? 0 : a16(int64_t(pat_words) * 32 + 16)));
         scratch_bytes_      = 0;
-        if (algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS) // LDS base case + LDS split scores
-            scratch_bytes_ = int32_t(a16(int64_t(kLeafCols) * kLeafColBytes + 2 * kSplitLds * 2));
+        if (hm) // LDS split scores of segments up to kSplitLds columns
+            scratch_bytes_ = int32_t(a16(int64_t(2) * kSplitLds * sc_bytes));
         lds_stack_off_ = lds_scratch_off_ + scratch_bytes_;
-        lds_bytes_     = lds_stack_off_ + (algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS ? kStackSize * 16 : 0);
+        lds_bytes_     = lds_stack_off_ + (hm ? kStackSize * 16 : 0);
         if (lds_bytes_ > 65536)
             throw std::invalid_argument("aligner problem size does not fit in LDS");
         pat_words_ = pat_words;
         int per_cu = 1, cus = 1;
-        GWAMD_HIP_CHECK(gwamd_internal_align_occupancy(algo_, lds_bytes_, &per_cu));
+        GWAMD_HIP_CHECK(gwamd_internal_align_occupancy(algo_ + (long_mode_ ? 100 : 0), lds_bytes_, &per_cu));
         GWAMD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
         slots_ = std::max(1, per_cu * cus);
-        if (algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS)
+        if (hm)
         {
-            // base cases too wide for LDS, the split scores of wide segments
-            // and of packed ones, then the breadth-first frontier: at most
-            // 2 * (query + 1) segments (every leaf has a query row or is one
-            // of the target-only halves of a split)
+            // slot: split scores of wide segments (forward, reverse), the
+            // breadth-first frontier (two buffers of (qb, qe, tb, te) + one
+            // split column per entry; at most 2 * (query + 1) segments: every
+            // leaf has a query row or is one of the target-only halves of a
+            // split), per-lane base cases (columns of every segment: target +
+            // one per segment; (offset, length) per segment; paths), and in
+            // long mode the query patterns and the striped sweeps' deltas
+            split_off_  = 0;
             front_cap_  = 2 * (max_q_ + 2);
-            front_off_  = a16(a16(int64_t(stride_ + 1) * kLeafColBytes) + int64_t(stride_ + 1 + kWave) * 4 + 64);
-            // per-lane base cases: columns of every segment (target + one per
-            // segment), (offset, length) per segment, paths (query + target)
+            front_off_  = a16(int64_t(2) * (stride_ + 1 + kWave) * sc_bytes + 64);
             leaf_cols_  = max_t_ + front_cap_ + 2;
-            leaf_off_   = a16(front_off_ + int64_t(front_cap_) * (2 * 8 + 2) + 64);
-            slot_bytes_ = a16(leaf_off_ + int64_t(leaf_cols_) * kLeafColBytes + 16 + int64_t(front_cap_) * 8 +
+            leaf_off_   = a16(front_off_ + int64_t(front_cap_) * (2 * 16 + 4) + 64);
+            int64_t end = a16(leaf_off_ + int64_t(leaf_cols_) * kLeafColBytes + 16 + int64_t(front_cap_) * 8 +
                               max_q_ + max_t_ + 64);
+            pat_off_  = end;
+            hbuf_off_ = a16(pat_off_ + (long_mode_ ? int64_t(pat_words) * 32 + 64 : 0));
+            tcod_off_ = a16(hbuf_off_ + (long_mode_ ? int64_t(max_t_) + 1 + kWave + 64 : 0));
+            slot_bytes_ = a16(tcod_off_ + (tcod_hbm_ ? int64_t(max_t_ + 15) / 16 * 4 + 64 : 0));
+            const int64_t cap = int64_t(16) << 30; // resident slots within 16 GiB of the 288 GB HBM
+            slots_            = int32_t(std::max<int64_t>(1, std::min<int64_t>(slots_, cap / slot_bytes_)));
         }
         else
         {
-            // full matrix: pv, mv, score per (word, column)
-            slot_bytes_ = a16(int64_t(pat_words) * (max_t_ + 1) * 12 + 64);
-            const int64_t cap = int64_t(4) << 30; // keep the resident slots within 4 GiB
-            slots_            = int32_t(std::max<int64_t>(1, std::min<int64_t>(slots_, cap / slot_bytes_)));
+            // full matrix: pv, mv, score per (word, column), then the stripes'
+            // per-column deltas, and in long mode the patterns and target codes
+            hbuf_off_   = a16(int64_t(pat_words) * (max_t_ + 1) * 12 + 64);
+            pat_off_    = a16(hbuf_off_ + int64_t(max_t_) + 1 + kWave + 64);
+            tcod_off_   = a16(pat_off_ + (long_mode_ ? int64_t(pat_words) * 32 + 64 : 0));
+            slot_bytes_ = a16(tcod_off_ + (tcod_hbm_ ? int64_t(max_t_ + 15) / 16 * 4 + 64 : 0));
+            if (slot_bytes_ > gwamd::host::kMyersMaxSlot)
+                throw std::invalid_argument("max_query_length x max_target_length too large for the full Myers "
+                                            "aligner's score matrix (" + std::to_string(slot_bytes_) + " bytes)");
+            // resident slots within kMyersWorkspace (or a single slot)
+            slots_ = int32_t(std::max<int64_t>(1, std::min<int64_t>(slots_, gwamd::host::kMyersWorkspace / slot_bytes_)));
         }
         apply_grid_override();
         slots_ = std::min(slots_, max_n_);
@@ -532,6 +597,12 @@ private:
         a.front_cap        = front_cap_;
         a.ws_leaf_off      = leaf_off_;
         a.leaf_cols        = leaf_cols_;
+        a.ws_split_off     = split_off_;
+        a.ws_pat_off       = pat_off_;
+        a.ws_hbuf_off      = hbuf_off_;
+        a.ws_tcod_off      = tcod_hbm_ ? tcod_off_ : -1;
+        a.long_mode        = long_mode_ ? 1 : 0;
+        a.stripe_blocks    = stripe_blocks_;
         a.lds_target_off   = lds_target_off_;
         a.lds_pat_off      = lds_pat_off_;
         a.lds_scratch_off  = lds_scratch_off_;
@@ -557,6 +628,10 @@ private:
     int32_t front_cap_ = 0;
     int64_t leaf_off_  = 0;
     int32_t leaf_cols_ = 0;
+    int64_t split_off_ = 0, pat_off_ = 0, hbuf_off_ = 0, tcod_off_ = 0;
+    bool tcod_hbm_     = false;
+    bool long_mode_    = false;
+    int32_t stripe_blocks_ = gwamd::aln::kMaxChunks;
     int32_t lds_seq2_off_ = 0, lds_tile_off_ = 0, tile_bytes_ = 0;
     int32_t slots_ = 1;
     int64_t slot_bytes_ = 0, device_bytes_ = 0;

@@ -23,7 +23,6 @@ constexpr int kLeafCols   = 128; // base-case columns kept in LDS (larger leaves
 constexpr int kSplitLds   = 512; // split segments up to this many columns keep their scores in LDS
 constexpr int kLeafColBytes = 20; // per column: pv u64, mv u64, score i32
 constexpr int kChunkWords  = 32;  // banded Myers: one reference warp of 32 words per step (myers_gpu.cu:35)
-constexpr int kBandChunks  = 8;   // banded Myers: up to 8 chunks (8192 query rows)
 constexpr int kUkChunks    = 8;   // Ukkonen: band rows k held 64 per chunk, up to 512
 constexpr int kUkkonenP    = 100; // aligner_global_ukkonen.cpp:29
 constexpr int16_t kUkMax   = 32766; // numeric_limits<int16_t>::max() - 1 (ukkonen_gpu.cu:75)
@@ -55,6 +54,12 @@ struct Args
     int32_t front_cap;       //   entries per frontier buffer (two buffers, then one u16 split column each)
     int64_t ws_leaf_off;     //   per-lane base cases: columns (pv, mv, score) then paths
     int32_t leaf_cols;       //   column capacity (target + one per segment)
+    int64_t ws_split_off;    //   split scores of segments too wide for LDS (forward, reverse)
+    int64_t ws_pat_off;      //   long mode: query patterns
+    int64_t ws_hbuf_off;     //   long mode: striped sweeps' per-column hand-over deltas
+    int64_t ws_tcod_off;     //   long mode: target letter codes when they do not fit LDS (-1: in LDS)
+    int32_t long_mode;       // queries / targets past the LDS-resident limits (see aligner_batch.cpp)
+    int32_t stripe_blocks;   // long mode: 64-word blocks per stripe of a tall sweep (kMaxChunks)
     // LDS layout (bytes)
     int32_t lds_target_off;
     int32_t lds_pat_off;     // [pat_words][8] u32: forward A C T G, reverse A C T G

@@ -42,7 +42,9 @@ __device__ __forceinline__ int letter(int c) { return (c >> 1) & 3; }
 // Query pattern words of the whole query: pat[k*8 + L] (L = A C T G forward,
 // 4 + L reversed), bit i of word k set where query[32k+i] (resp.
 // query[Q-1-(32k+i)]) equals the letter (myers_preprocess, :210-225).
-__device__ void build_patterns(GWAMD_LDS uint32_t* pat, const char* q, int Q, int lane)
+// PatW: an LDS pointer, or a global one for queries whose patterns do not fit LDS.
+template <typename PatW>
+__device__ void build_patterns(PatW pat, const char* q, int Q, int lane)
 {
     const int nw = (Q + kWordBits - 1) / kWordBits;
     const char letters[4] = {'A', 'C', 'T', 'G'};
@@ -72,7 +74,8 @@ __device__ void build_patterns(GWAMD_LDS uint32_t* pat, const char* q, int Q, in
 
 // Segment pattern word w for letter L: rows start at query offset `off` of the
 // (forward or reversed) query (get_query_pattern, :246-268).
-__device__ __forceinline__ uint32_t seg_pattern(const GWAMD_LDS uint32_t* pat, int pat_words, int off, int w, int L)
+template <typename PatPtr>
+__device__ __forceinline__ uint32_t seg_pattern(PatPtr pat, int pat_words, int off, int w, int L)
 {
     const int k  = (off >> 5) + w;
     const int sh = off & 31;
@@ -86,8 +89,10 @@ __device__ __forceinline__ uint32_t seg_pattern(const GWAMD_LDS uint32_t* pat, i
     return r;
 }
 
-// Target letter codes (letter(), 2 bits each, 16 per word) in LDS.
-__device__ inline void pack_target(GWAMD_LDS uint32_t* tc, const char* t, int T, int lane)
+// Target letter codes (letter(), 2 bits each, 16 per word) in LDS (or, for
+// targets too long for it, in HBM).
+template <typename TcW>
+__device__ inline void pack_target(TcW tc, const char* t, int T, int lane)
 {
     for (int k = lane; k * 16 < T; k += kWave)
     {
@@ -99,7 +104,8 @@ __device__ inline void pack_target(GWAMD_LDS uint32_t* tc, const char* t, int T,
     }
 }
 
-__device__ __forceinline__ int code_at(const GWAMD_LDS uint32_t* tc, int idx)
+template <typename TcPtr>
+__device__ __forceinline__ int code_at(TcPtr tc, int idx)
 {
     return int((tc[idx >> 4] >> (2 * (idx & 15))) & 3u);
 }

@@ -22,6 +22,7 @@
 #include "aligner_device.hpp"
 
 #include <climits>
+#include <type_traits>
 
 #ifdef GWAMD_ALN_PROFILE
 // Diagnostic build only: cycle counters per phase of hm_kernel, summed over
@@ -197,11 +198,11 @@ struct HalfSweep
 {
     MyersBlock B[N];
     int lc, ll, hb, score;
-    __device__ void init(const GWAMD_LDS uint32_t* pat, int pat_words, int Q, int qb, int qe, bool rev, int lane)
+    // m rows starting at row `off` of the forward (rev: reversed) query
+    template <typename PatPtr>
+    __device__ void init_rows(PatPtr pat, int pat_words, int off, int m, bool rev, int lane)
     {
-        const int m      = qe - qb;
         const int nwords = (m + kWordBits - 1) / kWordBits;
-        const int off    = rev ? Q - qe : qb;
         const int pbase  = rev ? 4 : 0;
         const int lw     = nwords - 1;
         lc               = lw / kWave;
@@ -221,16 +222,26 @@ struct HalfSweep
             B[c].act = __builtin_amdgcn_ballot_w64(valid);
         }
     }
-    __device__ __forceinline__ void step(int code, int lane, uint32_t hisel, uint32_t lane0bit)
+    template <typename PatPtr>
+    __device__ void init(PatPtr pat, int pat_words, int Q, int qb, int qe, bool rev, int lane)
     {
-        int h = 1, hl = 0; // top row 0, 1, 2, ...: +1 into the first block
+        init_rows(pat, pat_words, rev ? Q - qe : qb, qe - qb, rev, lane);
+    }
+    // one column; hin enters the first row, returns the delta leaving the last
+    __device__ __forceinline__ int step_in(int code, int hin, int lane, uint32_t hisel, uint32_t lane0bit)
+    {
+        int h = hin, hl = 0;
 #pragma unroll
         for (int c = 0; c < N; c++)
         {
             h  = block_step_bf(B[c], code, h, c == lc, ll, hb, lane, hisel, lane0bit);
             hl = c == lc ? h : hl;
         }
-        score += hl;
+        return hl;
+    }
+    __device__ __forceinline__ void step(int code, int lane, uint32_t hisel, uint32_t lane0bit)
+    {
+        score += step_in(code, 1, lane, hisel, lane0bit); // top row 0, 1, 2, ...: +1 into the first block
     }
 };
 
@@ -239,9 +250,9 @@ struct HalfSweep
 // fw[t] = D(q[qb, qm), target[tb, tb + t)), rv[t] = D(q[qm, qe) reversed,
 // target[te - t, te) reversed), t = 0..Ts.  N: 64-word blocks of the larger
 // half.
-template <int N, typename Buf>
-__device__ void split_sweep(const GWAMD_LDS uint32_t* pat, int pat_words, int Q, int qb, int qm, int qe,
-                            const GWAMD_LDS uint32_t* tcod, int tb, int te, int lane, Buf fw, Buf rv)
+template <int N, typename PatPtr, typename TcPtr, typename Buf>
+__device__ void split_sweep(PatPtr pat, int pat_words, int Q, int qb, int qm, int qe,
+                            TcPtr tcod, int tb, int te, int lane, Buf fw, Buf rv)
 {
     const uint32_t hisel    = lane >= 32 ? 1u : 0u;
     const uint32_t lane0bit = lane == 0 ? 1u : 0u;
@@ -267,9 +278,62 @@ __device__ void split_sweep(const GWAMD_LDS uint32_t* pat, int pat_words, int Q,
         }
         if (lane < cnt)
         {
-            fw[t0 + lane] = uint16_t(bf);
-            rv[t0 + lane] = uint16_t(br);
+            fw[t0 + lane] = bf;
+            rv[t0 + lane] = br;
         }
+    }
+}
+
+// One half of a split too tall for one register-resident sweep (more than
+// kMaxChunks blocks, queries over 16,384 bases): stripes of kMaxChunks blocks
+// from the half's first row down; the horizontal delta leaving a stripe's last
+// row at every column reaches the next stripe through hbuf (one int8 per
+// column, written and read back by the same lane).  out[t] = D(m, t) of the
+// half (forward, or reversed rows and columns), t = 0..Ts: the same values as
+// one tall sweep, since the Myers column recurrence is exact.
+template <typename PatPtr, typename TcPtr, typename Buf>
+__device__ void half_sweep_striped(PatPtr pat, int pat_words, int Q, int qb, int qe, bool rev,
+                                   TcPtr tcod, int tb, int te, int lane, Buf out, int8_t* hbuf,
+                                   int stripe_blocks)
+{
+    const int m        = qe - qb;
+    const int off0     = rev ? Q - qe : qb;
+    const int rows_per = stripe_blocks * kWave * kWordBits; // stripe_blocks <= kMaxChunks
+    const int Ts       = te - tb;
+    const uint32_t hisel    = lane >= 32 ? 1u : 0u;
+    const uint32_t lane0bit = lane == 0 ? 1u : 0u;
+    for (int r0 = 0; r0 < m; r0 += rows_per)
+    {
+        const int ms     = min(rows_per, m - r0);
+        const bool first = r0 == 0;
+        const bool last  = r0 + ms == m;
+        HalfSweep<kMaxChunks> H;
+        H.init_rows(pat, pat_words, off0 + r0, ms, rev, lane);
+        int score = m; // D(m, 0); only the last stripe's deltas reach row m
+        for (int t0 = 0; t0 <= Ts; t0 += kWave)
+        {
+            const int tt  = t0 + lane;
+            const bool in = tt >= 1 && tt <= Ts;
+            const int cd  = in ? code_at(tcod, rev ? te - tt : tb + tt - 1) : 0;
+            const int hv  = (!first && in) ? int(hbuf[tt]) : 1; // first stripe: the top row's +1
+            const int cnt = min(kWave, Ts + 1 - t0);
+            int ho        = 0;
+            uint32_t bo   = uint32_t(score);
+            for (int x = t0 == 0 ? 1 : 0; x < cnt; x++)
+            {
+                const int h = H.step_in(uni(__builtin_amdgcn_readlane(cd, x)), uni(__builtin_amdgcn_readlane(hv, x)),
+                                        lane, hisel, lane0bit);
+                score += h;
+                ho = lane == x ? h : ho;
+                bo = lane == x ? uint32_t(score) : bo;
+            }
+            if (!last && in)
+                hbuf[tt] = int8_t(ho);
+            if (last && lane < cnt)
+                out[t0 + lane] = bo;
+        }
+        __threadfence_block();
+        wave_sync();
     }
 }
 
@@ -296,119 +360,9 @@ __device__ int split_argmin(Buf fw, Buf rv, int Ts, int lane)
     return uni(int(uint32_t(best)));
 }
 
-// ---------------------------------------------------------------------------
-// Full-Myers base case of a segment shorter than 63 rows (one 64-bit word,
-// wave-uniform): column state into `leaf` (LDS or HBM), then the backtrace
-// (hirschberg_myers_compute_path / append_myers_backtrace, :372-392, :100-160).
-template <typename LeafPtr64, typename LeafPtr32>
-__device__ int leaf_full_myers(const GWAMD_LDS uint32_t* pat, int pat_words, int qb, int qe,
-                               const GWAMD_LDS uint32_t* tcod, int tb, int te, LeafPtr64 lpv, LeafPtr64 lmv,
-                               LeafPtr32 lsc, int8_t* path, int lane)
-{
-    const int m          = qe - qb;
-    const int T          = te - tb;
-    const uint64_t full  = (uint64_t(1) << m) - 1;
-    // segment patterns as one 64-bit word per letter
-    uint64_t e[4];
-    {
-        const int k  = qb >> 5;
-        const int sh = qb & 31;
-#pragma unroll
-        for (int L = 0; L < 4; L++)
-        {
-            const uint64_t w0 = k < pat_words ? pat[k * 8 + L] : 0u;
-            const uint64_t w1 = k + 1 < pat_words ? pat[(k + 1) * 8 + L] : 0u;
-            const uint64_t w2 = k + 2 < pat_words ? pat[(k + 2) * 8 + L] : 0u;
-            uint64_t r        = (w0 | (w1 << 32)) >> sh;
-            if (sh != 0)
-                r |= w2 << (64 - sh);
-            e[L] = uni64(r & full);
-        }
-    }
-    uint64_t pv = full, mv = 0;
-    int score   = m;
-    if (lane == 0)
-    {
-        lpv[0] = pv;
-        lmv[0] = mv;
-        lsc[0] = score;
-    }
-    for (int t = 1; t <= T; t++)
-    {
-        const int code    = uni(code_at(tcod, tb + t - 1));
-        const uint64_t lo = (code & 1) ? e[1] : e[0];
-        const uint64_t hi = (code & 1) ? e[3] : e[2];
-        const uint64_t eq = (code & 2) ? hi : lo;
-        const uint64_t xv = eq | mv;
-        const uint64_t xh = (((eq & pv) + pv) ^ pv) | eq;
-        uint64_t ph       = mv | ~(xh | pv);
-        uint64_t mh       = pv & xh;
-        score += int((ph >> (m - 1)) & 1u) - int((mh >> (m - 1)) & 1u);
-        ph = (ph << 1) | 1u;
-        mh = mh << 1;
-        pv = (mh | ~(xv | ph)) & full;
-        mv = (ph & xv) & full;
-        if (lane == 0)
-        {
-            lpv[t] = pv;
-            lmv[t] = mv;
-            lsc[t] = score;
-        }
-    }
-    __threadfence_block(); // the HBM variant: lane 0's stores before the wave's loads
-    wave_sync();
-    // D(i, j) = D(m, j) - sum of vertical deltas of rows i+1..m
-    auto D = [&](int i, int j) -> int {
-        if (i == 0)
-            return j;
-        const uint64_t hm = full & ~((uint64_t(1) << i) - 1);
-        const uint64_t p  = uni64(lpv[j]);
-        const uint64_t n  = uni64(lmv[j]);
-        return uni(lsc[j]) - __builtin_popcountll(p & hm) + __builtin_popcountll(n & hm);
-    };
-    int i = m, j = T, pos = 0;
-    int s = D(i, j);
-    while (i > 0 && j > 0)
-    {
-        const int above = D(i - 1, j);
-        const int diag  = D(i - 1, j - 1);
-        const int left  = D(i, j - 1);
-        int8_t r;
-        if (left + 1 == s)
-        {
-            r = kInsertion;
-            s = left;
-            --j;
-        }
-        else if (above + 1 == s)
-        {
-            r = kDeletion;
-            s = above;
-            --i;
-        }
-        else
-        {
-            r = diag == s ? kMatch : kMismatch;
-            s = diag;
-            --i;
-            --j;
-        }
-        if (lane == 0)
-            path[pos] = r;
-        ++pos;
-    }
-    for (int k = lane; k < i; k += kWave)
-        path[pos + k] = kDeletion;
-    pos += i;
-    for (int k = lane; k < j; k += kWave)
-        path[pos + k] = kInsertion;
-    pos += j;
-    return pos;
-}
-
-template <typename Buf>
-__device__ void run_split(int nblk, const GWAMD_LDS uint32_t* pat, int pat_words, int Q, int qb, int qm, int qe,
-                          const GWAMD_LDS uint32_t* tcod, int tb, int te, int lane, Buf fw, Buf rv)
+template <typename PatPtr, typename TcPtr, typename Buf>
+__device__ void run_split(int nblk, PatPtr pat, int pat_words, int Q, int qb, int qm, int qe,
+                          TcPtr tcod, int tb, int te, int lane, Buf fw, Buf rv)
 {
     switch (nblk)
     {
@@ -440,14 +394,10 @@ __device__ void run_split(int nblk, const GWAMD_LDS uint32_t* pat, int pat_words
 // half, one 32-row word per lane), with the carry look-ahead and the one-bit
 // shift cut at the group boundaries and the target letter read per lane.
 
-struct Seg16
+// frontier entry: query rows [qb, qe), target columns [tb, te)
+__device__ __forceinline__ uint4 seg_pack(int qb, int qe, int tb, int te)
 {
-    uint16_t qb, qe, tb, te;
-};
-
-__device__ __forceinline__ uint2 seg_pack(int qb, int qe, int tb, int te)
-{
-    return make_uint2(uint32_t(qb) | (uint32_t(qe) << 16), uint32_t(tb) | (uint32_t(te) << 16));
+    return make_uint4(uint32_t(qb), uint32_t(qe), uint32_t(tb), uint32_t(te));
 }
 
 // base case kinds (:577-611): 1 no target, 2 no query, 3 one query base,
@@ -477,9 +427,9 @@ struct PackSeg
 // segment holds the words of rows [qb, qm) (forward), group R those of rows
 // [qm, qe) of the reversed query.  fw / rv + boff receive the scores of
 // columns 0..Ts as split_sweep does for one segment.
-template <typename Buf>
-__device__ void packed_split_sweep(const GWAMD_LDS uint32_t* pat, int pat_words, int Q,
-                                   const GWAMD_LDS PackSeg* segs, int nseg, const GWAMD_LDS uint32_t* tcod, int lane,
+template <typename PatPtr, typename TcPtr, typename Buf>
+__device__ void packed_split_sweep(PatPtr pat, int pat_words, int Q,
+                                   const GWAMD_LDS PackSeg* segs, int nseg, TcPtr tcod, int lane,
                                    Buf fw, Buf rv)
 {
     // this lane's group
@@ -519,7 +469,7 @@ __device__ void packed_split_sweep(const GWAMD_LDS uint32_t* pat, int pat_words,
     int score    = g_m;
     Buf out      = g_rev ? rv : fw;
     if (is_last)
-        out[g_boff] = uint16_t(score);
+        out[g_boff] = score;
     // the letter of column t for this lane, read one column ahead
     auto code_of = [&](int t) -> int {
         if (!valid || t > g_ts)
@@ -553,7 +503,7 @@ __device__ void packed_split_sweep(const GWAMD_LDS uint32_t* pat, int pat_words,
         pv = mh | ~(xv | ph);
         mv = ph & xv;
         if (is_last && t <= g_ts)
-            out[g_boff + t] = uint16_t(score);
+            out[g_boff + t] = score;
         code = next;
     }
 }
@@ -602,12 +552,14 @@ __device__ int emit_base(int kind, int qb, int qe, int tb, int te, const char* q
     return leaf(qb, qe, tb, te, path);
 }
 
-// Full-Myers base case run by ONE lane (each lane of the wave takes one base
-// case of the frontier): the same recurrence and backtrace as
-// leaf_full_myers, with the column state in the lane's own stretch of the
-// slot and the path (end -> start) in its own stretch of path scratch.
-__device__ int leaf_lane(const GWAMD_LDS uint32_t* pat, int pat_words, int qb, int qe,
-                         const GWAMD_LDS uint32_t* tcod, int tb, int te, uint64_t* lpv, uint64_t* lmv, int32_t* lsc,
+// Full-Myers base case of a segment shorter than 63 rows (one 64-bit word;
+// hirschberg_myers_compute_path / append_myers_backtrace, :372-392,
+// :100-160), run by ONE lane (each lane of the wave takes one base case of
+// the frontier), with the column state in the lane's own stretch of the slot
+// and the path (end -> start) in its own stretch of path scratch.
+template <typename PatPtr, typename TcPtr>
+__device__ int leaf_lane(PatPtr pat, int pat_words, int qb, int qe,
+                         TcPtr tcod, int tb, int te, uint64_t* lpv, uint64_t* lmv, int32_t* lsc,
                          int8_t* path)
 {
     const int m         = qe - qb;
@@ -699,25 +651,47 @@ __device__ int leaf_lane(const GWAMD_LDS uint32_t* pat, int pat_words, int qb, i
 
 // ---------------------------------------------------------------------------
 // Hirschberg + Myers (hirschberg_myers, :569-638), one wave per pair.
+// LONG (queries over 16,384 or targets over 65,535 bases): query patterns in
+// the HBM slot instead of LDS, 32-bit split scores, and halves taller than
+// kMaxChunks blocks swept in stripes (half_sweep_striped).
+template <bool LONG>
 __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
 {
+    using SC = typename std::conditional<LONG, uint32_t, uint16_t>::type; // split score
+    using PatPtr = typename std::conditional<LONG, const uint32_t*, const GWAMD_LDS uint32_t*>::type;
+    // target letter codes: LDS; in long mode a generic pointer, to LDS when the
+    // target's codes fit it (a.ws_tcod_off < 0), else to the HBM slot
+    using TcW = typename std::conditional<LONG, uint32_t*, GWAMD_LDS uint32_t*>::type;
     extern __shared__ __align__(16) uint8_t lds[];
     const int lane                  = threadIdx.x;
     GWAMD_LDS uint8_t* base         = (GWAMD_LDS uint8_t*)(lds);
-    GWAMD_LDS uint32_t* tcod        = (GWAMD_LDS uint32_t*)(base + a.lds_target_off);
-    GWAMD_LDS uint32_t* pat         = (GWAMD_LDS uint32_t*)(base + a.lds_pat_off);
     GWAMD_LDS uint8_t* scratch      = base + a.lds_scratch_off;
     // split scores of segments up to kSplitLds columns (wider ones in HBM)
-    GWAMD_LDS uint16_t* fwl         = (GWAMD_LDS uint16_t*)(scratch + kLeafCols * kLeafColBytes);
-    GWAMD_LDS uint16_t* rvl         = fwl + kSplitLds;
+    GWAMD_LDS SC* fwl               = (GWAMD_LDS SC*)(scratch);
+    GWAMD_LDS SC* rvl               = fwl + kSplitLds;
     GWAMD_LDS PackSeg* pack         = (GWAMD_LDS PackSeg*)(base + a.lds_stack_off);
     uint8_t* ws                     = a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes);
-    uint16_t* fwg = reinterpret_cast<uint16_t*>(ws + ((int64_t(a.stride + 1) * kLeafColBytes + 15) & ~int64_t(15)));
-    uint16_t* rvg = fwg + (a.stride + 1 + kWave);
-    uint2* front[2];
-    front[0]      = reinterpret_cast<uint2*>(ws + a.ws_front_off);
+    SC* fwg       = reinterpret_cast<SC*>(ws + a.ws_split_off);
+    SC* rvg       = fwg + (a.stride + 1 + kWave);
+    int8_t* hbuf  = reinterpret_cast<int8_t*>(ws + a.ws_hbuf_off); // LONG: stripe hand-over
+    uint32_t* patw = reinterpret_cast<uint32_t*>(ws + a.ws_pat_off); // LONG: query patterns
+    PatPtr pat;
+    TcW tcod;
+    if constexpr (LONG)
+    {
+        pat  = patw;
+        tcod = a.ws_tcod_off >= 0 ? reinterpret_cast<uint32_t*>(ws + a.ws_tcod_off)
+                                  : (uint32_t*)((GWAMD_LDS uint32_t*)(base + a.lds_target_off));
+    }
+    else
+    {
+        pat  = (GWAMD_LDS uint32_t*)(base + a.lds_pat_off);
+        tcod = (GWAMD_LDS uint32_t*)(base + a.lds_target_off);
+    }
+    uint4* front[2];
+    front[0]      = reinterpret_cast<uint4*>(ws + a.ws_front_off);
     front[1]      = front[0] + a.front_cap;
-    uint16_t* spl = reinterpret_cast<uint16_t*>(front[1] + a.front_cap); // split column per entry
+    int32_t* spl  = reinterpret_cast<int32_t*>(front[1] + a.front_cap); // split column per entry
     // per-lane base cases: column state (pv, mv, score) and paths; (path
     // offset, length) per frontier entry
     uint64_t* lcol_pv = reinterpret_cast<uint64_t*>(ws + a.ws_leaf_off);
@@ -738,7 +712,10 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
         const int T    = uni(a.lens[2 * idx + 1]);
         int8_t* path   = a.paths + size_t(idx) * a.max_path_length;
         pack_target(tcod, tg, T, lane);
-        build_patterns(pat, q, Q, lane);
+        if constexpr (LONG)
+            build_patterns(patw, q, Q, lane); // read back after the fence below
+        else
+            build_patterns((GWAMD_LDS uint32_t*)(base + a.lds_pat_off), q, Q, lane);
         const int pat_words = (Q + kWordBits - 1) / kWordBits;
         if (lane == 0)
             front[0][0] = seg_pack(0, Q, 0, T);
@@ -763,16 +740,16 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
                     const int bo = uni(pack[s].boff);
                     const int bt = split_argmin(fwg + bo, rvg + bo, Ts, lane);
                     if (lane == 0)
-                        spl[uni(pack[s].f)] = uint16_t(bt);
+                        spl[uni(pack[s].f)] = bt;
                 }
                 wave_sync();
                 npk = 0, lanes_used = 0, boff = 0;
             };
             for (int f = 0; f < nf; f++)
             {
-                const uint2 v  = front[cur][f];
-                const int qb   = uni(int(v.x & 0xffffu)), qe = uni(int(v.x >> 16));
-                const int tb   = uni(int(v.y & 0xffffu)), te = uni(int(v.y >> 16));
+                const uint4 v  = front[cur][f];
+                const int qb   = uni(int(v.x)), qe = uni(int(v.y));
+                const int tb   = uni(int(v.z)), te = uni(int(v.w));
                 const int m    = qe - qb;
                 const int Ts   = te - tb;
                 if (base_kind(m, Ts, a.max_matrix_elems) != 0)
@@ -802,7 +779,15 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
                 pr[4] += uint64_t(Ts) * nblk;
 #endif
                 int bt;
-                if (Ts + 1 <= kSplitLds)
+                if (LONG && nblk > a.stripe_blocks)
+                {
+                    // halves over 8,192 rows (stripe_blocks = kMaxChunks; fewer
+                    // in the parity tests): one striped sweep per half
+                    half_sweep_striped(pat, pat_words, Q, qb, qm, false, tcod, tb, te, lane, fwg, hbuf, a.stripe_blocks);
+                    half_sweep_striped(pat, pat_words, Q, qm, qe, true, tcod, tb, te, lane, rvg, hbuf, a.stripe_blocks);
+                    bt = split_argmin(fwg, rvg, Ts, lane);
+                }
+                else if (Ts + 1 <= kSplitLds)
                 {
                     run_split(nblk, pat, pat_words, Q, qb, qm, qe, tcod, tb, te, lane, fwl, rvl);
                     wave_sync();
@@ -816,7 +801,7 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
                     bt = split_argmin(fwg, rvg, Ts, lane);
                 }
                 if (lane == 0)
-                    spl[f] = uint16_t(bt);
+                    spl[f] = bt;
                 wave_sync();
             }
             flush();
@@ -832,9 +817,9 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
             {
                 const int f      = f0 + lane;
                 const bool in    = f < nf;
-                const uint2 v    = in ? front[cur][f] : make_uint2(0, 0);
-                const int qb     = int(v.x & 0xffffu), qe = int(v.x >> 16);
-                const int tb     = int(v.y & 0xffffu), te = int(v.y >> 16);
+                const uint4 v    = in ? front[cur][f] : make_uint4(0, 0, 0, 0);
+                const int qb     = int(v.x), qe = int(v.y);
+                const int tb     = int(v.z), te = int(v.w);
                 const bool split = in && base_kind(qe - qb, te - tb, a.max_matrix_elems) == 0;
                 const int cnt    = in ? (split ? 2 : 1) : 0;
                 // exclusive prefix sum of cnt over the lanes
@@ -876,9 +861,9 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
             {
                 const int f   = f0 + lane;
                 const bool in = f < nf;
-                const uint2 v = in ? front[cur][f] : make_uint2(0, 0);
-                const int qb = int(v.x & 0xffffu), qe = int(v.x >> 16);
-                const int tb = int(v.y & 0xffffu), te = int(v.y >> 16);
+                const uint4 v = in ? front[cur][f] : make_uint4(0, 0, 0, 0);
+                const int qb = int(v.x), qe = int(v.y);
+                const int tb = int(v.z), te = int(v.w);
                 const bool full_myers = in && base_kind(qe - qb, te - tb, a.max_matrix_elems) == 4;
                 // scratch stretches: columns 0..Ts, path up to m + Ts states
                 int cc = full_myers ? te - tb + 1 : 0, pc = full_myers ? qe - qb + te - tb : 0;
@@ -910,9 +895,9 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
         int len = 0;
         for (int f = nf - 1; f >= 0; f--)
         {
-            const uint2 v = front[cur][f];
-            const int qb  = uni(int(v.x & 0xffffu)), qe = uni(int(v.x >> 16));
-            const int tb  = uni(int(v.y & 0xffffu)), te = uni(int(v.y >> 16));
+            const uint4 v = front[cur][f];
+            const int qb  = uni(int(v.x)), qe = uni(int(v.y));
+            const int tb  = uni(int(v.z)), te = uni(int(v.w));
             const int kind = base_kind(qe - qb, te - tb, a.max_matrix_elems);
             if (kind == 4)
             {
@@ -944,14 +929,37 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
 // Full Myers (myers_compute_score_matrix_kernel + myers_backtrace,
 // myers_gpu.cu:95-375): per (word, column) pv, mv and the score of the word's
 // last row in the workgroup's HBM slot, then the backtrace on the wave.
+// Queries over kMaxChunks blocks (8,192 bases) are swept in stripes of
+// kMaxChunks blocks, top to bottom, each over all columns; the horizontal
+// delta leaving a stripe's last row at every column reaches the next stripe
+// through a per-column int8 buffer in the slot (written and read back by the
+// same lane).  LONG: query patterns in the slot, target letter codes through
+// a generic pointer (LDS, or the slot for targets too long for LDS).
+template <bool LONG>
 __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
 {
+    using PatPtr = typename std::conditional<LONG, const uint32_t*, const GWAMD_LDS uint32_t*>::type;
+    using TcW    = typename std::conditional<LONG, uint32_t*, GWAMD_LDS uint32_t*>::type;
     extern __shared__ __align__(16) uint8_t lds[];
     const int lane          = threadIdx.x;
     GWAMD_LDS uint8_t* base = (GWAMD_LDS uint8_t*)(lds);
-    GWAMD_LDS uint8_t* tgt  = base + a.lds_target_off;
-    GWAMD_LDS uint32_t* pat = (GWAMD_LDS uint32_t*)(base + a.lds_pat_off);
     uint8_t* ws             = a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes);
+    int8_t* hbuf            = reinterpret_cast<int8_t*>(ws + a.ws_hbuf_off);
+    uint32_t* patw          = reinterpret_cast<uint32_t*>(ws + a.ws_pat_off);
+    PatPtr pat;
+    TcW tcod;
+    if constexpr (LONG)
+    {
+        pat  = patw;
+        tcod = a.ws_tcod_off >= 0 ? reinterpret_cast<uint32_t*>(ws + a.ws_tcod_off)
+                                  : (uint32_t*)((GWAMD_LDS uint32_t*)(base + a.lds_target_off));
+    }
+    else
+    {
+        pat  = (GWAMD_LDS uint32_t*)(base + a.lds_pat_off);
+        tcod = (GWAMD_LDS uint32_t*)(base + a.lds_target_off);
+    }
+    const int stripe_words = kMaxChunks * kWave;
 #ifdef GWAMD_ALN_PROFILE
     // [0] forward (score matrix) cycles, [1] backtrace cycles, [3] total,
     // [4] column-blocks, [5] backtrace steps
@@ -966,31 +974,39 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
         const int Q    = uni(a.lens[2 * idx]);
         const int T    = uni(a.lens[2 * idx + 1]);
         int8_t* path   = a.paths + size_t(idx) * a.max_path_length;
-        for (int k = lane; k < T; k += kWave)
-            tgt[k] = uint8_t(tg[k]);
-        build_patterns(pat, q, Q, lane);
+        pack_target(tcod, tg, T, lane);
+        if constexpr (LONG)
+            build_patterns(patw, q, Q, lane);
+        else
+            build_patterns((GWAMD_LDS uint32_t*)(base + a.lds_pat_off), q, Q, lane);
         const int nw = (Q + kWordBits - 1) / kWordBits;
+        __threadfence_block();
         wave_sync();
         uint32_t* wpv = reinterpret_cast<uint32_t*>(ws);
         uint32_t* wmv = wpv + size_t(nw) * (T + 1);
         int32_t* wsc  = reinterpret_cast<int32_t*>(wmv + size_t(nw) * (T + 1));
         GWAMD_PROF_T0(t_fwd);
-        if (Q > 0)
+        const uint32_t hisel    = lane >= 32 ? 1u : 0u;
+        const uint32_t lane0bit = lane == 0 ? 1u : 0u;
+        const int gl            = nw - 1;               // last word of the query
+        const int ghb           = (Q - 1) % kWordBits;  // its last row
+        for (int w0 = 0; w0 < nw; w0 += stripe_words)
         {
-            const int nch           = uni((nw + kWave - 1) / kWave);
-            const int lw            = nw - 1;
+            const int sw            = min(stripe_words, nw - w0);
+            const bool first        = w0 == 0;
+            const bool last_stripe  = w0 + sw == nw;
+            const int nch           = uni((sw + kWave - 1) / kWave);
+            const int lw            = sw - 1;
             const int lc            = lw / kWave;
             const int ll            = lw % kWave;
-            const int hb            = (Q - 1) % kWordBits;
-            const uint32_t hisel    = lane >= 32 ? 1u : 0u;
-            const uint32_t lane0bit = lane == 0 ? 1u : 0u;
+            const int hb            = last_stripe ? ghb : kWordBits - 1;
             MyersBlock B[kMaxChunks];
             int score[kMaxChunks];
 #pragma unroll
             for (int c = 0; c < kMaxChunks; c++)
             {
-                const int w      = c * kWave + lane;
-                const bool valid = c < nch && w < nw;
+                const int w      = w0 + c * kWave + lane;
+                const bool valid = c < nch && w < w0 + sw;
 #pragma unroll
                 for (int L = 0; L < 4; L++)
                     B[c].e[L] = valid ? seg_pattern(pat, nw, 0, w, L) : 0u;
@@ -1005,28 +1021,30 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
                     wsc[w] = score[c];
                 }
             }
-            int tv = 0;
+            int tv = 0, hv = 1, ho = 0;
             for (int t = 1; t <= T; t++)
             {
                 const int tl = (t - 1) & (kWave - 1);
                 if (tl == 0)
                 {
-                    const int x = t - 1 + lane;
-                    tv          = x < T ? int(tgt[x]) : 0;
+                    // next 64 columns: letter codes and the deltas entering the stripe
+                    const int x = t + lane;
+                    tv          = x <= T ? code_at(tcod, x - 1) : 0;
+                    hv          = (!first && x <= T) ? int(hbuf[x]) : 1; // first stripe: the top row's +1
                 }
-                const int code = letter(uni(__builtin_amdgcn_readlane(tv, tl)));
-                int h          = 1;
+                const int code = uni(__builtin_amdgcn_readlane(tv, tl));
+                int h          = uni(__builtin_amdgcn_readlane(hv, tl));
 #pragma unroll
                 for (int c = 0; c < kMaxChunks; c++)
                 {
                     if (c < nch)
                     {
-                        const int w = c * kWave + lane;
+                        const int w = w0 + c * kWave + lane;
                         int own     = 0;
                         h = myers_block_step<true>(B[c], code, h, c == lc, ll, hb, lane, hisel, lane0bit,
-                                                   w == lw ? hb : 31, &own);
+                                                   w == gl ? ghb : 31, &own);
                         score[c] += own;
-                        if (w < nw)
+                        if (w < w0 + sw)
                         {
                             wpv[size_t(t) * nw + w] = B[c].pv;
                             wmv[size_t(t) * nw + w] = B[c].mv;
@@ -1034,7 +1052,20 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
                         }
                     }
                 }
+                if (!last_stripe)
+                {
+                    // the delta leaving this stripe's last row, for the next stripe
+                    ho = lane == tl ? h : ho;
+                    if (tl == kWave - 1 || t == T)
+                    {
+                        const int x = t - tl + lane;
+                        if (x <= T)
+                            hbuf[x] = int8_t(ho);
+                    }
+                }
             }
+            __threadfence_block();
+            wave_sync();
         }
         __threadfence_block();
         wave_sync();
@@ -1117,10 +1148,14 @@ extern "C" hipError_t gwamd_internal_align_launch(const gwamd::aln::Args* a, int
     using namespace gwamd::aln;
     if (a->n <= 0)
         return hipSuccess;
-    if (algo == 0)
-        hipLaunchKernelGGL(hm_kernel, dim3(grid), dim3(kWave), size_t(a->lds_bytes), stream, *a);
+    if (algo == 0 && a->long_mode)
+        hipLaunchKernelGGL(hm_kernel<true>, dim3(grid), dim3(kWave), size_t(a->lds_bytes), stream, *a);
+    else if (algo == 0)
+        hipLaunchKernelGGL(hm_kernel<false>, dim3(grid), dim3(kWave), size_t(a->lds_bytes), stream, *a);
+    else if (a->long_mode)
+        hipLaunchKernelGGL(myers_kernel<true>, dim3(grid), dim3(kWave), size_t(a->lds_bytes), stream, *a);
     else
-        hipLaunchKernelGGL(myers_kernel, dim3(grid), dim3(kWave), size_t(a->lds_bytes), stream, *a);
+        hipLaunchKernelGGL(myers_kernel<false>, dim3(grid), dim3(kWave), size_t(a->lds_bytes), stream, *a);
     return hipGetLastError();
 }
 
@@ -1128,8 +1163,13 @@ extern "C" hipError_t gwamd_internal_align_occupancy(int algo, int lds_bytes, in
 {
     using namespace gwamd::aln;
     if (algo == 0)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, hm_kernel, kWave, size_t(lds_bytes));
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, myers_kernel, kWave, size_t(lds_bytes));
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, hm_kernel<false>, kWave, size_t(lds_bytes));
+    if (algo == 100)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, hm_kernel<true>, kWave, size_t(lds_bytes));
+    if (algo == 101)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, myers_kernel<true>, kWave,
+                                                            size_t(lds_bytes));
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, myers_kernel<false>, kWave, size_t(lds_bytes));
 }
 
 #ifdef GWAMD_ALN_PROFILE

@@ -108,8 +108,10 @@ int32_t gwamd_aligner_get_config(const gwamd_aligner* aligner, int32_t* grid, in
 /* Length limits of this implementation (the reference has none,
  * aligner_global_hirschberg_myers.cpp:47-51): gwamd_aligner_create throws
  * std::invalid_argument (GWAMD_E_INVALID_ARGUMENT) above them.  Hirschberg-
- * Myers: query 16384, target 65535; full and banded Myers: query 8192;
- * Ukkonen: target 65535 and a band of at most 512 diagonals.  *max_query and
+ * Myers and full Myers: 2^24 bases each (full Myers also needs one pair's
+ * score matrix, 0.375 B per cell, within a 32 GiB workspace slot); banded
+ * Myers: 65,536 each (patterns and target codes in LDS); Ukkonen: target
+ * 65535 and a band of at most 512 diagonals.  *max_query and
  * *max_target receive the query and target limits (Ukkonen: the largest
  * target for which any query passes). */
 int32_t gwamd_aligner_max_lengths(int32_t algorithm, int32_t* max_query, int32_t* max_target);

@@ -1,0 +1,123 @@
+"""GPU parity of the aligners past round 2's length limits (queries over
+16,384 bases for Hirschberg-Myers, over 8,192 for full and banded Myers,
+targets over 65,535): the long-mode kernels (query patterns in HBM, striped
+Myers sweeps, target codes in HBM past 131,072 bases, banded chunk state in
+HBM for bands wider than LDS) against the aligner oracle and the golden
+vectors of tests/golden/aligner_long.json (the reference's own benchmark
+recipes, cudaaligner/benchmarks/main.cpp:33-60, :85-124).  The reference has
+no length limit (aligner_global_hirschberg_myers.cpp:47-51)."""
+import hashlib
+import json
+import os
+import random
+
+import pytest
+
+from claragenomicsanalysis_amd import synth
+from claragenomicsanalysis_amd.cudaaligner import CudaAlignerBatch
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+LONG = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "aligner_long.json")))
+OALGO = {"hirschberg_myers": oracle.ALIGN_HM, "myers": oracle.ALIGN_MYERS, "myers_banded": oracle.ALIGN_MYERS_BANDED}
+
+
+def gpu_states(pairs, algorithm, max_q=None, max_t=None):
+    mq = max_q or max(len(q) for q, _ in pairs)
+    mt = max_t or max(len(t) for _, t in pairs)
+    b = CudaAlignerBatch(mq, mt, len(pairs), algorithm=algorithm)
+    for q, t in pairs:
+        assert b.add_alignment(q, t) == 0
+    b.align_all()
+    b.sync_alignments()
+    paths, plen = b.raw_paths()
+    return [paths[i, :plen[i]][::-1].tolist() for i in range(len(pairs))], mq
+
+
+def mutate(rng, s, err):
+    q = list(s)
+    for _ in range(int(len(s) * err)):
+        k, p = rng.randrange(3), rng.randrange(len(q) + 1)
+        if k == 0 and p < len(q):
+            q[p] = rng.choice("ACGT")
+        elif k == 1:
+            q.insert(p, rng.choice("ACGT"))
+        elif p < len(q):
+            del q[p]
+    return "".join(q)
+
+
+def rand_seq(rng, n):
+    return "".join(rng.choice("ACGT") for _ in range(n))
+
+
+@pytest.mark.parametrize("stripe_blocks", ["1", "2"])
+def test_hm_striped_sweeps_on_short_pairs(stripe_blocks, monkeypatch):
+    # GWAMD_HM_STRIPE_BLOCKS forces the long-mode kernel with stripes of 1 or 2
+    # blocks (2,048 / 4,096 rows), so 300 bp - 6 kb pairs cross several stripes
+    monkeypatch.setenv("GWAMD_HM_STRIPE_BLOCKS", stripe_blocks)
+    rng = random.Random(11 + int(stripe_blocks))
+    pairs = []
+    for n in (300, 2100, 4500, 6000, 9000):
+        t = rand_seq(rng, n)
+        pairs.append((mutate(rng, t, 0.1), t))
+    pairs.append(("A" * 5000, "C" * 4000))  # no match at all
+    got, mq = gpu_states(pairs, "hirschberg_myers")
+    for (q, t), g in zip(pairs, got):
+        assert g == oracle.align(q, t, oracle.ALIGN_HM, mq), (len(q), len(t))
+
+
+def test_hm_long_pairs_match_oracle():
+    rng = random.Random(21)
+    t1 = rand_seq(rng, 20000)
+    t2 = rand_seq(rng, 5000)
+    t3 = rand_seq(rng, 70000)
+    pairs = [(mutate(rng, t1, 0.1), t1),             # query > 16,384
+             (mutate(rng, t2, 0.02) + rand_seq(rng, 13000), t2),  # tall query, short target
+             (mutate(rng, t3[:30000], 0.05), t3)]     # target > 65,535
+    got, mq = gpu_states(pairs, "hirschberg_myers")
+    for (q, t), g in zip(pairs, got):
+        assert g == oracle.align(q, t, oracle.ALIGN_HM, mq), (len(q), len(t))
+
+
+@pytest.mark.parametrize("algo", ["myers", "myers_banded"])
+def test_myers_long_pairs_match_oracle(algo):
+    rng = random.Random(31)
+    t1 = rand_seq(rng, 20000)
+    t2 = rand_seq(rng, 9000)
+    pairs = [(mutate(rng, t1, 0.1), t1), (mutate(rng, t2, 0.03), t2[:3000])]
+    got, mq = gpu_states(pairs, algo)
+    for (q, t), g in zip(pairs, got):
+        assert g == oracle.align(q, t, OALGO[algo], mq), (len(q), len(t))
+
+
+def test_myers_banded_chunk_state_in_hbm(monkeypatch):
+    # a 4 KiB LDS region holds 256 band words; dissimilar 12 kb sequences
+    # double the band to the whole query (375 words), so the chunk state of
+    # the sweep goes through HBM (the path long queries take when the band
+    # outgrows LDS)
+    monkeypatch.setenv("GWAMD_BAND_TILE_BYTES", "4096")
+    rng = random.Random(41)
+    t = rand_seq(rng, 12000)
+    pairs = [(mutate(rng, t, 0.45), t), (rand_seq(rng, 11000), t)]
+    got, mq = gpu_states(pairs, "myers_banded")
+    for (q, tt), g in zip(pairs, got):
+        assert g == oracle.align(q, tt, oracle.ALIGN_MYERS_BANDED, mq)
+
+
+def _reference_pair(c):
+    e = c["size"] // 30
+    muts, genomes = synth.pairs(1, 1, c["size"], c["size"] if c["truncate_target"] else c["size"] + e + 1, e, e, e)
+    return genomes[0].decode(), muts[0].decode()
+
+
+@pytest.mark.parametrize("c", LONG["cases"], ids=lambda c: "%s-%s" % (c["recipe"], c["algorithm"]))
+def test_reference_benchmark_pairs_golden(c):
+    q, t = _reference_pair(c)
+    assert (len(q), len(t)) == (c["query_length"], c["target_length"])
+    got, _ = gpu_states([(q, t)], c["algorithm"], c["max_query_length"], c["max_target_length"])
+    p = got[0]
+    assert len(p) == c["path_length"]
+    assert [sum(1 for x in p if x == k) for k in range(4)] == c["counts"]
+    assert hashlib.sha256(bytes(p)).hexdigest() == c["path_sha256"]

@@ -76,10 +76,12 @@ def test_synthetic_generator_is_deterministic():
 
 def test_aligner_length_limits_are_queryable(built):
     # this implementation's limits (the reference has none): documented in
-    # include/gwamd_cudaaligner.h, INTEGRATION.md and DESIGN.md
+    # include/gwamd_cudaaligner.h, INTEGRATION.md and DESIGN.md.  The
+    # reference's own benchmarks run 100 kb (BM_SingleAlignment) and 65,536 bp
+    # batches for every aligner (cudaaligner/benchmarks/main.cpp:135-158).
     from claragenomicsanalysis_amd.cudaaligner import max_lengths
-    assert max_lengths("hirschberg_myers") == (16384, 65535)
-    assert max_lengths("myers") == (8192, 65535)
-    assert max_lengths("myers_banded") == (8192, 65535)
+    assert max_lengths("hirschberg_myers") == (1 << 24, 1 << 24)
+    assert max_lengths("myers") == (1 << 24, 1 << 24)  # and the pair's matrix within one 32 GiB slot
+    assert max_lengths("myers_banded") == (65536, 65536)
     q, t = max_lengths("ukkonen")
     assert q == 65535 and 8000 < t < 8300

@@ -170,3 +170,20 @@ def test_banded_paths_are_valid(seed):
     # the banded backtrace labels match / mismatch by score equality
     # (myers_gpu.cu:420-425), so only the consumption is checked here
     assert sum(s != 2 for s in st2) == len(q2) and sum(s != 3 for s in st2) == len(t)
+
+
+def test_long_golden_banded_65536_reproduces():
+    # tests/golden/aligner_long.json (make_aligner_long.py): the banded 65,536 bp
+    # case is cheap enough to re-derive here (~5 s); the others are pinned by the
+    # same script and checked on the GPU (tests/test_aligner_long.py)
+    import hashlib
+    import json
+    from claragenomicsanalysis_amd import synth
+    long = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "aligner_long.json")))
+    c = [c for c in long["cases"] if c["algorithm"] == "myers_banded"][0]
+    e = c["size"] // 30
+    muts, genomes = synth.pairs(1, 1, c["size"], c["size"], e, e, e)
+    q, t = genomes[0].decode(), muts[0].decode()
+    p = oracle.align(q, t, oracle.ALIGN_MYERS_BANDED, len(q))
+    assert len(p) == c["path_length"]
+    assert hashlib.sha256(bytes(p)).hexdigest() == c["path_sha256"]

@@ -167,31 +167,25 @@ def test_align_overlaps_more_engines_than_overlaps():
 
 
 @pytest.mark.gpu
-def test_align_overlaps_longer_than_the_aligner_limit(capfd):
-    # Hirschberg-Myers here takes queries of up to 16384 bases (the reference
-    # has no limit): an overlap past it is left without a CIGAR and reported
-    # on stderr, the others are aligned as usual (with the aligner sized by
-    # the overlaps it aligns)
+def test_align_overlaps_long_overlap_gets_its_cigar():
+    # an overlap longer than 16,384 query / 65,535 target bases (round 2's
+    # limits) takes the long-mode Hirschberg-Myers kernel (striped sweeps,
+    # patterns in HBM) and gets the same CIGAR as the oracle, like the
+    # reference's cudamapper -a (main.cu:48-122), which has no length limit
     from oracle import oracle
-    from claragenomicsanalysis_amd.cudaaligner import max_lengths
-    lim_q, lim_t = max_lengths("hirschberg_myers")
     queries, targets, ovs = _dataset(23, 3, 6, 300, 1500)
     rng = random.Random(5)
-    big_t = "".join(rng.choice("ACGT") for _ in range(lim_q + 700))
-    big_q = _mutate(rng, big_t, 0.02)
-    assert len(big_q) > lim_q
+    big_t = "".join(rng.choice("ACGT") for _ in range(70000))
+    big_q = _mutate(rng, big_t[:20000], 0.03)
     targets.append(big_t)
     queries.append(big_q)
     ovs.append(cm.Overlap(len(queries) - 1, len(targets) - 1, 0, len(big_q), 0, len(big_t), "+", 10))
     cigars = cm.align_overlaps(ovs, queries, targets, num_alignment_engines=2)
-    assert cigars[-1] == ""
-    assert "left without a CIGAR" in capfd.readouterr().err
-    mq = max(o.query_end - o.query_start for o in ovs[:-1])
-    for o, c in zip(ovs[:-1], cigars[:-1]):
+    mq = max(o.query_end - o.query_start for o in ovs)
+    for o, c in zip(ovs, cigars):
         qr = queries[o.query_read_id][o.query_start:o.query_end]
         tr = targets[o.target_read_id][o.target_start:o.target_end]
-        assert c == oracle.cigar(oracle.align(qr, rc(tr) if o.strand == "-" else tr, oracle.ALIGN_HM, mq))
+        assert c and c == oracle.cigar(oracle.align(qr, rc(tr) if o.strand == "-" else tr, oracle.ALIGN_HM, mq))
     paf = cm.format_paf(ovs, cigars, [("q%d" % i, s) for i, s in enumerate(queries)],
                         [("t%d" % i, s) for i, s in enumerate(targets)], 15)
-    lines = paf.splitlines()
-    assert "cg:Z:" not in lines[-1] and all("cg:Z:" in ln for ln in lines[:-1])
+    assert all("cg:Z:" in ln for ln in paf.splitlines())
