@@ -15,6 +15,11 @@ timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 step "bench default"
 timeout -k 10 600 python bench.py > $OUT/bench_default.log 2>&1 || { tail -20 $OUT/bench_default.log; exit 1; }
 tail -c 600 $OUT/bench_default.log
+for C in D_100k D_myers_64k D_banded_64k; do
+  step "bench $C"
+  timeout -k 10 300 python bench.py --config $C --steps 1 --warmup 1 --no-cpu > $OUT/bench_$C.log 2>&1 || { tail -20 $OUT/bench_$C.log; exit 1; }
+  tail -c 300 $OUT/bench_$C.log
+done
 step "aln_prof myers"
 timeout -k 10 300 python scripts/aln_prof.py 20000 myers > $OUT/alnprof_myers.log 2>&1 || { tail -5 $OUT/alnprof_myers.log; exit 1; }
 cat $OUT/alnprof_myers.log
