@@ -68,12 +68,14 @@ def test_multibatch_config_b_shape_sample():
 
 
 def test_multibatch_overlong_window_is_skipped_not_stale():
-    # a window whose read exceeds max_sequence_size fits no empty batch; the
-    # reference's loop stops every thread there.  Here the window gets
-    # exceeded_maximum_sequence_size, the rest are processed, and output
-    # arrays reused from an earlier call never keep stale rows.
+    # a window whose longest read needs more score-matrix memory than a whole
+    # batch has (reserve_buf fails on an empty batch, cudapoa_batch.cuh:542-564)
+    # fits no batch; the reference's loop stops every thread there.  Here the
+    # window gets exceeded_maximum_sequence_size (its read is longer than the
+    # batch's 300), the rest are processed, and output arrays reused from an
+    # earlier call never keep stale rows.
     wins = synth.poa_windows(4001, 30, 150, 6, 6, 6, 6)
-    wins.insert(11, [b"ACGT" * 100, b"ACGT" * 99])  # 400 > 300
+    wins.insert(11, [b"ACGT" * 7500, b"ACGT" * 99])
     mb = CudaPoaMultiBatch(8, 300, num_batches=2, mem_per_batch=mem_for(300, 8, 7))
     flat = [r for w in wins for r in w]
     bases = np.frombuffer(b"".join(flat), np.uint8)
