@@ -29,4 +29,9 @@ step "sq D"
 TAG=r3_D PROF_TIMEOUT=300 BENCH_ARGS="--config D --steps 1 --warmup 0 --no-cpu" bash scripts/pmc_sq.sh > $OUT/sq_D.log 2>&1 || { tail -20 $OUT/sq_D.log; exit 1; }
 step "sq D_myers"
 TAG=r3_D_myers PROF_TIMEOUT=300 BENCH_ARGS="--config D_myers --steps 1 --warmup 0 --no-cpu" bash scripts/pmc_sq.sh > $OUT/sq_D_myers.log 2>&1 || { tail -20 $OUT/sq_D_myers.log; exit 1; }
-step done
+step done1
+for P in tsprof bandprof; do
+  step "C counters $P"
+  GWAMD_LIBRARY=$PWD/claragenomicsanalysis_amd/lib/$P/libgwamd.so timeout -k 10 300 python bench.py --config C --steps 1 --warmup 0 --no-cpu --no-secondary > $OUT/bench_C_$P.log 2>&1 || { tail -20 $OUT/bench_C_$P.log; exit 1; }
+done
+step done2
