@@ -72,6 +72,11 @@ CONFIGS = {
     # BatchSize(10600, 16, 256) -> int32 scores and node ids
     "C": dict(backbone=10000, reads=16, err=500, max_seq=10600, banded=True, bw=256, windows=128, msa=True,
               mem_per_window=400e6),
+    # band widths past the LDS band kernel's 128 / 256 (the reference accepts any
+    # multiple of 128, batch.hpp:85-94): the global-memory kernel
+    "B_banded_512": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=True, bw=512, windows=1024),
+    "C_512": dict(backbone=10000, reads=16, err=500, max_seq=10600, banded=True, bw=512, windows=128, msa=True,
+                  mem_per_window=600e6),
 }
 # the config-B generator, seeds 1..1e6, 125k per GPU
 STREAM_CONFIGS = {"E": dict(CONFIGS["B"], windows_per_step=E_STEP_WINDOWS)}

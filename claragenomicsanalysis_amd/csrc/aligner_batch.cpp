@@ -529,6 +529,8 @@ private:
         scratch_bytes_      = 0;
         if (hm) // LDS split scores of segments up to kSplitLds columns
             scratch_bytes_ = int32_t(a16(int64_t(2) * kSplitLds * sc_bytes));
+        else // full Myers: the backtrace tile (8 words x 64 columns of pv, mv, score)
+            scratch_bytes_ = 8 * 64 * 12;
         lds_stack_off_ = lds_scratch_off_ + scratch_bytes_;
         lds_bytes_     = lds_stack_off_ + (hm ? kStackSize * 16 : 0);
         if (lds_bytes_ > 65536)

@@ -935,6 +935,9 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
 // through a per-column int8 buffer in the slot (written and read back by the
 // same lane).  LONG: query patterns in the slot, target letter codes through
 // a generic pointer (LDS, or the slot for targets too long for LDS).
+constexpr int kTbW = 8;  // full-Myers backtrace tile: words
+constexpr int kTbC = 64; // and columns (12 B per entry in LDS)
+
 template <bool LONG>
 __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
 {
@@ -1074,23 +1077,55 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
         pr[4] += uint64_t(T) * uint64_t((nw + kWave - 1) / kWave);
 #endif
         GWAMD_PROF_T0(t_bt);
-        // backtrace (myers_backtrace, myers_gpu.cu:181-245)
+        // backtrace (myers_backtrace, myers_gpu.cu:181-245).  The walk reads
+        // words (i-2)/32, (i-1)/32 of columns j-1, j; a tile of kTbW words x
+        // kTbC columns ending at the current cell is staged in LDS with one
+        // round of lane-parallel loads and refilled when the walk leaves it
+        // (about every 64 steps), so a step costs LDS reads, not HBM latency.
         const uint32_t last_mask = (Q % kWordBits) != 0 ? (1u << (Q % kWordBits)) - 1u : ~0u;
-        auto gms                 = [&](int i, int j) -> int {
+        GWAMD_LDS uint32_t* tpv  = (GWAMD_LDS uint32_t*)(base + a.lds_scratch_off);
+        GWAMD_LDS uint32_t* tmv  = tpv + kTbW * kTbC;
+        GWAMD_LDS int32_t* tsc   = (GWAMD_LDS int32_t*)(tmv + kTbW * kTbC);
+        int tw0 = 0, tc0 = 0;
+        auto refill = [&](int i, int j) {
+            tw0 = max(0, (i - 1) / kWordBits - (kTbW - 1));
+            tc0 = max(0, j - (kTbC - 1));
+            wave_sync(); // the previous tile's readers are done
+#pragma unroll
+            for (int e0 = 0; e0 < kTbW * kTbC; e0 += kWave)
+            {
+                const int e = e0 + lane;
+                const int c = tc0 + e / kTbW, w = tw0 + e % kTbW;
+                if (c <= j && w < nw)
+                {
+                    const size_t o = size_t(c) * nw + w;
+                    tpv[e]         = wpv[o];
+                    tmv[e]         = wmv[o];
+                    tsc[e]         = wsc[o];
+                }
+            }
+            wave_sync();
+        };
+        auto gms = [&](int i, int j) -> int {
             const int wi     = (i - 1) / kWordBits;
             const int bi     = (i - 1) % kWordBits;
             uint32_t mask    = (~1u) << bi;
             if (wi == nw - 1)
                 mask &= last_mask;
-            const size_t o   = size_t(j) * nw + wi;
-            const uint32_t p = uniu(wpv[o]);
-            const uint32_t n = uniu(wmv[o]);
-            return uni(wsc[o]) - __builtin_popcount(mask & p) + __builtin_popcount(mask & n);
+            const int e      = (j - tc0) * kTbW + (wi - tw0);
+            const uint32_t p = uniu(tpv[e]);
+            const uint32_t n = uniu(tmv[e]);
+            return uni(tsc[e]) - __builtin_popcount(mask & p) + __builtin_popcount(mask & n);
         };
         int i = Q, j = T, pos = 0;
         int s = Q > 0 ? uni(wsc[size_t(T) * nw + (nw - 1)]) : 0;
+        int pbuf = 0; // 64 path states, one per lane, stored together
+        if (i > 0 && j > 0)
+            refill(i, j);
         while (i > 0 && j > 0)
         {
+            if (j - 1 < tc0 || (i > 1 && (i - 2) / kWordBits < tw0))
+                refill(i, j);
             const int above = i == 1 ? j : gms(i - 1, j);
             const int diag  = i == 1 ? j - 1 : gms(i - 1, j - 1);
             const int left  = gms(i, j - 1);
@@ -1114,10 +1149,13 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
                 --i;
                 --j;
             }
-            if (lane == 0)
-                path[pos] = r;
+            pbuf = lane == (pos & (kWave - 1)) ? int(r) : pbuf;
+            if ((pos & (kWave - 1)) == kWave - 1)
+                path[pos - (kWave - 1) + lane] = int8_t(pbuf);
             ++pos;
         }
+        if (lane < (pos & (kWave - 1)))
+            path[(pos & ~(kWave - 1)) + lane] = int8_t(pbuf);
         for (int k = lane; k < i; k += kWave)
             path[pos + k] = kDeletion;
         pos += i;

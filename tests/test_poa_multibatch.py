@@ -105,7 +105,7 @@ def test_multibatch_overlong_window_is_skipped_not_stale():
 
 
 def test_multibatch_rejects_inconsistent_inputs():
-    mb = CudaPoaMultiBatch(4, 100, num_batches=1, mem_per_batch=mem_for(100, 4, 4))
+    mb = CudaPoaMultiBatch(4, 300, num_batches=1, mem_per_batch=mem_for(300, 4, 4))
     with pytest.raises(ValueError):
         mb.process_packed(np.zeros(10, np.uint8), np.array([5, 5], np.int32), [3])
     with pytest.raises(ValueError):
