@@ -812,51 +812,37 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
         {
             // the loop state is wave-uniform; saying so keeps it in SGPRs with
             // scalar branches whatever the caller's control flow looks like
-            tail    = uniform(tail);
-            q       = uniform(q);
-            vinfo   = uint32_t(uniform(int(vinfo)));
-            int deg = int((vinfo >> 16) & 63u);
+            tail      = uniform(tail);
+            q         = uniform(q);
+            vinfo     = uint32_t(uniform(int(vinfo)));
+            const int deg = int((vinfo >> 16) & 63u);
+            // The word of the next queue entry, when it is queued already, is
+            // final (a queued node is never decremented again), so its read is
+            // issued together with this pop's successor read: one LDS round
+            // trip per node where the graph is wide.  Otherwise the next node
+            // is the first one this pop releases (its word is in a register).
+            const bool have_next = q + 1 < tail;
+            uint32_t nxt         = have_next ? pop_info(q + 1, tail) : 0u;
             if (deg == 1)
             {
-                // single-successor run: one dependent LDS read per node.  A
-                // released node's word is not written back (nothing decrements
-                // it again and a pop uses only its degree and successor bits),
-                // and one popped next comes from the register, not the queue.
-                for (;;)
+                // single successor: release it when its in-degree reaches 0
+                // (a released node's word is not written back: nothing
+                // decrements it again and a pop uses only its degree and
+                // successor bits)
+                const int o       = int(vinfo & 0xffffu);
+                const uint32_t oi = uint32_t(uniform(int(info[o]))) - (1u << 24);
+                if ((oi >> 24) == 0u)
                 {
-                    const int o       = int(vinfo & 0xffffu);
-                    const uint32_t oi = uint32_t(uniform(int(info[o]))) - (1u << 24);
-                    q++;
-                    if ((oi >> 24) == 0u)
-                    {
-                        queue[tail] = uint16_t(o);
-                        if (q == tail)
-                        {
-                            tail++;
-                            vinfo = oi;
-                            if (((oi >> 16) & 63u) == 1u)
-                                continue;
-                            break;
-                        }
-                        if (kMode != 0)
-                            qinfo[uint32_t(tail) & qmask] = oi;
-                        tail++;
-                    }
-                    else
-                    {
-                        info[o] = oi;
-                        if (q >= tail)
-                            break;
-                    }
-                    vinfo = pop_info(q, tail);
-                    if (((vinfo >> 16) & 63u) != 1u)
-                        break;
+                    queue[tail] = uint16_t(o);
+                    if (kMode != 0 && have_next)
+                        qinfo[uint32_t(tail) & qmask] = oi;
+                    nxt = have_next ? nxt : oi;
+                    tail++;
                 }
-                continue;
+                else
+                    info[o] = oi;
             }
-            const int qtail     = tail; // entries pushed by this step start here
-            uint32_t first_info = 0;
-            if (deg >= 2)
+            else if (deg >= 2)
             {
                 // all successors at once, one per lane: children are distinct,
                 // so the decrements are independent; ready ones are queued in
@@ -878,14 +864,13 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
                         if (kMode != 0)
                             qinfo[uint32_t(tail + before) & qmask] = oi;
                     }
-                    first_info = uint32_t(__builtin_amdgcn_readlane(int(oi), __builtin_ctzll(ready)));
+                    if (!have_next)
+                        nxt = uint32_t(__builtin_amdgcn_readlane(int(oi), __builtin_ctzll(ready)));
                     tail += __popcll(ready);
                 }
             }
             q++;
-            if (q < tail)
-                vinfo = (q == qtail) ? first_info
-                                     : pop_info(q, tail);
+            vinfo = nxt;
         }
         return tail;
     };
