@@ -567,10 +567,12 @@ private:
         {
             // full matrix: pv, mv, score per (word, column), then the stripes'
             // per-column deltas, and in long mode the patterns and target codes
-            hbuf_off_   = a16(int64_t(pat_words) * (max_t_ + 1) * 12 + 64);
+            const int64_t nwp = (int64_t(pat_words) + 31) & ~int64_t(31); // 128-B rows
+            hbuf_off_   = a16(nwp * (max_t_ + 1) * 12 + 64);
             pat_off_    = a16(hbuf_off_ + int64_t(max_t_) + 1 + kWave + 64);
             tcod_off_   = a16(pat_off_ + (long_mode_ ? int64_t(pat_words) * 32 + 64 : 0));
             slot_bytes_ = a16(tcod_off_ + (tcod_hbm_ ? int64_t(max_t_ + 15) / 16 * 4 + 64 : 0));
+            slot_bytes_ = (slot_bytes_ + 255) & ~int64_t(255); // slots start on whole lines
             if (slot_bytes_ > gwamd::host::kMyersMaxSlot)
                 throw std::invalid_argument("max_query_length x max_target_length too large for the full Myers "
                                             "aligner's score matrix (" + std::to_string(slot_bytes_) + " bytes)");

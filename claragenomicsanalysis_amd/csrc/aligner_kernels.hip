@@ -985,9 +985,14 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
         const int nw = (Q + kWordBits - 1) / kWordBits;
         __threadfence_block();
         wave_sync();
+        // (word, column) entry t * nwp + w; the row stride is padded to whole
+        // 128-B lines and the pad words are stored too, so every line a
+        // column writes is written whole by one store (no partial lines for
+        // the L2 to fill from HBM)
+        const int nwp = (nw + 31) & ~31;
         uint32_t* wpv = reinterpret_cast<uint32_t*>(ws);
-        uint32_t* wmv = wpv + size_t(nw) * (T + 1);
-        int32_t* wsc  = reinterpret_cast<int32_t*>(wmv + size_t(nw) * (T + 1));
+        uint32_t* wmv = wpv + size_t(nwp) * (T + 1);
+        int32_t* wsc  = reinterpret_cast<int32_t*>(wmv + size_t(nwp) * (T + 1));
         GWAMD_PROF_T0(t_fwd);
         const uint32_t hisel    = lane >= 32 ? 1u : 0u;
         const uint32_t lane0bit = lane == 0 ? 1u : 0u;
@@ -1003,6 +1008,7 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
             const int lc            = lw / kWave;
             const int ll            = lw % kWave;
             const int hb            = last_stripe ? ghb : kWordBits - 1;
+            const int wend          = last_stripe ? nwp : w0 + sw; // stored words (incl. the pad)
             MyersBlock B[kMaxChunks];
             int score[kMaxChunks];
 #pragma unroll
@@ -1017,7 +1023,7 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
                 B[c].mv  = 0u;
                 B[c].act = __builtin_amdgcn_ballot_w64(valid);
                 score[c] = min((w + 1) * kWordBits, Q); // myers_gpu.cu:341
-                if (valid)
+                if (c < nch && w < wend)
                 {
                     wpv[w] = ~0u;
                     wmv[w] = 0u;
@@ -1047,11 +1053,11 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
                         h = myers_block_step<true>(B[c], code, h, c == lc, ll, hb, lane, hisel, lane0bit,
                                                    w == gl ? ghb : 31, &own);
                         score[c] += own;
-                        if (w < w0 + sw)
+                        if (w < wend)
                         {
-                            wpv[size_t(t) * nw + w] = B[c].pv;
-                            wmv[size_t(t) * nw + w] = B[c].mv;
-                            wsc[size_t(t) * nw + w] = score[c];
+                            wpv[size_t(t) * nwp + w] = B[c].pv;
+                            wmv[size_t(t) * nwp + w] = B[c].mv;
+                            wsc[size_t(t) * nwp + w] = score[c];
                         }
                     }
                 }
@@ -1098,7 +1104,7 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
                 const int c = tc0 + e / kTbW, w = tw0 + e % kTbW;
                 if (c <= j && w < nw)
                 {
-                    const size_t o = size_t(c) * nw + w;
+                    const size_t o = size_t(c) * nwp + w;
                     tpv[e]         = wpv[o];
                     tmv[e]         = wmv[o];
                     tsc[e]         = wsc[o];
@@ -1118,7 +1124,7 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
             return uni(tsc[e]) - __builtin_popcount(mask & p) + __builtin_popcount(mask & n);
         };
         int i = Q, j = T, pos = 0;
-        int s = Q > 0 ? uni(wsc[size_t(T) * nw + (nw - 1)]) : 0;
+        int s = Q > 0 ? uni(wsc[size_t(T) * nwp + (nw - 1)]) : 0;
         int pbuf = 0; // 64 path states, one per lane, stored together
         if (i > 0 && j > 0)
             refill(i, j);
