@@ -31,7 +31,7 @@ constexpr int32_t kHmMaxTarget = 1 << 24;
 constexpr int32_t kHmLdsTarget = 131072;
 // full Myers: one pair's (word, column) state (0.375 B per cell) per slot
 constexpr int64_t kMyersMaxSlot   = int64_t(32) << 30;
-constexpr int64_t kMyersWorkspace = int64_t(48) << 30; // resident slots within 48 GiB of the 288 GB HBM
+constexpr int64_t kMyersWorkspace = int64_t(64) << 30; // resident slots within 64 GiB of the 288 GB HBM
 // Hirschberg-Myers takes the LDS-resident kernel (hm_kernel<false>, patterns in
 // LDS, register-resident sweeps of up to 4 blocks per half) up to these sizes
 constexpr int32_t kHmShortQuery  = 16384;
@@ -510,6 +510,8 @@ private:
         // full Myers takes it past 8,192 x 65,535 (its stripes work either way)
         long_mode_ = hm ? (max_q_ > gwamd::host::kHmShortQuery || max_t_ > gwamd::host::kHmShortTarget)
                         : (max_q_ > 8192 || max_t_ > gwamd::host::kHmShortTarget);
+        if (!hm && std::getenv("GWAMD_MYERS_LONG")) // experiment: patterns in HBM at any size (less LDS per wave)
+            long_mode_ = std::atoi(std::getenv("GWAMD_MYERS_LONG")) != 0 || long_mode_;
         // GWAMD_HM_STRIPE_BLOCKS=1..4 (parity tests): long mode at any size, with
         // stripes of that many blocks, so short pairs take the striped sweeps
         stripe_blocks_ = kMaxChunks;
@@ -529,8 +531,8 @@ private:
         scratch_bytes_      = 0;
         if (hm) // LDS split scores of segments up to kSplitLds columns
             scratch_bytes_ = int32_t(a16(int64_t(2) * kSplitLds * sc_bytes));
-        else // full Myers: the backtrace tile (8 words x 64 columns of pv, mv, score)
-            scratch_bytes_ = 8 * 64 * 12;
+        else // full Myers: the backtrace tile (kTbW words x 64 columns of pv, mv, score)
+            scratch_bytes_ = 4 * 64 * 12;
         lds_stack_off_ = lds_scratch_off_ + scratch_bytes_;
         lds_bytes_     = lds_stack_off_ + (hm ? kStackSize * 16 : 0);
         if (lds_bytes_ > 65536)

@@ -935,7 +935,7 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
 // through a per-column int8 buffer in the slot (written and read back by the
 // same lane).  LONG: query patterns in the slot, target letter codes through
 // a generic pointer (LDS, or the slot for targets too long for LDS).
-constexpr int kTbW = 8;  // full-Myers backtrace tile: words
+constexpr int kTbW = 4;  // full-Myers backtrace tile: words
 constexpr int kTbC = 64; // and columns (12 B per entry in LDS)
 
 template <bool LONG>

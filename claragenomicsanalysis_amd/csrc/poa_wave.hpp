@@ -289,33 +289,72 @@ __device__ __forceinline__ int add_alignment_parallel(WinGraph<SizeT> g, int& no
             X.gid[rp] = uint16_t(int(ag[k]) < 0 ? 0xffff : int(ag[k]));
     }
     wave_sync();
-    // kinds and existing targets
-    for (int rp = lane; rp < L; rp += kWave)
+    // kinds and existing targets.  kAU positions per lane and pass, their
+    // graph loads issued together (the graph is in HBM: one round trip per
+    // dependent level instead of one per position)
+    constexpr int kAU = 4;
+    for (int r0 = 0; r0 < L; r0 += kAU * kWave)
     {
-        const int gid    = int(X.gid[rp]);
-        const uint8_t rb = read[rp];
-        int kind = 2, curr = 0;
-        if (gid != 0xffff)
+        int gid[kAU], kind[kAU], curr[kAU], na[kAU], gb[kAU];
+        uint8_t rb[kAU];
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
         {
-            if (g.base[gid] == rb)
-                kind = 0, curr = gid;
-            else
+            const int rp = r0 + u * kWave + lane;
+            gid[u]       = rp < L ? int(X.gid[rp]) : 0xffff;
+            rb[u]        = rp < L ? read[rp] : uint8_t(0);
+        }
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            const bool has = gid[u] != 0xffff;
+            gb[u]          = has ? int(g.base[gid[u]]) : 0;
+            na[u]          = has ? int(g.aln_cnt[gid[u]]) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            kind[u] = gid[u] == 0xffff ? 2 : (gb[u] == int(rb[u]) ? 0 : 3);
+            curr[u] = kind[u] == 0 ? gid[u] : 0;
+        }
+        // aligned-node lists of the mismatching positions, 4 entries at a
+        // time: the first aligned node with the read's base (:130-150)
+        for (int n0 = 0;; n0 += 4)
+        {
+            bool need = false;
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+                need |= kind[u] == 3 && n0 < na[u];
+            if (__builtin_amdgcn_ballot_w64(need) == 0)
+                break;
+            int aid[kAU][4], ab[kAU][4];
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    aid[u][j] = (kind[u] == 3 && n0 + j < na[u]) ? int(g.aln[gid[u] * kMaxAlignments + n0 + j]) : -1;
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    ab[u][j] = aid[u][j] >= 0 ? int(g.base[aid[u][j]]) : -1;
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (kind[u] == 3 && aid[u][j] >= 0 && ab[u][j] == int(rb[u]))
+                        kind[u] = 1, curr[u] = aid[u][j];
+        }
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            const int rp = r0 + u * kWave + lane;
+            if (rp < L)
             {
-                kind         = 3;
-                const int na = int(g.aln_cnt[gid]);
-                for (int n = 0; n < na; n++)
-                {
-                    const int aid = int(g.aln[gid * kMaxAlignments + n]);
-                    if (g.base[aid] == rb)
-                    {
-                        kind = 1, curr = aid;
-                        break;
-                    }
-                }
+                X.kind[rp] = uint8_t(kind[u]);
+                X.curr[rp] = uint16_t(curr[u]);
             }
         }
-        X.kind[rp] = uint8_t(kind);
-        X.curr[rp] = uint16_t(curr);
     }
     wave_sync();
     // new node ids: prefix sum over new-node elements in read order
@@ -376,28 +415,58 @@ __device__ __forceinline__ int add_alignment_parallel(WinGraph<SizeT> g, int& no
     wave_sync();
     if (X.sh[0])
         return -1;
-    // edge existence and edge-limit errors
-    for (int rp = lane + 1; rp < L; rp += kWave)
+    // edge existence and edge-limit errors (kAU positions per lane and pass)
+    for (int r0 = 1; r0 < L; r0 += kAU * kWave)
     {
-        const int head = int(X.curr[rp - 1]);
-        const int curr = int(X.curr[rp]);
-        const int kind = X.kind[rp];
-        bool exists    = false;
-        int ic         = 0;
-        if (kind < 2)
+        int head[kAU], curr[kAU], kind[kAU], ic[kAU], oc[kAU];
+        bool exists[kAU];
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
         {
-            ic = int(g.in_cnt[curr]);
-            for (int e = 0; e < ic; e++)
-                exists |= int(g.in_e[curr * kMaxEdges + e]) == head;
+            const int rp = r0 + u * kWave + lane;
+            const bool in = rp < L;
+            head[u]       = in ? int(X.curr[rp - 1]) : 0;
+            curr[u]       = in ? int(X.curr[rp]) : 0;
+            kind[u]       = in ? int(X.kind[rp]) : 2;
+            const int kp  = in ? int(X.kind[rp - 1]) & 3 : 2; // (bit 2 may be set by the previous pass)
+            ic[u]         = kind[u] < 2 ? int(g.in_cnt[curr[u]]) : 0;
+            oc[u]         = kp >= 2 ? 0 : int(g.out_cnt[head[u]]);
+            exists[u]     = false;
         }
-        if (!exists)
+        for (int e0 = 0;; e0 += 4)
         {
-            const int oc = X.kind[rp - 1] >= 2 ? 0 : int(g.out_cnt[head]);
-            if (oc + 1 >= kMaxEdges || ic + 1 >= kMaxEdges)
-                err = min(err, (rp << 8) | int(kEdgeCountExceeded));
+            bool need = false;
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+                need |= !exists[u] && e0 < ic[u];
+            if (__builtin_amdgcn_ballot_w64(need) == 0)
+                break;
+            int ie[kAU][4];
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    ie[u][j] = (!exists[u] && e0 + j < ic[u]) ? int(g.in_e[curr[u] * kMaxEdges + e0 + j]) : -1;
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    exists[u] |= ie[u][j] == head[u];
         }
-        else
-            X.kind[rp] = uint8_t(kind | 4);
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            const int rp = r0 + u * kWave + lane;
+            if (rp >= L)
+                continue;
+            if (!exists[u])
+            {
+                if (oc[u] + 1 >= kMaxEdges || ic[u] + 1 >= kMaxEdges)
+                    err = min(err, (rp << 8) | int(kEdgeCountExceeded));
+            }
+            else
+                X.kind[rp] = uint8_t(kind[u] | 4);
+        }
     }
     err = -wave_max(-err); // wave-wide minimum
     if (err != INT_MAX)
@@ -436,54 +505,102 @@ __device__ __forceinline__ int add_alignment_parallel(WinGraph<SizeT> g, int& no
         }
     }
     wave_sync();
-    // writes 2: the edge head -> curr and the coverage of curr
-    for (int rp = lane; rp < L; rp += kWave)
+    // writes 2: the edge head -> curr and the coverage of curr.  Element rp
+    // touches only curr's in-list and coverage and head's out-list (head =
+    // element rp-1's curr), so the elements are independent; kAU per lane and
+    // pass, with their loads issued together.
+    for (int r0 = 0; r0 < L; r0 += kAU * kWave)
     {
-        const int curr = int(X.curr[rp]);
-        if (MSA && rp == 0)
-            seq_begin[s] = SizeT(curr);
-        if (rp > 0)
+        int curr[kAU], head[kAU], kind[kAU], wsum[kAU], ic[kAU], oc[kAU], cv[kAU], hit[kAU], ohit[kAU];
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
         {
-            const int head = int(X.curr[rp - 1]);
-            const int wsum = int(uint16_t(int(w[rp - 1]))) + int(w[rp]);
-            if (X.kind[rp] & 4)
-            {
-                const int ic = int(g.in_cnt[curr]);
-                for (int e = 0; e < ic; e++)
-                    if (int(g.in_e[curr * kMaxEdges + e]) == head)
-                        g.in_w[curr * kMaxEdges + e] = uint16_t(int(g.in_w[curr * kMaxEdges + e]) + wsum);
-                if (MSA)
+            const int rp = r0 + u * kWave + lane;
+            const bool in = rp < L;
+            curr[u]       = in ? int(X.curr[rp]) : 0;
+            head[u]       = (in && rp > 0) ? int(X.curr[rp - 1]) : 0;
+            kind[u]       = (in && rp > 0) ? int(X.kind[rp]) : -1; // -1: no edge (rp 0 or out of range)
+            wsum[u]       = (in && rp > 0) ? int(uint16_t(int(w[rp - 1]))) + int(w[rp]) : 0;
+            if (MSA && in && rp == 0)
+                seq_begin[s] = SizeT(curr[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            const int rp = r0 + u * kWave + lane;
+            ic[u]        = kind[u] >= 0 ? int(g.in_cnt[curr[u]]) : 0;
+            oc[u]        = (kind[u] >= 0 && (!(kind[u] & 4) || MSA)) ? int(g.out_cnt[head[u]]) : 0;
+            cv[u]        = rp < L ? int(g.cov[curr[u]]) : 0;
+            hit[u]       = -1;
+            ohit[u]      = -1;
+        }
+        // existing edges: their slot in curr's in-list (and, MSA, in head's out-list)
+        for (int e0 = 0;; e0 += 4)
+        {
+            bool need = false;
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+                need |= kind[u] >= 0 && (kind[u] & 4) && ((hit[u] < 0 && e0 < ic[u]) || (MSA && ohit[u] < 0 && e0 < oc[u]));
+            if (__builtin_amdgcn_ballot_w64(need) == 0)
+                break;
+            int ie[kAU][4], oe[kAU][4];
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
                 {
-                    const int oc = int(g.out_cnt[head]);
-                    for (int e = 0; e < oc; e++)
+                    const bool ex = kind[u] >= 0 && (kind[u] & 4);
+                    ie[u][j] = (ex && hit[u] < 0 && e0 + j < ic[u]) ? int(g.in_e[curr[u] * kMaxEdges + e0 + j]) : -1;
+                    oe[u][j] = (MSA && ex && ohit[u] < 0 && e0 + j < oc[u]) ? int(g.out_e[head[u] * kMaxEdges + e0 + j])
+                                                                             : -1;
+                }
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                {
+                    if (hit[u] < 0 && ie[u][j] >= 0 && ie[u][j] == head[u])
+                        hit[u] = e0 + j;
+                    if (MSA && ohit[u] < 0 && oe[u][j] >= 0 && oe[u][j] == curr[u])
+                        ohit[u] = e0 + j;
+                }
+        }
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            const int rp = r0 + u * kWave + lane;
+            if (rp >= L)
+                continue;
+            if (kind[u] >= 0)
+            {
+                const int cu = curr[u], hd = head[u];
+                if (kind[u] & 4)
+                {
+                    if (hit[u] >= 0)
+                        g.in_w[cu * kMaxEdges + hit[u]] = uint16_t(int(g.in_w[cu * kMaxEdges + hit[u]]) + wsum[u]);
+                    if (MSA && ohit[u] >= 0)
                     {
-                        if (int(g.out_e[head * kMaxEdges + e]) == curr)
-                        {
-                            const int c                                       = int(ecov_cnt[head * kMaxEdges + e]);
-                            ecov[size_t(head * kMaxEdges + e) * max_seqs + c] = uint16_t(s);
-                            ecov_cnt[head * kMaxEdges + e]                    = uint16_t(c + 1);
-                            break;
-                        }
+                        const int c                                             = int(ecov_cnt[hd * kMaxEdges + ohit[u]]);
+                        ecov[size_t(hd * kMaxEdges + ohit[u]) * max_seqs + c] = uint16_t(s);
+                        ecov_cnt[hd * kMaxEdges + ohit[u]]                      = uint16_t(c + 1);
                     }
                 }
-            }
-            else
-            {
-                const int ic                   = int(g.in_cnt[curr]);
-                g.in_e[curr * kMaxEdges + ic]  = SizeT(head);
-                g.in_w[curr * kMaxEdges + ic]  = uint16_t(wsum);
-                g.in_cnt[curr]                 = uint16_t(ic + 1);
-                const int oc                   = int(g.out_cnt[head]);
-                g.out_e[head * kMaxEdges + oc] = SizeT(curr);
-                if (MSA)
+                else
                 {
-                    ecov_cnt[head * kMaxEdges + oc]                = 1;
-                    ecov[size_t(head * kMaxEdges + oc) * max_seqs] = uint16_t(s);
+                    g.in_e[cu * kMaxEdges + ic[u]] = SizeT(hd);
+                    g.in_w[cu * kMaxEdges + ic[u]] = uint16_t(wsum[u]);
+                    g.in_cnt[cu]                   = uint16_t(ic[u] + 1);
+                    g.out_e[hd * kMaxEdges + oc[u]] = SizeT(cu);
+                    if (MSA)
+                    {
+                        ecov_cnt[hd * kMaxEdges + oc[u]]                = 1;
+                        ecov[size_t(hd * kMaxEdges + oc[u]) * max_seqs] = uint16_t(s);
+                    }
+                    g.out_cnt[hd] = uint16_t(oc[u] + 1);
                 }
-                g.out_cnt[head] = uint16_t(oc + 1);
             }
+            g.cov[curr[u]] = uint16_t(cv[u] + 1);
         }
-        g.cov[curr]++;
     }
     node_count = nc0 + nnew;
     wave_sync();
@@ -709,9 +826,10 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
 #ifdef GWAMD_TOPSORT_PROFILE
     const uint64_t tp0 = __builtin_amdgcn_s_memtime();
 #endif
+    // info[n]: a dummy word the branch-free pop of a sink decrements
     GWAMD_LDS uint32_t* info  = (GWAMD_LDS uint32_t*)(scratch);
-    GWAMD_LDS uint16_t* queue = (GWAMD_LDS uint16_t*)(scratch + n * 4);
-    const int head_bytes      = (n * 6 + 15) & ~15;
+    GWAMD_LDS uint16_t* queue = (GWAMD_LDS uint16_t*)(scratch + (n + 1) * 4);
+    const int head_bytes      = ((n + 1) * 4 + (n + 1) * 2 + 15) & ~15;
     GWAMD_LDS uint16_t* edges = (GWAMD_LDS uint16_t*)(scratch + head_bytes);
     if (head_bytes > scratch_bytes || n > 65535 || n <= 0)
         return false;
@@ -771,7 +889,7 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
     // kQRing pushes: a pop at q reads the ring while tail - q <= kQRing, the
     // node word otherwise; the queue holds about the graph's width)
     constexpr int kQRing = 1024;
-    const int q_mode     = uniform(qinfo_off + n * 4 <= scratch_bytes ? 1 : (qinfo_off + kQRing * 4 <= scratch_bytes ? 2 : 0));
+    const int q_mode     = uniform(qinfo_off + (n + 1) * 4 <= scratch_bytes ? 1 : (qinfo_off + kQRing * 4 <= scratch_bytes ? 2 : 0));
     const bool use_q     = q_mode != 0;
     const uint32_t qmask = q_mode == 2 ? uint32_t(kQRing - 1) : 0xffffffffu;
     GWAMD_LDS uint32_t* qinfo    = (GWAMD_LDS uint32_t*)(scratch + qinfo_off);
@@ -798,12 +916,17 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
 #endif
     // FIFO (cudapoa_topsort.cuh:58-85), instantiated with and without the
     // queued info words so the loop carries no per-node mode test
+    if (lane == 0)
+        info[n] = 0xff000000u;
+    wave_sync();
     auto fifo = [&](auto useq_tag) -> int {
         constexpr int kMode = decltype(useq_tag)::value; // 0 node words, 1 all queued words, 2 ring
+        // (a VGPR value, made uniform where it is used, so the read stays in
+        // flight next to the pop's own successor read)
         auto pop_info = [&](int qq, int tl) -> uint32_t {
             if (kMode == 1 || (kMode == 2 && tl - qq <= kQRing))
-                return uint32_t(uniform(int(qinfo[uint32_t(qq) & (kMode == 2 ? uint32_t(kQRing - 1) : 0xffffffffu)])));
-            return uint32_t(uniform(int(info[int(queue[qq])])));
+                return qinfo[uint32_t(qq) & (kMode == 2 ? uint32_t(kQRing - 1) : 0xffffffffu)];
+            return info[int(queue[qq])];
         };
         int tail       = uniform(k);
         int q          = 0;
@@ -818,31 +941,30 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
             const int deg = int((vinfo >> 16) & 63u);
             // The word of the next queue entry, when it is queued already, is
             // final (a queued node is never decremented again), so its read is
-            // issued together with this pop's successor read: one LDS round
-            // trip per node where the graph is wide.  Otherwise the next node
-            // is the first one this pop releases (its word is in a register).
+            // issued together with this pop's successor read.  Otherwise the
+            // next node is the first one this pop releases.
             const bool have_next = q + 1 < tail;
             uint32_t nxt         = have_next ? pop_info(q + 1, tail) : 0u;
-            if (deg == 1)
+            if (deg <= 1)
             {
-                // single successor: release it when its in-degree reaches 0
-                // (a released node's word is not written back: nothing
-                // decrements it again and a pop uses only its degree and
+                // no or one successor, without branches: a sink decrements the
+                // dummy word info[n] and releases nothing; the queue / queued-
+                // word stores at `tail` only count when the successor is
+                // released (otherwise the slot is rewritten by the next push),
+                // and writing a released node's word back is harmless (nothing
+                // decrements it again, a pop reads only its degree and
                 // successor bits)
-                const int o       = int(vinfo & 0xffffu);
+                const int o       = deg == 1 ? int(vinfo & 0xffffu) : n;
                 const uint32_t oi = uint32_t(uniform(int(info[o]))) - (1u << 24);
-                if ((oi >> 24) == 0u)
-                {
-                    queue[tail] = uint16_t(o);
-                    if (kMode != 0 && have_next)
-                        qinfo[uint32_t(tail) & qmask] = oi;
-                    nxt = have_next ? nxt : oi;
-                    tail++;
-                }
-                else
-                    info[o] = oi;
+                const bool rel    = deg == 1 && (oi >> 24) == 0u;
+                info[o]           = oi;
+                queue[tail]       = uint16_t(o);
+                if (kMode != 0)
+                    qinfo[uint32_t(tail) & qmask] = oi;
+                nxt = have_next ? nxt : oi;
+                tail += rel ? 1 : 0;
             }
-            else if (deg >= 2)
+            else
             {
                 // all successors at once, one per lane: children are distinct,
                 // so the decrements are independent; ready ones are queued in
