@@ -508,10 +508,11 @@ private:
         const bool hm       = algo_ == GWAMD_ALIGNER_HIRSCHBERG_MYERS;
         // long mode: patterns in HBM, target codes through a generic pointer;
         // full Myers takes it past 8,192 x 65,535 (its stripes work either way)
-        long_mode_ = hm ? (max_q_ > gwamd::host::kHmShortQuery || max_t_ > gwamd::host::kHmShortTarget)
-                        : (max_q_ > 8192 || max_t_ > gwamd::host::kHmShortTarget);
-        if (!hm && std::getenv("GWAMD_MYERS_LONG")) // experiment: patterns in HBM at any size (less LDS per wave)
-            long_mode_ = std::atoi(std::getenv("GWAMD_MYERS_LONG")) != 0 || long_mode_;
+        // full Myers always: its patterns are read only when a stripe starts,
+        // and with them in HBM a wave needs ~4 KiB of LDS instead of ~10 KiB,
+        // so the occupancy query allows twice the waves (config D_myers:
+        // 353 -> 241 ms per 100k pairs, profiles/r3e_bench)
+        long_mode_ = hm ? (max_q_ > gwamd::host::kHmShortQuery || max_t_ > gwamd::host::kHmShortTarget) : true;
         // GWAMD_HM_STRIPE_BLOCKS=1..4 (parity tests): long mode at any size, with
         // stripes of that many blocks, so short pairs take the striped sweeps
         stripe_blocks_ = kMaxChunks;

@@ -1444,7 +1444,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
 #endif
 #ifdef GWAMD_BAND_PROFILE
             // counters over the phase slots (read raw: value = phase_ms * 1e5)
-            // backbone: traceback tile-staging cycles, add: path-flush cycles,
+            // backbone: traceback tile-staging cycles, add: sequential adds,
             // topsort: move-window refills, output: forward cycles, rowprog:
             // traceback steps, total: traceback cycles
             int64_t* ph8 = b.phase + size_t(w) * kPhases;
@@ -1466,7 +1466,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
             else
             {
             ph8[kPhBackbone] = int64_t(bp.v[kBpTileCyc]);
-            ph8[kPhAdd]      = int64_t(bp.v[kBpFlushCyc]);
+            ph8[kPhAdd]      = int64_t(bp.v[kBpAddSeq]); // reads added by the sequential add
             ph8[kPhTopsort]  = int64_t(bp.v[kBpRefill]);
             ph8[kPhOutput]   = int64_t(bp.v[kBpFwdCyc]);
             ph8[kPhRowProg]  = int64_t(bp.v[kBpSteps]);
