@@ -1383,7 +1383,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
                     AX.kind  = work + 4 * ls;
                     AX.owner = (GWAMD_LDS uint16_t*)(work + 5 * ls);
                     AX.sh    = (GWAMD_LDS int*)(shb);
-                    rc = add_alignment_parallel<SizeT, MSA>(g, nc, ag, ar, alen, L, lread, wts_g, s, ecov, ecovc,
+                    rc = add_alignment_parallel_batched<SizeT, MSA>(g, nc, ag, ar, alen, L, lread, wts_g, s, ecov, ecovc,
                                                             seq_begin, d.max_seqs, AX, lane);
                 }
             }

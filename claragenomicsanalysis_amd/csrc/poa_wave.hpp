@@ -491,6 +491,348 @@ __device__ __forceinline__ int add_alignment_parallel(WinGraph<SizeT> g, int& no
     return kSuccess;
 }
 
+// The same add with kAU = 4 read positions per lane and pass and their graph
+// loads issued together (one HBM round trip per dependent level instead of one
+// per position): used by the banded kernel, whose windows are long (config C:
+// 10 kb reads, 21 ms of adds per window before); the LDS full-alignment kernel
+// keeps the one-position form (the batched one raises its register count and
+// slows its forward pass).
+template <typename SizeT, bool MSA>
+__device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g, int& node_count, const SizeT* ag, const SizeT* ar,
+                                      int alen, int L, const uint8_t* read, const int8_t* w, int s, uint16_t* ecov,
+                                      uint16_t* ecov_cnt, SizeT* seq_begin, int max_seqs, const AddScratch& X,
+                                      int lane)
+{
+    g = as_global(g);
+    const int nc0 = node_count;
+    int err       = INT_MAX; // first error in read order: (pos << 8) | status
+    if (lane == 0)
+        X.sh[0] = 0;
+    for (int k = lane; k < alen; k += kWave)
+    {
+        const int rp = int(ar[k]);
+        if (rp >= 0 && rp < L)
+            X.gid[rp] = uint16_t(int(ag[k]) < 0 ? 0xffff : int(ag[k]));
+    }
+    wave_sync();
+    // kinds and existing targets.  kAU positions per lane and pass, their
+    // graph loads issued together (the graph is in HBM: one round trip per
+    // dependent level instead of one per position)
+    constexpr int kAU = 4;
+    for (int r0 = 0; r0 < L; r0 += kAU * kWave)
+    {
+        int gid[kAU], kind[kAU], curr[kAU], na[kAU], gb[kAU];
+        uint8_t rb[kAU];
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            const int rp = r0 + u * kWave + lane;
+            gid[u]       = rp < L ? int(X.gid[rp]) : 0xffff;
+            rb[u]        = rp < L ? read[rp] : uint8_t(0);
+        }
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            const bool has = gid[u] != 0xffff;
+            gb[u]          = has ? int(g.base[gid[u]]) : 0;
+            na[u]          = has ? int(g.aln_cnt[gid[u]]) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            kind[u] = gid[u] == 0xffff ? 2 : (gb[u] == int(rb[u]) ? 0 : 3);
+            curr[u] = kind[u] == 0 ? gid[u] : 0;
+        }
+        // aligned-node lists of the mismatching positions, 4 entries at a
+        // time: the first aligned node with the read's base (:130-150)
+        for (int n0 = 0;; n0 += 4)
+        {
+            bool need = false;
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+                need |= kind[u] == 3 && n0 < na[u];
+            if (__builtin_amdgcn_ballot_w64(need) == 0)
+                break;
+            int aid[kAU][4], ab[kAU][4];
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    aid[u][j] = (kind[u] == 3 && n0 + j < na[u]) ? int(g.aln[gid[u] * kMaxAlignments + n0 + j]) : -1;
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    ab[u][j] = aid[u][j] >= 0 ? int(g.base[aid[u][j]]) : -1;
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (kind[u] == 3 && aid[u][j] >= 0 && ab[u][j] == int(rb[u]))
+                        kind[u] = 1, curr[u] = aid[u][j];
+        }
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            const int rp = r0 + u * kWave + lane;
+            if (rp < L)
+            {
+                X.kind[rp] = uint8_t(kind[u]);
+                X.curr[rp] = uint16_t(curr[u]);
+            }
+        }
+    }
+    wave_sync();
+    // new node ids: prefix sum over new-node elements in read order
+    int nnew = 0;
+    for (int r0 = 0; r0 < L; r0 += kWave)
+    {
+        const int rp     = r0 + lane;
+        const bool isnew = rp < L && X.kind[rp] >= 2;
+        int total        = 0;
+        const int excl   = wave_excl_sum(isnew ? 1 : 0, lane, total);
+        if (isnew)
+        {
+            const int id = nc0 + nnew + excl;
+            X.curr[rp]   = uint16_t(id);
+            if (id + 1 >= g.max_nodes)
+                err = min(err, (rp << 8) | int(kNodeCountExceeded));
+        }
+        nnew += total;
+    }
+    wave_sync();
+    // independence checks without atomics: every element claims its node (and,
+    // for aligned hits / ring updates, its aligned group); after a barrier an
+    // element that no longer owns a claimed node has a conflicting partner.
+    for (int rp = lane; rp < L; rp += kWave)
+        X.owner[int(X.curr[rp])] = uint16_t(rp);
+    wave_sync();
+    bool conflict = false;
+    for (int rp = lane; rp < L; rp += kWave)
+        conflict |= int(X.owner[int(X.curr[rp])]) != rp;
+    wave_sync();
+    for (int rp = lane; rp < L; rp += kWave)
+    {
+        const int kind = X.kind[rp];
+        if (kind == 1 || kind == 3)
+        {
+            const int gid = int(X.gid[rp]);
+            X.owner[gid]  = uint16_t(rp);
+            const int na  = int(g.aln_cnt[gid]);
+            for (int n = 0; n < na; n++)
+                X.owner[int(g.aln[gid * kMaxAlignments + n])] = uint16_t(rp);
+        }
+    }
+    wave_sync();
+    for (int rp = lane; rp < L; rp += kWave)
+    {
+        const int kind = X.kind[rp];
+        if (kind == 1 || kind == 3)
+        {
+            const int gid = int(X.gid[rp]);
+            conflict |= int(X.owner[gid]) != rp;
+            const int na = int(g.aln_cnt[gid]);
+            for (int n = 0; n < na; n++)
+                conflict |= int(X.owner[int(g.aln[gid * kMaxAlignments + n])]) != rp;
+        }
+    }
+    if (conflict)
+        X.sh[0] = 1;
+    wave_sync();
+    if (X.sh[0])
+        return -1;
+    // edge existence and edge-limit errors (kAU positions per lane and pass)
+    for (int r0 = 1; r0 < L; r0 += kAU * kWave)
+    {
+        int head[kAU], curr[kAU], kind[kAU], ic[kAU], oc[kAU];
+        bool exists[kAU];
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            const int rp = r0 + u * kWave + lane;
+            const bool in = rp < L;
+            head[u]       = in ? int(X.curr[rp - 1]) : 0;
+            curr[u]       = in ? int(X.curr[rp]) : 0;
+            kind[u]       = in ? int(X.kind[rp]) : 2;
+            const int kp  = in ? int(X.kind[rp - 1]) & 3 : 2; // (bit 2 may be set by the previous pass)
+            ic[u]         = kind[u] < 2 ? int(g.in_cnt[curr[u]]) : 0;
+            oc[u]         = kp >= 2 ? 0 : int(g.out_cnt[head[u]]);
+            exists[u]     = false;
+        }
+        for (int e0 = 0;; e0 += 4)
+        {
+            bool need = false;
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+                need |= !exists[u] && e0 < ic[u];
+            if (__builtin_amdgcn_ballot_w64(need) == 0)
+                break;
+            int ie[kAU][4];
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    ie[u][j] = (!exists[u] && e0 + j < ic[u]) ? int(g.in_e[curr[u] * kMaxEdges + e0 + j]) : -1;
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    exists[u] |= ie[u][j] == head[u];
+        }
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            const int rp = r0 + u * kWave + lane;
+            if (rp >= L)
+                continue;
+            if (!exists[u])
+            {
+                if (oc[u] + 1 >= kMaxEdges || ic[u] + 1 >= kMaxEdges)
+                    err = min(err, (rp << 8) | int(kEdgeCountExceeded));
+            }
+            else
+                X.kind[rp] = uint8_t(kind[u] | 4);
+        }
+    }
+    err = -wave_max(-err); // wave-wide minimum
+    if (err != INT_MAX)
+        return err & 0xff;
+    wave_sync();
+    // writes 1: new nodes and aligned rings (one lane per element)
+    for (int rp = lane; rp < L; rp += kWave)
+    {
+        const int kind = X.kind[rp] & 3;
+        if (kind < 2)
+            continue;
+        const int curr  = int(X.curr[rp]);
+        g.base[curr]    = read[rp];
+        g.out_cnt[curr] = 0;
+        g.in_cnt[curr]  = 0;
+        g.aln_cnt[curr] = 0;
+        g.cov[curr]     = 0;
+        if (kind == 3)
+        {
+            const int gid = int(X.gid[rp]);
+            const int na  = int(g.aln_cnt[gid]);
+            int cnt       = 0;
+            for (int n = 0; n < na; n++)
+            {
+                const int aid                      = int(g.aln[gid * kMaxAlignments + n]);
+                const int ac                       = int(g.aln_cnt[aid]);
+                g.aln[aid * kMaxAlignments + ac]   = SizeT(curr);
+                g.aln_cnt[aid]                     = uint16_t(ac + 1);
+                g.aln[curr * kMaxAlignments + cnt] = SizeT(aid);
+                cnt++;
+            }
+            g.aln[gid * kMaxAlignments + na]   = SizeT(curr);
+            g.aln_cnt[gid]                     = uint16_t(na + 1);
+            g.aln[curr * kMaxAlignments + cnt] = SizeT(gid);
+            g.aln_cnt[curr]                    = uint16_t(cnt + 1);
+        }
+    }
+    wave_sync();
+    // writes 2: the edge head -> curr and the coverage of curr.  Element rp
+    // touches only curr's in-list and coverage and head's out-list (head =
+    // element rp-1's curr), so the elements are independent; kAU per lane and
+    // pass, with their loads issued together.
+    for (int r0 = 0; r0 < L; r0 += kAU * kWave)
+    {
+        int curr[kAU], head[kAU], kind[kAU], wsum[kAU], ic[kAU], oc[kAU], cv[kAU], hit[kAU], ohit[kAU];
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            const int rp = r0 + u * kWave + lane;
+            const bool in = rp < L;
+            curr[u]       = in ? int(X.curr[rp]) : 0;
+            head[u]       = (in && rp > 0) ? int(X.curr[rp - 1]) : 0;
+            kind[u]       = (in && rp > 0) ? int(X.kind[rp]) : -1; // -1: no edge (rp 0 or out of range)
+            wsum[u]       = (in && rp > 0) ? int(uint16_t(int(w[rp - 1]))) + int(w[rp]) : 0;
+            if (MSA && in && rp == 0)
+                seq_begin[s] = SizeT(curr[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            const int rp = r0 + u * kWave + lane;
+            ic[u]        = kind[u] >= 0 ? int(g.in_cnt[curr[u]]) : 0;
+            oc[u]        = (kind[u] >= 0 && (!(kind[u] & 4) || MSA)) ? int(g.out_cnt[head[u]]) : 0;
+            cv[u]        = rp < L ? int(g.cov[curr[u]]) : 0;
+            hit[u]       = -1;
+            ohit[u]      = -1;
+        }
+        // existing edges: their slot in curr's in-list (and, MSA, in head's out-list)
+        for (int e0 = 0;; e0 += 4)
+        {
+            bool need = false;
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+                need |= kind[u] >= 0 && (kind[u] & 4) && ((hit[u] < 0 && e0 < ic[u]) || (MSA && ohit[u] < 0 && e0 < oc[u]));
+            if (__builtin_amdgcn_ballot_w64(need) == 0)
+                break;
+            int ie[kAU][4], oe[kAU][4];
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                {
+                    const bool ex = kind[u] >= 0 && (kind[u] & 4);
+                    ie[u][j] = (ex && hit[u] < 0 && e0 + j < ic[u]) ? int(g.in_e[curr[u] * kMaxEdges + e0 + j]) : -1;
+                    oe[u][j] = (MSA && ex && ohit[u] < 0 && e0 + j < oc[u]) ? int(g.out_e[head[u] * kMaxEdges + e0 + j])
+                                                                             : -1;
+                }
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                {
+                    if (hit[u] < 0 && ie[u][j] >= 0 && ie[u][j] == head[u])
+                        hit[u] = e0 + j;
+                    if (MSA && ohit[u] < 0 && oe[u][j] >= 0 && oe[u][j] == curr[u])
+                        ohit[u] = e0 + j;
+                }
+        }
+#pragma unroll
+        for (int u = 0; u < kAU; u++)
+        {
+            const int rp = r0 + u * kWave + lane;
+            if (rp >= L)
+                continue;
+            if (kind[u] >= 0)
+            {
+                const int cu = curr[u], hd = head[u];
+                if (kind[u] & 4)
+                {
+                    if (hit[u] >= 0)
+                        g.in_w[cu * kMaxEdges + hit[u]] = uint16_t(int(g.in_w[cu * kMaxEdges + hit[u]]) + wsum[u]);
+                    if (MSA && ohit[u] >= 0)
+                    {
+                        const int c                                             = int(ecov_cnt[hd * kMaxEdges + ohit[u]]);
+                        ecov[size_t(hd * kMaxEdges + ohit[u]) * max_seqs + c] = uint16_t(s);
+                        ecov_cnt[hd * kMaxEdges + ohit[u]]                      = uint16_t(c + 1);
+                    }
+                }
+                else
+                {
+                    g.in_e[cu * kMaxEdges + ic[u]] = SizeT(hd);
+                    g.in_w[cu * kMaxEdges + ic[u]] = uint16_t(wsum[u]);
+                    g.in_cnt[cu]                   = uint16_t(ic[u] + 1);
+                    g.out_e[hd * kMaxEdges + oc[u]] = SizeT(cu);
+                    if (MSA)
+                    {
+                        ecov_cnt[hd * kMaxEdges + oc[u]]                = 1;
+                        ecov[size_t(hd * kMaxEdges + oc[u]) * max_seqs] = uint16_t(s);
+                    }
+                    g.out_cnt[hd] = uint16_t(oc[u] + 1);
+                }
+            }
+            g.cov[curr[u]] = uint16_t(cv[u] + 1);
+        }
+    }
+    node_count = nc0 + nnew;
+    wave_sync();
+    return kSuccess;
+}
+
 // racon/SPOA DFS sort (cudapoa_topsort.cuh:94-189) by one wave with the node
 // marks and the DFS stack in LDS: the predecessor and aligned-node lists of
 // the node on top of the stack are read one entry per lane, and the entries to
