@@ -508,11 +508,20 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
     int err       = INT_MAX; // first error in read order: (pos << 8) | status
     if (lane == 0)
         X.sh[0] = 0;
-    for (int k = lane; k < alen; k += kWave)
+    for (int k0 = 0; k0 < alen; k0 += 4 * kWave)
     {
-        const int rp = int(ar[k]);
-        if (rp >= 0 && rp < L)
-            X.gid[rp] = uint16_t(int(ag[k]) < 0 ? 0xffff : int(ag[k]));
+        int rp[4], gv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+        {
+            const int k = k0 + u * kWave + lane;
+            rp[u]       = k < alen ? int(ar[k]) : -1;
+            gv[u]       = k < alen ? int(ag[k]) : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (rp[u] >= 0 && rp[u] < L)
+                X.gid[rp[u]] = uint16_t(gv[u] < 0 ? 0xffff : gv[u]);
     }
     wave_sync();
     // kinds and existing targets.  kAU positions per lane and pass, their
@@ -611,30 +620,64 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
     for (int rp = lane; rp < L; rp += kWave)
         conflict |= int(X.owner[int(X.curr[rp])]) != rp;
     wave_sync();
-    for (int rp = lane; rp < L; rp += kWave)
+    // aligned groups of the mismatching positions: claim every member, then
+    // check the claims (kAU positions per lane, loads batched as above)
+    for (int pass = 0; pass < 2; pass++)
     {
-        const int kind = X.kind[rp];
-        if (kind == 1 || kind == 3)
+        for (int r0 = 0; r0 < L; r0 += kAU * kWave)
         {
-            const int gid = int(X.gid[rp]);
-            X.owner[gid]  = uint16_t(rp);
-            const int na  = int(g.aln_cnt[gid]);
-            for (int n = 0; n < na; n++)
-                X.owner[int(g.aln[gid * kMaxAlignments + n])] = uint16_t(rp);
+            int gid[kAU], na[kAU];
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+            {
+                const int rp   = r0 + u * kWave + lane;
+                const int kind = rp < L ? int(X.kind[rp]) : 0;
+                gid[u]         = (kind == 1 || kind == 3) ? int(X.gid[rp]) : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+                na[u] = gid[u] >= 0 ? int(g.aln_cnt[gid[u]]) : 0;
+#pragma unroll
+            for (int u = 0; u < kAU; u++)
+            {
+                const int rp = r0 + u * kWave + lane;
+                if (gid[u] < 0)
+                    continue;
+                if (pass == 0)
+                    X.owner[gid[u]] = uint16_t(rp);
+                else
+                    conflict |= int(X.owner[gid[u]]) != rp;
+            }
+            for (int n0 = 0;; n0 += 4)
+            {
+                bool need = false;
+#pragma unroll
+                for (int u = 0; u < kAU; u++)
+                    need |= n0 < na[u];
+                if (__builtin_amdgcn_ballot_w64(need) == 0)
+                    break;
+                int aid[kAU][4];
+#pragma unroll
+                for (int u = 0; u < kAU; u++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        aid[u][j] = n0 + j < na[u] ? int(g.aln[gid[u] * kMaxAlignments + n0 + j]) : -1;
+#pragma unroll
+                for (int u = 0; u < kAU; u++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                    {
+                        if (aid[u][j] < 0)
+                            continue;
+                        const int rp = r0 + u * kWave + lane;
+                        if (pass == 0)
+                            X.owner[aid[u][j]] = uint16_t(rp);
+                        else
+                            conflict |= int(X.owner[aid[u][j]]) != rp;
+                    }
+            }
         }
-    }
-    wave_sync();
-    for (int rp = lane; rp < L; rp += kWave)
-    {
-        const int kind = X.kind[rp];
-        if (kind == 1 || kind == 3)
-        {
-            const int gid = int(X.gid[rp]);
-            conflict |= int(X.owner[gid]) != rp;
-            const int na = int(g.aln_cnt[gid]);
-            for (int n = 0; n < na; n++)
-                conflict |= int(X.owner[int(g.aln[gid * kMaxAlignments + n])]) != rp;
-        }
+        wave_sync();
     }
     if (conflict)
         X.sh[0] = 1;
