@@ -761,8 +761,16 @@ def bench_stream(ctx, key, steps, warmup, args, with_cpu):
     alg_bytes = cells_total * 2 * 2 + 2 * int(read_lens.sum()) + 3 * int(clen.sum())
     busy_ms = busy_union_ms(launches["start_ms"], launches["stop_ms"])
     durations = launches["stop_ms"] - launches["start_ms"]
-    traffic, tsrc = load_traffic("poa", key, nwin)
+    # PMC HBM bytes per window of a profiled stream (scripts/summarize_profile.py, config E)
+    traffic, tsrc = None, None
+    try:
+        tf = json.load(open(os.path.join(ROOT, "profiles", "traffic_poa_E.json")))
+        traffic, tsrc = int(tf["hbm_bytes_per_window"] * nwin), tf.get("source")
+    except (OSError, ValueError, KeyError):
+        pass
     roof = roofline(alg_bytes, busy_ms, traffic, "poa_window_kernel_lds", tsrc, load_sq("poa_" + key))
+    if traffic:
+        roof["traffic_note"] = "PMC bytes per window of a profiled stream x this rank's windows"
     roof.update({"launches": int(len(durations)), "kernel_ms_sum": round(float(durations.sum()), 3),
                  "kernel_busy_ms": round(busy_ms, 3), "kernel_ms_mean_per_launch": round(float(durations.mean()), 3),
                  "windows_per_launch_mean": round(float(launches["windows"].mean()), 1),

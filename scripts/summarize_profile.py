@@ -36,8 +36,21 @@ def main(src, name, config="B", windows=1024, kernel="poa_window_kernel"):
             "hbm_bytes_per_launch": hbm,
             "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, KB per dispatch; "
                     "hbm bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024"}
+    if config == "E":
+        # config E streams many launches of varying size: bytes per window,
+        # summed over every dispatch of the profiled run
+        fsum = sum(vals["FETCH_SIZE"])
+        wsum = sum(vals["WRITE_SIZE"])
+        tot = int((2 * fsum + wsum) * 1024)
+        summ["hbm_bytes_all_dispatches"] = tot
+        summ["windows"] = windows
+        summ["hbm_bytes_per_window"] = tot / windows
     json.dump(summ, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
-    if kernel == "poa_window_kernel":
+    if config == "E":
+        json.dump({"config": config, "windows": windows, "hbm_bytes_per_window": tot / windows,
+                   "source": "profiles/" + name}, open(os.path.join(ROOT, "profiles", "traffic_poa_E.json"), "w"),
+                  indent=1)
+    elif kernel == "poa_window_kernel":
         json.dump({"config": config, "windows": windows, "hbm_bytes_per_launch": hbm, "source": "profiles/" + name},
                   open(os.path.join(ROOT, "profiles", "traffic_poa_%s.json" % config), "w"), indent=1)
     else:
