@@ -366,6 +366,28 @@ __device__ __forceinline__ void band_fetch(int p, int d, int r, const int (&Hp)[
             F[c] = __builtin_amdgcn_update_dpp(minv, Hp[c - 1], 0x130, 0xf, 0xf, false); // wave_shl:1
         return;
     }
+    if (CPL > 4 && (d % CPL) != 0)
+    {
+        // band shift not a multiple of the lane's CPL cells (CPL 8: shifts are
+        // multiples of 4): element-wise loads from position d + CPL*(lane+1) - 1
+        const int pos = min(d + CPL * (lane + 1), rowsz - CPL);
+        if (r - p < kBandRing)
+        {
+            const GWAMD_LDS ScoreT* q = ring + (p & (kBandRing - 1)) * rowsz + pos;
+#pragma unroll
+            for (int c = 0; c <= CPL; c++)
+                F[c] = int(q[c - 1]);
+        }
+        else
+        {
+            const ScoreT* q = spill + size_t(p) * rowsz + pos;
+#pragma unroll
+            for (int c = 0; c <= CPL; c++)
+                F[c] = int(q[c - 1]);
+            vm_drain();
+        }
+        return;
+    }
     const int gmax = rowsz / CPL - 1;
     const int gi   = min(d / CPL + lane + 1, gmax);
     if (r - p < kBandRing)
@@ -385,10 +407,19 @@ __device__ __forceinline__ void band_fetch(int p, int d, int r, const int (&Hp)[
 // predecessor loops.  Row records and read bytes are software-pipelined: the
 // record of row r+2 and the read bytes of row r+1 are requested while row r is
 // computed.
+template <int CPL>
+using ReadBytesT = typename std::conditional<(CPL > 4), uint64_t, uint32_t>::type;
+
 template <typename ScoreT, int CPL>
-__device__ __forceinline__ uint32_t band_read_bytes(GWAMD_LDS const uint8_t* read, int bs, int lane)
+__device__ __forceinline__ ReadBytesT<CPL> band_read_bytes(GWAMD_LDS const uint8_t* read, int bs, int lane)
 {
-    if constexpr (CPL == 4)
+    if constexpr (CPL == 8)
+    {
+        // band starts are multiples of 4: two aligned 4-byte reads
+        const GWAMD_LDS uint32_t* p = reinterpret_cast<GWAMD_LDS const uint32_t*>(read + bs + 8 * lane);
+        return uint64_t(p[0]) | (uint64_t(p[1]) << 32);
+    }
+    else if constexpr (CPL == 4)
         return *reinterpret_cast<GWAMD_LDS const uint32_t*>(read + bs + 4 * lane);
     else
         return uint32_t(*reinterpret_cast<GWAMD_LDS const uint16_t*>(read + bs + 2 * lane));
@@ -477,7 +508,7 @@ __device__ __forceinline__ int band_forward(WinGraph<SizeT> g, BandAux X, int V,
         uint32_t b1  = uint32_t(uniform(int(srec[4 * q1 + 1])));
         uint32_t c1  = uint32_t(uniform(int(srec[4 * q1 + 2])));
         uint32_t e1  = uint32_t(uniform(int(srec[4 * q1 + 3])));
-        uint32_t rbw = band_read_bytes<ScoreT, CPL>(read, ra_bs(a), lane);
+        ReadBytesT<CPL> rbw = band_read_bytes<ScoreT, CPL>(read, ra_bs(a), lane);
         bp.add(kBpStageCyc, BandProf::now() - st0);
         bp.add(kBpRows, uint64_t(rend - r0 + 1));
         for (int r = r0; r <= rend; r++)
@@ -488,7 +519,7 @@ __device__ __forceinline__ int band_forward(WinGraph<SizeT> g, BandAux X, int V,
             const uint32_t vb2 = srec[4 * q2 + 1];
             const uint32_t vc2 = srec[4 * q2 + 2];
             const uint32_t ve2 = srec[4 * q2 + 3];
-            const uint32_t rbn = band_read_bytes<ScoreT, CPL>(read, ra_bs(a1), lane);
+            const ReadBytesT<CPL> rbn = band_read_bytes<ScoreT, CPL>(read, ra_bs(a1), lane);
 
             const int bs = ra_bs(a);
             const int gb = ra_base(a);
@@ -745,7 +776,15 @@ __device__ __forceinline__ int band_forward(WinGraph<SizeT> g, BandAux X, int V,
             // store codes (one byte per cell)
             {
                 uint8_t* crow = X.codes + size_t(r) * bw + CPL * lane;
-                if constexpr (CPL == 4)
+                if constexpr (CPL == 8)
+                {
+                    uint64_t w8 = 0;
+#pragma unroll
+                    for (int c = 0; c < 8; c++)
+                        w8 |= uint64_t(uint8_t(code[c % CPL])) << (8 * c);
+                    *reinterpret_cast<uint64_t*>(crow) = w8;
+                }
+                else if constexpr (CPL == 4)
                 {
                     const uint32_t w4 = uint32_t(code[0]) | (uint32_t(code[1]) << 8) | (uint32_t(code[2]) << 16) |
                                         (uint32_t(code[3]) << 24);
@@ -1257,8 +1296,9 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
             B.max_column = sh_job[2] + 1;
             B.gradient   = __int_as_float(sh_job[3]);
             BandProf bp;
-            band_forward_ad<ScoreT, SizeT, CPL>(g, X, sh_job[1], (GWAMD_LDS const uint8_t*)(lread), sh_job[2], B, sc,
-                                                ring, spill, rowsz, d.score_rows, lane, wave, nw, adsh, bp);
+            if constexpr (CPL <= 4) // the anti-diagonal pass serves band widths 128 and 256
+                band_forward_ad<ScoreT, SizeT, CPL>(g, X, sh_job[1], (GWAMD_LDS const uint8_t*)(lread), sh_job[2], B,
+                                                    sc, ring, spill, rowsz, d.score_rows, lane, wave, nw, adsh, bp);
             __syncthreads(); // pass done
         }
         return;
@@ -1325,8 +1365,10 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
             ph.lap<kPhRowProg>();
             cells += int64_t(V + 1) * (d.band_width + kBandPad);
             int end_row;
-            if (d.band_ad && npmax <= kAdMaxSlots)
+            if (CPL <= 4 && d.band_ad && npmax <= kAdMaxSlots)
             {
+              if constexpr (CPL <= 4)
+              {
                 band_ad_init<ScoreT, CPL>(ring, rowsz, d.band_width, int(band_min_value<ScoreT>(sc)), adsh, lane);
                 if (nw > 1)
                 {
@@ -1349,6 +1391,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
                     status = kGenericError; // a progress wait ran out: the scores are not trustworthy
                     break;
                 }
+              }
             }
             else
                 end_row = band_forward<ScoreT, SizeT, CPL>(g, X, V, (GWAMD_LDS const uint8_t*)(lread), L, B, sc, ring,
@@ -1521,6 +1564,8 @@ extern "C" hipError_t gwamd_internal_poa_band_launch(const gwamd::poa::Buffers* 
         return hipGetLastError();                                                                             \
     }
 #define GWAMD_BAND_CPL(ST, ZT, MS)          \
+    if (d->lds_cpl == 8)                    \
+        GWAMD_BAND_LAUNCH(ST, ZT, MS, 8)    \
     if (d->lds_cpl == 4)                    \
         GWAMD_BAND_LAUNCH(ST, ZT, MS, 4)    \
     if (d->lds_cpl == 2)                    \
@@ -1564,6 +1609,8 @@ extern "C" int gwamd_internal_poa_band_blocks_per_cu(const gwamd::poa::Dims* d, 
         return n;                                                                                             \
     }
 #define GWAMD_BAND_OCC_CPL(ST, ZT, MS)     \
+    if (d->lds_cpl == 8)                   \
+        GWAMD_BAND_OCC(ST, ZT, MS, 8)      \
     if (d->lds_cpl == 4)                   \
         GWAMD_BAND_OCC(ST, ZT, MS, 4)      \
     if (d->lds_cpl == 2)                   \

@@ -696,7 +696,7 @@ private:
         if (env && std::string(env) == "v1")
             return;
         const int bw = dims_.band_width;
-        if ((bw != 128 && bw != 256) || gap_ > 0)
+        if ((bw != 128 && bw != 256 && bw != 512) || gap_ > 0)
             return;
         auto a16          = [](int64_t v) { return (v + 15) & ~int64_t(15); };
         const int cpl     = bw / 64;
@@ -716,7 +716,8 @@ private:
         // GWAMD_BAND_FWD=ad|row forces it on (planning for it) or off.
         const int64_t ad_b    = a16(int64_t(gwamd::poa::kAdRing) * rowsz * sbytes + gwamd::poa::kWave * sbytes);
         const char* fwd_env   = std::getenv("GWAMD_BAND_FWD");
-        const bool force_ad   = fwd_env && std::string(fwd_env) == "ad";
+        // (band widths 128 / 256 only: its ring of kAdRing rows is too large beyond)
+        const bool force_ad   = fwd_env && std::string(fwd_env) == "ad" && cpl <= 4;
         const bool no_ad      = fwd_env && std::string(fwd_env) == "row";
         const int64_t min_w   = std::max({ring_b, tile_b, flags_b, force_ad ? ad_b : int64_t(0)});
         const int64_t want_w  = std::max(min_w, add_b);
@@ -741,7 +742,7 @@ private:
         int ad_waves = gwamd::poa::kAdMaxWaves;
         if (const char* ev = std::getenv("GWAMD_BAND_AD_WAVES")) // diagnostic: fewer waves per window
             ad_waves = std::max(1, std::min(gwamd::poa::kAdMaxWaves, std::atoi(ev)));
-        dims_.band_ad        = (!no_ad && chosen_per_cu == 1 && work >= ad_b) ? ad_waves : 0;
+        dims_.band_ad        = (!no_ad && cpl <= 4 && chosen_per_cu == 1 && work >= ad_b) ? ad_waves : 0;
         dims_.tb_rank        = tb_rank_default();
         dims_.lds_cpl        = cpl;
         dims_.lds_waves      = 1;

@@ -101,7 +101,7 @@ def test_full_parity_int32_scores():
         assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage)
 
 
-@pytest.mark.parametrize("bw", [128, 256])
+@pytest.mark.parametrize("bw", [128, 256, 512])
 def test_banded_parity_synthetic(bw):
     wins = synth.poa_windows(21, 12, 600, 10, 30, 30, 30)
     max_seq = 700
@@ -262,7 +262,7 @@ def test_config_c_msa_10kb_banded_int32():
 
 
 @pytest.mark.parametrize("variant", ["v1", "band"])
-@pytest.mark.parametrize("bw", [128, 256])
+@pytest.mark.parametrize("bw", [128, 256, 512])
 def test_banded_kernel_variants(variant, bw, monkeypatch):
     # the banded kernel (codes + LDS ring) and the global-memory kernel agree
     # with the oracle, including reads much shorter than the band (every row
@@ -284,6 +284,22 @@ def test_banded_kernel_variants(variant, bw, monkeypatch):
     for i, w in enumerate(wins):
         r = run_oracle(w, 800, 10, banded=True, bw=bw, score_bits=sbits)
         assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), (variant, bw, i)
+
+
+@pytest.mark.parametrize("bw", [512])
+def test_banded_512_msa_int32_and_spoa(bw, monkeypatch):
+    # band width 512: the LDS band kernel with 8 cells per lane (row-parallel
+    # pass; predecessor band shifts of 4 take the element-wise fetch), int32
+    # scores, MSA and SPOA_ACCURATE, against the oracle
+    monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    wins = synth.poa_windows(711, 4, 1500, 8, 75, 75, 75)
+    for spoa in (False, True):
+        b = run_gpu(wins, 6000, 8, banded=True, bw=bw, output_type="msa", spoa_accurate=spoa)
+        assert b.kernel_variant() == 3 and b.get_types()[0] == 32
+        msa, st = b.get_msa()
+        for i, w in enumerate(wins):
+            r = run_oracle(w, 6000, 8, banded=True, bw=bw, msa=True, score_bits=32, spoa_accurate=spoa)
+            assert (st[i], msa[i]) == (r.status, r.msa), (spoa, i)
 
 
 def test_banded_kernel_msa_graph_int32(monkeypatch):
