@@ -38,6 +38,11 @@ namespace poa
 {
 
 constexpr int kBandRing  = 16; // LDS ring rows (power of two)
+#ifndef GWAMD_BAND_ADD_AU
+#define GWAMD_BAND_ADD_AU 8
+#endif
+// read positions per lane and pass of the add (one wave per SIMD: registers to spare)
+constexpr int kBandAddAU = GWAMD_BAND_ADD_AU;
 constexpr int kBandTile  = 64; // traceback tile rows
 constexpr uint32_t kNpEsc = 63;
 
@@ -168,18 +173,27 @@ __device__ __forceinline__ int band_np2(WinGraph<SizeT> g, int r, uint32_t a, ui
 
 // Row program of rows 1..V (after every topological sort).  Loads are batched
 // kRP rows per lane for memory-level parallelism; spill flags (a successor
-// reads the row from kBandRing or more rows later) are collected as LDS bytes
-// from the successor's side and folded into rec_a in a second pass.
+// reads the row from spill_dist or more rows later) are collected as LDS bytes
+// from the successor's side and folded into rec_a in a second pass; far flags
+// (a successor far_dist or more rows later: the anti-diagonal pass reads the
+// row from HBM) become bit 1 of X.flags.
 template <typename SizeT>
 __device__ __forceinline__ int band_row_program(WinGraph<SizeT> g, int V, const Band& B, BandAux X, int lane,
-                                 GWAMD_LDS uint8_t* flags, int spill_dist)
+                                 GWAMD_LDS uint8_t* flags, int spill_dist, int far_dist)
 {
     X = as_global(X);
     g = as_global(g);
     constexpr int kRP = 4;
+    GWAMD_LDS uint8_t* far = flags + ((V + 2 + 15) & ~15);
     for (int r = lane; r <= V + 1; r += kWave)
-        flags[r] = 0;
+        flags[r] = 0, far[r] = 0;
     wave_sync();
+    auto mark = [&](int p, int dist) {
+        if (dist >= spill_dist)
+            flags[p] = 1;
+        if (dist >= far_dist)
+            far[p] = 1;
+    };
     int xbase = 0;
     int npmax = 0; // largest predecessor count (returned, wave-uniform)
     static_assert(kRP * kWave == kStageRows, "one row-program pass per staged block");
@@ -238,22 +252,19 @@ __device__ __forceinline__ int band_row_program(WinGraph<SizeT> g, int V, const 
                     if (n >= 1)
                     {
                         bw = uint32_t(r - p0[u]);
-                        if (r - p0[u] >= spill_dist)
-                            flags[p0[u]] = 1;
+                        mark(p0[u], r - p0[u]);
                     }
                     if (n >= 2)
                     {
                         bw |= uint32_t(r - p1[u]) << 16;
-                        if (r - p1[u] >= spill_dist)
-                            flags[p1[u]] = 1;
+                        mark(p1[u], r - p1[u]);
                     }
                     if (n >= 3)
                     {
                         X.recc[r] = uint32_t(r - p2) | (uint32_t(r - p3) << 16);
-                        if (r - p2 >= spill_dist)
-                            flags[p2] = 1;
-                        if (n == 4 && r - p3 >= spill_dist)
-                            flags[p3] = 1;
+                        mark(p2, r - p2);
+                        if (n == 4)
+                            mark(p3, r - p3);
                     }
                 }
                 else
@@ -265,8 +276,7 @@ __device__ __forceinline__ int band_row_program(WinGraph<SizeT> g, int V, const 
                         const int pk = k == 0 ? p0[u] : (k == 1 ? p1[u] : pred_row(g, node[u], k));
                         if (fit)
                             X.xl[off + k] = pk;
-                        if (r - pk >= spill_dist)
-                            flags[pk] = 1;
+                        mark(pk, r - pk);
                     }
                     a |= (fit ? uint32_t(n) : kNpEsc) << 8;
                     bw = 0x80000000u | uint32_t(off);
@@ -289,7 +299,6 @@ __device__ __forceinline__ int band_row_program(WinGraph<SizeT> g, int V, const 
                 }
                 X.reca[r]  = a;
                 X.recb[r]  = bw;
-                X.flags[r] = 0; // set by the forward pass for rows it spills
             }
             xbase += total;
         }
@@ -298,9 +307,13 @@ __device__ __forceinline__ int band_row_program(WinGraph<SizeT> g, int V, const 
         X.bx[(V + kStageRows - 1) / kStageRows] = xbase;
     wave_sync();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    // X.flags bit 0 is set by the forward pass for the rows it spills
     for (int r = lane + 1; r <= V; r += kWave)
+    {
         if (flags[r])
             X.reca[r] |= 1u << 15;
+        X.flags[r] = far[r] ? 2 : 0;
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     wave_sync();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -1360,7 +1373,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
             B.gradient   = float(L + 1) / float(V + 1); // cudapoa_nw_banded.cuh:206
             // spill rows for successors kBandRing or more rows later: enough for
             // both forward passes (kAdSpillDist > kBandRing)
-            const int npmax = band_row_program<SizeT>(g, V, B, X, lane, work, kBandRing);
+            const int npmax = band_row_program<SizeT>(g, V, B, X, lane, work, kBandRing, kAdSpillDist);
             wave_sync();
             ph.lap<kPhRowProg>();
             cells += int64_t(V + 1) * (d.band_width + kBandPad);
@@ -1369,7 +1382,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
             {
               if constexpr (CPL <= 4)
               {
-                band_ad_init<ScoreT, CPL>(ring, rowsz, d.band_width, int(band_min_value<ScoreT>(sc)), adsh, lane);
+                band_ad_init<ScoreT, CPL>(ring, rowsz, d.band_width, int(band_min_value<ScoreT>(sc)), V, adsh, lane);
                 if (nw > 1)
                 {
                     if (lane == 0)
@@ -1426,7 +1439,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
                     AX.kind  = work + 4 * ls;
                     AX.owner = (GWAMD_LDS uint16_t*)(work + 5 * ls);
                     AX.sh    = (GWAMD_LDS int*)(shb);
-                    rc = add_alignment_parallel_batched<SizeT, MSA>(g, nc, ag, ar, alen, L, lread, wts_g, s, ecov, ecovc,
+                    rc = add_alignment_parallel_batched<SizeT, MSA, kBandAddAU>(g, nc, ag, ar, alen, L, lread, wts_g, s, ecov, ecovc,
                                                             seq_begin, d.max_seqs, AX, lane);
                 }
             }
@@ -1542,15 +1555,25 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
 } // namespace poa
 } // namespace gwamd
 
-// Launch of the banded kernel (called by gwamd_internal_poa_launch).
-extern "C" hipError_t gwamd_internal_poa_band_launch(const gwamd::poa::Buffers* b, const gwamd::poa::Dims* d,
-                                                     const gwamd::poa::Scores* sc, int score_bits, int size_bits,
-                                                     int msa, hipStream_t stream)
+// Launch and occupancy entry points of one band-width class: poa_band.hip is
+// compiled once per cells-per-lane value (poa_band_c2/c4/c8.hip define
+// GWAMD_BAND_TU_CPL) so the three instantiation sets build in parallel;
+// poa_band_dispatch.cpp picks the one the plan needs.
+#ifndef GWAMD_BAND_TU_CPL
+#error "poa_band.hip is built through poa_band_c2.hip, poa_band_c4.hip and poa_band_c8.hip"
+#endif
+#define GWAMD_BAND_CAT2(a, b) a##b
+#define GWAMD_BAND_CAT(a, b) GWAMD_BAND_CAT2(a, b)
+
+extern "C" hipError_t GWAMD_BAND_CAT(gwamd_internal_poa_band_launch_cpl, GWAMD_BAND_TU_CPL)(
+    const gwamd::poa::Buffers* b, const gwamd::poa::Dims* d, const gwamd::poa::Scores* sc, int score_bits,
+    int size_bits, int msa, hipStream_t stream)
 {
     using namespace gwamd::poa;
+    constexpr int CPL = GWAMD_BAND_TU_CPL;
     const dim3 grid(b->head ? b->num_slots : b->num_windows), blk(kWave * (d->band_ad ? d->band_ad : 1));
     const size_t lb = size_t(d->lds_bytes);
-#define GWAMD_BAND_LAUNCH(ST, ZT, MS, CPL)                                                                      \
+#define GWAMD_BAND_LAUNCH(ST, ZT, MS)                                                                           \
     {                                                                                                         \
         auto kfn = poa_window_kernel_band<ST, ZT, MS, CPL>;                                                   \
         if (lb > 65536)                                                                                       \
@@ -1563,20 +1586,12 @@ extern "C" hipError_t gwamd_internal_poa_band_launch(const gwamd::poa::Buffers* 
         hipLaunchKernelGGL(kfn, grid, blk, lb, stream, *b, *d, *sc);                                          \
         return hipGetLastError();                                                                             \
     }
-#define GWAMD_BAND_CPL(ST, ZT, MS)          \
-    if (d->lds_cpl == 8)                    \
-        GWAMD_BAND_LAUNCH(ST, ZT, MS, 8)    \
-    if (d->lds_cpl == 4)                    \
-        GWAMD_BAND_LAUNCH(ST, ZT, MS, 4)    \
-    if (d->lds_cpl == 2)                    \
-        GWAMD_BAND_LAUNCH(ST, ZT, MS, 2)    \
-    return hipErrorInvalidConfiguration;
 #define GWAMD_BAND_MSA(ST, ZT)              \
     if (msa)                                \
-    {                                       \
-        GWAMD_BAND_CPL(ST, ZT, true)        \
-    }                                       \
-    GWAMD_BAND_CPL(ST, ZT, false)
+        GWAMD_BAND_LAUNCH(ST, ZT, true)     \
+    GWAMD_BAND_LAUNCH(ST, ZT, false)
+    if (d->lds_cpl != CPL)
+        return hipErrorInvalidConfiguration;
     if (score_bits == 16)
     {
         GWAMD_BAND_MSA(int16_t, int16_t)
@@ -1587,16 +1602,17 @@ extern "C" hipError_t gwamd_internal_poa_band_launch(const gwamd::poa::Buffers* 
     }
     GWAMD_BAND_MSA(int32_t, int32_t)
 #undef GWAMD_BAND_MSA
-#undef GWAMD_BAND_CPL
 #undef GWAMD_BAND_LAUNCH
 }
 
 // Resident workgroups per CU of the planned banded kernel (persistent grid).
-extern "C" int gwamd_internal_poa_band_blocks_per_cu(const gwamd::poa::Dims* d, int score_bits, int size_bits, int msa)
+extern "C" int GWAMD_BAND_CAT(gwamd_internal_poa_band_blocks_per_cu_cpl, GWAMD_BAND_TU_CPL)(
+    const gwamd::poa::Dims* d, int score_bits, int size_bits, int msa)
 {
     using namespace gwamd::poa;
+    constexpr int CPL = GWAMD_BAND_TU_CPL;
     const size_t lb = size_t(d->lds_bytes);
-#define GWAMD_BAND_OCC(ST, ZT, MS, CPL)                                                                         \
+#define GWAMD_BAND_OCC(ST, ZT, MS)                                                                              \
     {                                                                                                         \
         auto kfn = poa_window_kernel_band<ST, ZT, MS, CPL>;                                                   \
         if (lb > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                             \
@@ -1608,20 +1624,12 @@ extern "C" int gwamd_internal_poa_band_blocks_per_cu(const gwamd::poa::Dims* d, 
             return 0;                                                                                         \
         return n;                                                                                             \
     }
-#define GWAMD_BAND_OCC_CPL(ST, ZT, MS)     \
-    if (d->lds_cpl == 8)                   \
-        GWAMD_BAND_OCC(ST, ZT, MS, 8)      \
-    if (d->lds_cpl == 4)                   \
-        GWAMD_BAND_OCC(ST, ZT, MS, 4)      \
-    if (d->lds_cpl == 2)                   \
-        GWAMD_BAND_OCC(ST, ZT, MS, 2)      \
-    return 0;
 #define GWAMD_BAND_OCC_MSA(ST, ZT)         \
     if (msa)                               \
-    {                                      \
-        GWAMD_BAND_OCC_CPL(ST, ZT, true)   \
-    }                                      \
-    GWAMD_BAND_OCC_CPL(ST, ZT, false)
+        GWAMD_BAND_OCC(ST, ZT, true)       \
+    GWAMD_BAND_OCC(ST, ZT, false)
+    if (d->lds_cpl != CPL)
+        return 0;
     if (score_bits == 16)
     {
         GWAMD_BAND_OCC_MSA(int16_t, int16_t)
@@ -1632,6 +1640,7 @@ extern "C" int gwamd_internal_poa_band_blocks_per_cu(const gwamd::poa::Dims* d, 
     }
     GWAMD_BAND_OCC_MSA(int32_t, int32_t)
 #undef GWAMD_BAND_OCC_MSA
-#undef GWAMD_BAND_OCC_CPL
 #undef GWAMD_BAND_OCC
 }
+#undef GWAMD_BAND_CAT
+#undef GWAMD_BAND_CAT2

@@ -14,7 +14,9 @@
 //     writes as it goes; a predecessor k >= 2 rows back wrote column c+1 k
 //     steps before it is needed, so its LDS read is issued one step ahead;
 //   * predecessors more than kWave rows before the block are read from the
-//     HBM spill rows, which this pass writes for every row.
+//     HBM spill rows, which this pass writes for the rows with such a
+//     successor (far rows, X.flags bit 1 from the row program) and for the
+//     rows the traceback's out-of-band step may read (below).
 // Per-row control (record decoding, predecessor lists) happens once per block
 // and lane, not once per row for the whole wave.
 //
@@ -74,6 +76,8 @@ struct AdCtx
     int lane, r, r0, V, L, bw, gap, match, mismatch, minv, cs, T, bs, base, np;
     int blk, delta; // block index; steps block blk-1 must lead by (0: no wait)
     bool act;
+    bool store;     // the lane's row goes to the spill rows
+    bool any_store; // some row of the block does (block-uniform)
     uint32_t a, b, c2;
     GWAMD_LDS const uint8_t* read;
     GWAMD_LDS ScoreT* ring;
@@ -135,7 +139,8 @@ __device__ __forceinline__ void ad_publish(GWAMD_LDS AdShared* sh, int blk, uint
 }
 
 // One block of rows; NS predecessor slots per lane, GEN: general step.
-// Returns the lane's emission at column L (its row's sink candidate).
+// Returns the lane's emission at column L (its row's sink candidate).  Rows
+// with C.store set also go to the HBM spill rows (see band_forward_ad).
 template <typename ScoreT, typename SizeT, int CPL, int NS, bool GEN>
 __device__ __forceinline__ int ad_block(const AdCtx<ScoreT>& C, WinGraph<SizeT> g, BandAux X)
 {
@@ -204,6 +209,8 @@ __device__ __forceinline__ int ad_block(const AdCtx<ScoreT>& C, WinGraph<SizeT> 
     const uint32_t soff = C.act ? uint32_t(sizeof(ScoreT)) * uint32_t(r * C.rowsz + k0 + CPL - 1) : 0u;
     const int base = C.base;
     const bool act = C.act;
+    const bool store     = C.act && C.store;
+    const bool any_store = C.any_store;
     const int T    = uniform(C.T);
     const int tL   = C.L - C.cs + lane; // step of column L
     // per-lane copies: keeps the step loop free of scalar reloads
@@ -343,8 +350,9 @@ __device__ __forceinline__ int ad_block(const AdCtx<ScoreT>& C, WinGraph<SizeT> 
             e = cell ? H : minv; // idx 0 is minv: every row of a fast block has band start > 0
         *(row ? wp + t : dw) = ScoreT(e);
         codes[cell ? uint32_t(coff + t) : uint32_t(lane)] = uint8_t(code);
-        *reinterpret_cast<ScoreT*>(spillb + (row ? soff + uint32_t(sizeof(ScoreT) * t)
-                                                 : uint32_t(sizeof(ScoreT) * lane))) = ScoreT(e);
+        if (any_store)
+            *reinterpret_cast<ScoreT*>(spillb + (row && store ? soff + uint32_t(sizeof(ScoreT) * t)
+                                                               : uint32_t(sizeof(ScoreT) * lane))) = ScoreT(e);
         sv  = t == tL ? e : sv;
         cur = e;
         }
@@ -354,13 +362,24 @@ __device__ __forceinline__ int ad_block(const AdCtx<ScoreT>& C, WinGraph<SizeT> 
 
 // Ring padding (idx bw+1 ..) and the progress words; run by one wave before
 // the pass.
+// Real-row bitmap of the pass (bit r: row r is real, see band_forward_ad),
+// after the ring and the sink words.
+template <typename ScoreT>
+__device__ __forceinline__ GWAMD_LDS uint32_t* ad_real_bits(GWAMD_LDS ScoreT* ring, int rowsz)
+{
+    return (GWAMD_LDS uint32_t*)(ring + kAdRing * rowsz + kWave);
+}
+
 template <typename ScoreT, int CPL>
-__device__ __forceinline__ void band_ad_init(GWAMD_LDS ScoreT* ring, int rowsz, int bw, int minv,
+__device__ __forceinline__ void band_ad_init(GWAMD_LDS ScoreT* ring, int rowsz, int bw, int minv, int V,
                                              GWAMD_LDS AdShared* sh, int lane)
 {
     for (int k = lane; k < kAdRing * rowsz; k += kWave)
         if (k % rowsz >= bw + CPL)
             ring[k] = ScoreT(minv);
+    GWAMD_LDS uint32_t* rbits = ad_real_bits(ring, rowsz);
+    for (int k = lane; k <= V / 32; k += kWave)
+        rbits[k] = 0;
     if (lane < kAdProg)
         sh->prog[lane] = -1;
     if (lane == 0)
@@ -370,6 +389,30 @@ __device__ __forceinline__ void band_ad_init(GWAMD_LDS ScoreT* ring, int rowsz, 
 
 // Blocks wave, wave + nw, ... of the pass.  Each wave leaves its first
 // strictly greatest sink candidate in sh->best / sh->end_row.
+//
+// Spill rows.  Far rows (a successor kAdSpillDist or more rows later, X.flags
+// bit 1 from the row program) are stored for this pass's own far reads.  The
+// traceback's out-of-band step (band_get_slow) compares min_score_value with a
+// neighbour plus match, mismatch or gap, so it can only match values <= Tmax =
+// max(minv - match, minv - mismatch, minv - gap); a row without such values
+// may stay out of HBM (X.flags bit 0 clear: the step then knows none of its
+// values matches).  A row is *real* when every in-band cell has a candidate
+// that descends, cell by cell, from the boundary values (row 0: idx * gap,
+// column 0) rather than from min_score_value:
+//   * a row with band start 0 (its column-0 value is real and every cell has
+//     the horizontal candidate), or with only the virtual row 0 as
+//     predecessor and band start < bw, is real;
+//   * so is a row with a real predecessor whose band covers the row's first
+//     cell (shift = band start difference < bw: the vertical candidate of
+//     index 1 reads the predecessor's in-band index shift + 1; later cells
+//     have the horizontal one).
+// Real values are >= min(gap, mismatch, 0) * (2V + L + bw + 16), and with no
+// positive wrap of the score type (max(match, 0) * (V + L + 16) in range) that
+// bound above Tmax means a real row holds no value <= Tmax.  When the bound
+// fails every row is stored.  Realness is decided at block setup from the
+// predecessors (bitmap in LDS; in-block predecessors are assumed real and the
+// assumption checked: if a lane fails, a fixed point over the block decides)
+// and published before the block's first progress word.
 template <typename ScoreT, typename SizeT, int CPL>
 __device__ __forceinline__ void band_forward_ad(WinGraph<SizeT> g, BandAux X, int V, GWAMD_LDS const uint8_t* read,
                                                 int L, const Band& B, const Scores sc, GWAMD_LDS ScoreT* ring,
@@ -401,6 +444,16 @@ __device__ __forceinline__ void band_forward_ad(WinGraph<SizeT> g, BandAux X, in
     C.codes_bytes = score_rows * bw;
     C.spill_bytes = score_rows * rowsz * int(sizeof(ScoreT));
     C.sh          = sh;
+    GWAMD_LDS uint32_t* rbits = ad_real_bits(ring, rowsz);
+    auto rbit = [&](int p) -> bool { return (rbits[p >> 5] >> (p & 31)) & 1u; };
+    // the real-value bound (see above); fails: every row is stored
+    bool store_all;
+    {
+        const int64_t tmax = max(max(minv - sc.match, minv - sc.mismatch), minv - sc.gap);
+        const int64_t lo   = int64_t(min(min(sc.gap, sc.mismatch), 0)) * (2 * int64_t(V) + L + bw + 16);
+        const int64_t hi   = int64_t(max(sc.match, 0)) * (int64_t(V) + L + 16);
+        store_all          = !(lo > tmax && hi < (sizeof(ScoreT) == 2 ? int64_t(INT16_MAX) : int64_t(INT32_MAX)));
+    }
     int best = INT_MIN, end_row = 0;
     for (int blk = wave; blk * kWave + 1 <= V; blk += nw)
     {
@@ -419,6 +472,7 @@ __device__ __forceinline__ void band_forward_ad(WinGraph<SizeT> g, BandAux X, in
         C.bs         = ra_bs(C.a);
         C.base       = ra_base(C.a);
         C.np         = a ? band_np2<SizeT>(g, rr, C.a, C.b) : 0;
+        const bool far = a && (X.flags[rr] & 2) != 0;
         C.cs         = uniform(C.bs); // lane 0 is always a row
         const int last = min(kWave - 1, V - r0);
         const int bsl  = __builtin_amdgcn_readlane(C.bs, last);
@@ -430,10 +484,16 @@ __device__ __forceinline__ void band_forward_ad(WinGraph<SizeT> g, BandAux X, in
             const int cs_prev = ra_bs(uint32_t(uniform(int(X.reca[r0 - kWave]))));
             C.delta           = C.cs - cs_prev + kWave + 1;
         }
-        // block-uniform dispatch: slot count and fast / general step
-        const int ns = uniform(wave_max(a ? max(C.np, 1) : 1));
-        bool gen     = !a ? false : (C.bs == 0 || C.np == 0);
-        if (!gen && a && C.np <= 8)
+        // block-uniform dispatch: slot count and fast / general step; with
+        // the same predecessor scan, the real-row test (earlier blocks' bits
+        // are final once block blk-1 has published its first word)
+        if (blk > 0 && nw > 1)
+            ad_wait(sh, blk - 1, 0);
+        const int ns  = uniform(wave_max(a ? max(C.np, 1) : 1));
+        bool gen      = !a ? false : (C.bs == 0 || C.np == 0);
+        const bool rb = !a || C.bs == 0 || (C.np == 0 && C.bs < bw);
+        bool rl       = rb;
+        if (a)
         {
             for (int s = 0; s < C.np; s++)
             {
@@ -441,9 +501,40 @@ __device__ __forceinline__ void band_forward_ad(WinGraph<SizeT> g, BandAux X, in
                 const int bsp = ra_bs(X.reca[p]);
                 if (C.bs - bsp > 4 || (p < r0 - kWave))
                     gen = true;
+                if (C.bs - bsp < bw && (p >= r0 || rbit(p)))
+                    rl = true;
             }
         }
         gen = __builtin_amdgcn_ballot_w64(gen || (a && C.np > 8)) != 0;
+        if (__builtin_amdgcn_ballot_w64(!rl) != 0)
+        {
+            // some row has no real predecessor outside the block and no base
+            // case: decide the block exactly, bits of earlier rounds only
+            rl = rb;
+            for (int it = 0; it <= kWave; it++)
+            {
+                if (a && rl)
+                    __hip_atomic_fetch_or(&rbits[r >> 5], 1u << (r & 31), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+                wave_sync();
+                bool nr = rl;
+                if (a && !rl)
+                    for (int s = 0; s < C.np; s++)
+                    {
+                        const int p = band_pred2<SizeT>(g, X, r, C.a, C.b, C.c2, s);
+                        if (C.bs - ra_bs(X.reca[p]) < bw && rbit(p))
+                            nr = true;
+                    }
+                if (__builtin_amdgcn_ballot_w64(nr && !rl) == 0)
+                    break;
+                rl = nr;
+            }
+        }
+        if (a && rl)
+            __hip_atomic_fetch_or(&rbits[r >> 5], 1u << (r & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        ad_publish(sh, blk, 0, lane); // setup done: this block's bits are out
+        C.store     = a && (far || !rl || store_all);
+        C.any_store = __builtin_amdgcn_ballot_w64(C.store) != 0;
         const uint64_t l_t0 = BandProf::now();
         bp.add(kBpAdSetup, l_t0 - s_t0);
         bp.add(kBpAdBlocks, 1);
@@ -494,7 +585,7 @@ __device__ __forceinline__ void band_forward_ad(WinGraph<SizeT> g, BandAux X, in
             end_row            = r0 + int(__builtin_ctzll(hit));
         }
         if (a)
-            X.flags[r] = 1; // every row is in the spill rows
+            X.flags[r] = C.store ? 1 : 0; // bit 0: the row is in the spill rows
         bp.add(kBpRows, uint64_t(last + 1));
         bp.add(kBpMulti, gen ? 1 : 0);
     }

@@ -708,13 +708,14 @@ private:
         const int64_t ring_b  = a16(int64_t(16) * rowsz * sbytes) + 4 * 256 * 4 + 1024 * 4; // + record staging
         const int64_t tile_b  = a16(int64_t(64) * bw + 64 * 16 + 512 + gwamd::poa::kTbRankBytes); // codes +
                                                                       // per-row decode info + walk tables
-        const int64_t flags_b = a16(mn + 2);
+        const int64_t flags_b = 2 * a16(mn + 2); // row program: spill and far flags
         const int64_t add_b   = 5 * a16(ms + 16) + 2 * (mn + ms + 16) + 16;
         // anti-diagonal forward pass (poa_band_ad.hpp): a kAdRing-row ring and
         // one dummy word per lane.  Default: whenever the windows-per-CU
         // choice below leaves room for it (large windows, one or two per CU);
         // GWAMD_BAND_FWD=ad|row forces it on (planning for it) or off.
-        const int64_t ad_b    = a16(int64_t(gwamd::poa::kAdRing) * rowsz * sbytes + gwamd::poa::kWave * sbytes);
+        const int64_t ad_b    = a16(int64_t(gwamd::poa::kAdRing) * rowsz * sbytes + gwamd::poa::kWave * sbytes) +
+                             a16(mn / 8 + 64); // + the real-row bitmap
         const char* fwd_env   = std::getenv("GWAMD_BAND_FWD");
         // (band widths 128 / 256 only: its ring of kAdRing rows is too large beyond)
         const bool force_ad   = fwd_env && std::string(fwd_env) == "ad" && cpl <= 4;

@@ -491,13 +491,13 @@ __device__ __forceinline__ int add_alignment_parallel(WinGraph<SizeT> g, int& no
     return kSuccess;
 }
 
-// The same add with kAU = 4 read positions per lane and pass and their graph
+// The same add with kAU read positions per lane and pass and their graph
 // loads issued together (one HBM round trip per dependent level instead of one
 // per position): used by the banded kernel, whose windows are long (config C:
 // 10 kb reads, 21 ms of adds per window before); the LDS full-alignment kernel
 // keeps the one-position form (the batched one raises its register count and
 // slows its forward pass).
-template <typename SizeT, bool MSA>
+template <typename SizeT, bool MSA, int kAU = 4>
 __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g, int& node_count, const SizeT* ag, const SizeT* ar,
                                       int alen, int L, const uint8_t* read, const int8_t* w, int s, uint16_t* ecov,
                                       uint16_t* ecov_cnt, SizeT* seq_begin, int max_seqs, const AddScratch& X,
@@ -527,7 +527,6 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
     // kinds and existing targets.  kAU positions per lane and pass, their
     // graph loads issued together (the graph is in HBM: one round trip per
     // dependent level instead of one per position)
-    constexpr int kAU = 4;
     for (int r0 = 0; r0 < L; r0 += kAU * kWave)
     {
         int gid[kAU], kind[kAU], curr[kAU], na[kAU], gb[kAU];
