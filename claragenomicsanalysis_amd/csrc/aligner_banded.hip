@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include "aligner_common.hpp"
+#include <type_traits>
 #include "aligner_device.hpp"
 
 namespace gwamd
@@ -318,11 +319,14 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                 // its state in LDS between columns; bands wider than the LDS
                 // region (long queries) read the previous column's state back
                 // from the band matrix in HBM, with a workgroup fence per column
-                const bool lds_state = nwb <= TLE;
+                // (two instantiations: with the state in LDS the sweep never
+                // loads from the band matrix, so its stores need no waits)
+                auto sweep = [&](auto lds_tag) -> int {
+                constexpr bool lds_state = decltype(lds_tag)::value;
                 for (int w = lane; w < nwb; w += kWave)
                 {
                     const BandEntry e0{~0u, 0u, min((w + 1) * kWordBits, bw), 0};
-                    if (lds_state)
+                    if constexpr (lds_state)
                         lds_put(reg + w, e0);
                     E[w] = e0;
                 }
@@ -340,7 +344,7 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                         const bool valid   = lane < kChunkWords && w < nwb;
                         const uint64_t act = ballot(valid);
                         BandEntry e;
-                        if (lds_state)
+                        if constexpr (lds_state)
                             e = lds_get(reg + (valid ? w : 0));
                         else
                             e = E[size_t(t - 1) * nwb + (valid ? w : 0)];
@@ -365,8 +369,11 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                             {
                                 // word 31 takes bit 0 of the next chunk's first word,
                                 // still the previous column's (:567-573)
-                                const BandEntry nx = lds_state ? lds_get(reg + (c + 1) * kChunkWords)
-                                                               : E[size_t(t - 1) * nwb + (c + 1) * kChunkWords];
+                                BandEntry nx;
+                                if constexpr (lds_state)
+                                    nx = lds_get(reg + (c + 1) * kChunkWords);
+                                else
+                                    nx = E[size_t(t - 1) * nwb + (c + 1) * kChunkWords];
                                 if (lane == kChunkWords - 1)
                                 {
                                     p2 |= (nx.pv & 1u) << 31;
@@ -392,12 +399,12 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                         if (valid)
                         {
                             const BandEntry o{pv, mv, sc, 0};
-                            if (lds_state)
+                            if constexpr (lds_state)
                                 lds_put(reg + w, o);
                             E[size_t(t) * nwb + w] = o;
                         }
                     }
-                    if (!lds_state)
+                    if constexpr (!lds_state)
                     {
                         // this column's entries before the next column reads them
                         __threadfence_block();
@@ -406,7 +413,12 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                 }
                 __threadfence_block();
                 wave_sync();
-                ed = lds_state ? uni(lds_get(reg + lastw).sc) : uni(E[size_t(T) * nwb + lastw].sc);
+                if constexpr (lds_state)
+                    return uni(lds_get(reg + lastw).sc);
+                else
+                    return uni(E[size_t(T) * nwb + lastw].sc);
+                };
+                ed = nwb <= TLE ? sweep(std::true_type{}) : sweep(std::false_type{});
             }
             if (ed <= est || bw == Q)
                 break;

@@ -39,7 +39,7 @@ namespace poa
 
 constexpr int kBandRing  = 16; // LDS ring rows (power of two)
 #ifndef GWAMD_BAND_ADD_AU
-#define GWAMD_BAND_ADD_AU 8
+#define GWAMD_BAND_ADD_AU 4
 #endif
 // read positions per lane and pass of the add (one wave per SIMD: registers to spare)
 constexpr int kBandAddAU = GWAMD_BAND_ADD_AU;
@@ -1336,6 +1336,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
     PhaseTimer ph;
     BandProf bp;
     uint64_t tsprof[4] = {0, 0, 0, 0}; // topsort sections (GWAMD_TOPSORT_PROFILE builds)
+    uint64_t addprof[8] = {0, 0, 0, 0, 0, 0, 0, 0}; // add sections (GWAMD_ADD_PROFILE builds)
     const WindowDesc wd = b.windows[w];
     const int nseq      = wd.num_seqs;
     int status          = kSuccess;
@@ -1440,7 +1441,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
                     AX.owner = (GWAMD_LDS uint16_t*)(work + 5 * ls);
                     AX.sh    = (GWAMD_LDS int*)(shb);
                     rc = add_alignment_parallel_batched<SizeT, MSA, kBandAddAU>(g, nc, ag, ar, alen, L, lread, wts_g, s, ecov, ecovc,
-                                                            seq_begin, d.max_seqs, AX, lane);
+                                                            seq_begin, d.max_seqs, AX, lane, addprof);
                 }
             }
             if (rc < 0)
@@ -1492,6 +1493,13 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
         if (b.phase)
         {
             ph.store(b.phase + size_t(w) * kPhases);
+#ifdef GWAMD_ADD_PROFILE
+            // add sections over all 8 slots (s_memtime cycles / 1000): gid fill,
+            // kinds, new ids, node claims, group claims, edge existence,
+            // writes 1, writes 2
+            for (int k = 0; k < 8; k++)
+                b.phase[size_t(w) * kPhases + k] = int64_t(addprof[k] / 1000);
+#endif
 #ifdef GWAMD_TOPSORT_PROFILE
             b.phase[size_t(w) * kPhases + kPhBackbone] = int64_t(tsprof[0] / 1000);
             b.phase[size_t(w) * kPhases + kPhAdd]      = int64_t(tsprof[1] / 1000);

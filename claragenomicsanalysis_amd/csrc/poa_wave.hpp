@@ -271,6 +271,69 @@ struct AddScratch
     GWAMD_LDS int* sh;         // [0] conflict
 };
 
+// writes 1 of the wave-parallel add: new nodes and aligned rings, one lane
+// per new element.  The new elements' positions are first compacted into the
+// owner array (free once the independence checks are done), so a 10 kb read
+// with ~1,000 new nodes takes ~16 lane-parallel rounds instead of one per 64
+// read positions; a ring's member loads are issued 4 at a time.
+template <typename SizeT>
+__device__ __forceinline__ void add_write_new_nodes(WinGraph<SizeT> g, const AddScratch& X, int L,
+                                                    const uint8_t* read, int lane)
+{
+    GWAMD_LDS uint16_t* newpos = X.owner;
+    int k = 0;
+    for (int r0 = 0; r0 < L; r0 += kWave)
+    {
+        const int rp     = r0 + lane;
+        const bool isnew = rp < L && (X.kind[rp] & 3) >= 2;
+        int total        = 0;
+        const int ex     = wave_excl_sum(isnew ? 1 : 0, lane, total);
+        if (isnew)
+            newpos[k + ex] = uint16_t(rp);
+        k += total;
+    }
+    wave_sync();
+    for (int i = lane; i < k; i += kWave)
+    {
+        const int rp    = int(newpos[i]);
+        const int kind  = X.kind[rp] & 3;
+        const int curr  = int(X.curr[rp]);
+        g.base[curr]    = read[rp];
+        g.out_cnt[curr] = 0;
+        g.in_cnt[curr]  = 0;
+        g.aln_cnt[curr] = 0;
+        g.cov[curr]     = 0;
+        if (kind == 3)
+        {
+            const int gid = int(X.gid[rp]);
+            const int na  = int(g.aln_cnt[gid]);
+            for (int n0 = 0; n0 < na; n0 += 4)
+            {
+                int aid[4], ac[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    aid[j] = n0 + j < na ? int(g.aln[gid * kMaxAlignments + n0 + j]) : 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    ac[j] = n0 + j < na ? int(g.aln_cnt[aid[j]]) : 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (n0 + j < na)
+                    {
+                        g.aln[aid[j] * kMaxAlignments + ac[j]] = SizeT(curr);
+                        g.aln_cnt[aid[j]]                      = uint16_t(ac[j] + 1);
+                        g.aln[curr * kMaxAlignments + n0 + j]  = SizeT(aid[j]);
+                    }
+            }
+            g.aln[gid * kMaxAlignments + na]   = SizeT(curr);
+            g.aln_cnt[gid]                     = uint16_t(na + 1);
+            g.aln[curr * kMaxAlignments + na]  = SizeT(gid);
+            g.aln_cnt[curr]                    = uint16_t(na + 1);
+        }
+    }
+    wave_sync();
+}
+
 template <typename SizeT, bool MSA>
 __device__ __forceinline__ int add_alignment_parallel(WinGraph<SizeT> g, int& node_count, const SizeT* ag, const SizeT* ar,
                                       int alen, int L, const uint8_t* read, const int8_t* w, int s, uint16_t* ecov,
@@ -404,39 +467,7 @@ __device__ __forceinline__ int add_alignment_parallel(WinGraph<SizeT> g, int& no
     if (err != INT_MAX)
         return err & 0xff;
     wave_sync();
-    // writes 1: new nodes and aligned rings (one lane per element)
-    for (int rp = lane; rp < L; rp += kWave)
-    {
-        const int kind = X.kind[rp] & 3;
-        if (kind < 2)
-            continue;
-        const int curr  = int(X.curr[rp]);
-        g.base[curr]    = read[rp];
-        g.out_cnt[curr] = 0;
-        g.in_cnt[curr]  = 0;
-        g.aln_cnt[curr] = 0;
-        g.cov[curr]     = 0;
-        if (kind == 3)
-        {
-            const int gid = int(X.gid[rp]);
-            const int na  = int(g.aln_cnt[gid]);
-            int cnt       = 0;
-            for (int n = 0; n < na; n++)
-            {
-                const int aid                      = int(g.aln[gid * kMaxAlignments + n]);
-                const int ac                       = int(g.aln_cnt[aid]);
-                g.aln[aid * kMaxAlignments + ac]   = SizeT(curr);
-                g.aln_cnt[aid]                     = uint16_t(ac + 1);
-                g.aln[curr * kMaxAlignments + cnt] = SizeT(aid);
-                cnt++;
-            }
-            g.aln[gid * kMaxAlignments + na]   = SizeT(curr);
-            g.aln_cnt[gid]                     = uint16_t(na + 1);
-            g.aln[curr * kMaxAlignments + cnt] = SizeT(gid);
-            g.aln_cnt[curr]                    = uint16_t(cnt + 1);
-        }
-    }
-    wave_sync();
+    add_write_new_nodes<SizeT>(g, X, L, read, lane);
     // writes 2: the edge head -> curr and the coverage of curr
     for (int rp = lane; rp < L; rp += kWave)
     {
@@ -501,9 +532,15 @@ template <typename SizeT, bool MSA, int kAU = 4>
 __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g, int& node_count, const SizeT* ag, const SizeT* ar,
                                       int alen, int L, const uint8_t* read, const int8_t* w, int s, uint16_t* ecov,
                                       uint16_t* ecov_cnt, SizeT* seq_begin, int max_seqs, const AddScratch& X,
-                                      int lane)
+                                      int lane, uint64_t* prof = nullptr)
 {
     g = as_global(g);
+#ifdef GWAMD_ADD_PROFILE
+    uint64_t pt = now_ticks();
+    auto lap = [&](int k) { const uint64_t t = now_ticks(); if (prof) prof[k] += t - pt; pt = t; };
+#else
+    auto lap = [&](int) {};
+#endif
     const int nc0 = node_count;
     int err       = INT_MAX; // first error in read order: (pos << 8) | status
     if (lane == 0)
@@ -524,6 +561,7 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
                 X.gid[rp[u]] = uint16_t(gv[u] < 0 ? 0xffff : gv[u]);
     }
     wave_sync();
+    lap(0);
     // kinds and existing targets.  kAU positions per lane and pass, their
     // graph loads issued together (the graph is in HBM: one round trip per
     // dependent level instead of one per position)
@@ -591,6 +629,7 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
         }
     }
     wave_sync();
+    lap(1);
     // new node ids: prefix sum over new-node elements in read order
     int nnew = 0;
     for (int r0 = 0; r0 < L; r0 += kWave)
@@ -609,6 +648,7 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
         nnew += total;
     }
     wave_sync();
+    lap(2);
     // independence checks without atomics: every element claims its node (and,
     // for aligned hits / ring updates, its aligned group); after a barrier an
     // element that no longer owns a claimed node has a conflicting partner.
@@ -619,6 +659,7 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
     for (int rp = lane; rp < L; rp += kWave)
         conflict |= int(X.owner[int(X.curr[rp])]) != rp;
     wave_sync();
+    lap(3);
     // aligned groups of the mismatching positions: claim every member, then
     // check the claims (kAU positions per lane, loads batched as above)
     for (int pass = 0; pass < 2; pass++)
@@ -683,6 +724,7 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
     wave_sync();
     if (X.sh[0])
         return -1;
+    lap(4);
     // edge existence and edge-limit errors (kAU positions per lane and pass)
     for (int r0 = 1; r0 < L; r0 += kAU * kWave)
     {
@@ -740,39 +782,9 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
     if (err != INT_MAX)
         return err & 0xff;
     wave_sync();
-    // writes 1: new nodes and aligned rings (one lane per element)
-    for (int rp = lane; rp < L; rp += kWave)
-    {
-        const int kind = X.kind[rp] & 3;
-        if (kind < 2)
-            continue;
-        const int curr  = int(X.curr[rp]);
-        g.base[curr]    = read[rp];
-        g.out_cnt[curr] = 0;
-        g.in_cnt[curr]  = 0;
-        g.aln_cnt[curr] = 0;
-        g.cov[curr]     = 0;
-        if (kind == 3)
-        {
-            const int gid = int(X.gid[rp]);
-            const int na  = int(g.aln_cnt[gid]);
-            int cnt       = 0;
-            for (int n = 0; n < na; n++)
-            {
-                const int aid                      = int(g.aln[gid * kMaxAlignments + n]);
-                const int ac                       = int(g.aln_cnt[aid]);
-                g.aln[aid * kMaxAlignments + ac]   = SizeT(curr);
-                g.aln_cnt[aid]                     = uint16_t(ac + 1);
-                g.aln[curr * kMaxAlignments + cnt] = SizeT(aid);
-                cnt++;
-            }
-            g.aln[gid * kMaxAlignments + na]   = SizeT(curr);
-            g.aln_cnt[gid]                     = uint16_t(na + 1);
-            g.aln[curr * kMaxAlignments + cnt] = SizeT(gid);
-            g.aln_cnt[curr]                    = uint16_t(cnt + 1);
-        }
-    }
-    wave_sync();
+    lap(5);
+    add_write_new_nodes<SizeT>(g, X, L, read, lane);
+    lap(6);
     // writes 2: the edge head -> curr and the coverage of curr.  Element rp
     // touches only curr's in-list and coverage and head's out-list (head =
     // element rp-1's curr), so the elements are independent; kAU per lane and
@@ -872,6 +884,7 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
     }
     node_count = nc0 + nnew;
     wave_sync();
+    lap(7);
     return kSuccess;
 }
 
