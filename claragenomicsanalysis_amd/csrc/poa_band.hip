@@ -1431,7 +1431,8 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
                 // add-alignment scratch in the work region, sized for this read
                 auto a16             = [](int v) { return (v + 15) & ~15; };
                 const int ls         = a16(L + 16);
-                const int need       = 5 * ls + 2 * (V + L + 16) + 16;
+                const int hoff       = 5 * ls + a16(2 * (V + L + 16));
+                const int need       = hoff + 2 * ls;
                 if (need <= d.lds_work_bytes)
                 {
                     AddScratch AX;
@@ -1439,6 +1440,8 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
                     AX.curr  = (GWAMD_LDS uint16_t*)(work + 2 * ls);
                     AX.kind  = work + 4 * ls;
                     AX.owner = (GWAMD_LDS uint16_t*)(work + 5 * ls);
+                    AX.hit   = work + hoff;
+                    AX.ohit  = work + hoff + ls;
                     AX.sh    = (GWAMD_LDS int*)(shb);
                     rc = add_alignment_parallel_batched<SizeT, MSA, kBandAddAU>(g, nc, ag, ar, alen, L, lread, wts_g, s, ecov, ecovc,
                                                             seq_begin, d.max_seqs, AX, lane, addprof);
@@ -1485,8 +1488,9 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
         }
     }
 
+    uint64_t oprof[3] = {0, 0, 0}; // output sections (GWAMD_OUTPUT_PROFILE builds)
     finish_window<SizeT, MSA>(b, d, w, lane, g, status, nseq, node_count, cscore, cpred, ecov, ecovc, seq_begin,
-                              sh_len, sh_status, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off);
+                              sh_len, sh_status, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, oprof);
     ph.lap<kPhOutput>();
     if (lane == 0)
     {
@@ -1494,11 +1498,17 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
         {
             ph.store(b.phase + size_t(w) * kPhases);
 #ifdef GWAMD_ADD_PROFILE
-            // add sections over all 8 slots (s_memtime cycles / 1000): gid fill,
-            // kinds, new ids, node claims, group claims, edge existence,
-            // writes 1, writes 2
+            // add sections over all 8 slots (ticks): gid fill, kinds, new ids,
+            // node claims, group claims, edge existence, writes 1, writes 2
             for (int k = 0; k < 8; k++)
-                b.phase[size_t(w) * kPhases + k] = int64_t(addprof[k] / 1000);
+                b.phase[size_t(w) * kPhases + k] = int64_t(addprof[k]);
+#endif
+#ifdef GWAMD_OUTPUT_PROFILE
+            // output sections over the backbone / add / rowprog slots (ticks):
+            // consensus, racon sort + column map, MSA rows
+            b.phase[size_t(w) * kPhases + kPhBackbone] = int64_t(oprof[0]);
+            b.phase[size_t(w) * kPhases + kPhAdd]      = int64_t(oprof[1]);
+            b.phase[size_t(w) * kPhases + kPhRowProg]  = int64_t(oprof[2]);
 #endif
 #ifdef GWAMD_TOPSORT_PROFILE
             b.phase[size_t(w) * kPhases + kPhBackbone] = int64_t(tsprof[0] / 1000);

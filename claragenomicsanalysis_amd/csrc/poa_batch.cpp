@@ -709,7 +709,7 @@ private:
         const int64_t tile_b  = a16(int64_t(64) * bw + 64 * 16 + 512 + gwamd::poa::kTbRankBytes); // codes +
                                                                       // per-row decode info + walk tables
         const int64_t flags_b = 2 * a16(mn + 2); // row program: spill and far flags
-        const int64_t add_b   = 5 * a16(ms + 16) + 2 * (mn + ms + 16) + 16;
+        const int64_t add_b   = 7 * a16(ms + 16) + a16(2 * (mn + ms + 16)); // + the edge-slot bytes
         // anti-diagonal forward pass (poa_band_ad.hpp): a kAdRing-row ring and
         // one dummy word per lane.  Default: whenever the windows-per-CU
         // choice below leaves room for it (large windows, one or two per CU);

@@ -58,9 +58,16 @@ template <typename SizeT, bool MSA>
 __device__ __forceinline__ void finish_window(const Buffers& b, const Dims& d, int w, int lane, WinGraph<SizeT> g, int status,
                               int nseq, int node_count, int32_t* cscore, SizeT* cpred, uint16_t* ecov,
                               uint16_t* ecovc, SizeT* seq_begin, int& sh_len, int& sh_status,
-                              GWAMD_LDS uint8_t* scratch = nullptr, int scratch_bytes = 0)
+                              GWAMD_LDS uint8_t* scratch = nullptr, int scratch_bytes = 0,
+                              uint64_t* oprof = nullptr)
 {
     g = as_global(g);
+#ifdef GWAMD_OUTPUT_PROFILE
+    uint64_t ot = now_ticks();
+    auto olap = [&](int k) { const uint64_t t = now_ticks(); if (oprof) oprof[k] += t - ot; ot = t; };
+#else
+    auto olap = [&](int) {};
+#endif
     uint8_t* cons_out = b.cons + size_t(w) * d.max_consensus;
     const int graph_status = status;
     if (!MSA || d.want_consensus)
@@ -108,8 +115,10 @@ __device__ __forceinline__ void finish_window(const Buffers& b, const Dims& d, i
         // the racon sort and the node -> column map by the wave in LDS when the
         // graph fits; the racon stack region (cpred) holds node -> column
         int lds_cols        = 0;
+        olap(0);
         const bool lds_done = graph_status == kSuccess && nseq > 0 &&
                               topsort_racon_lds<SizeT>(g, node_count, scratch, scratch_bytes, lane, cpred, &lds_cols);
+        olap(1);
         if (lane == 0)
         {
             int msa_len = 0;
@@ -193,6 +202,7 @@ __device__ __forceinline__ void finish_window(const Buffers& b, const Dims& d, i
                 msa_out[size_t(sr) * d.max_consensus + int(mpos[node])] = g.base[node];
             }
         }
+        olap(2);
         if (lane == 0)
         {
             b.msa_len[w]    = msa_len;
@@ -269,6 +279,10 @@ struct AddScratch
     GWAMD_LDS uint8_t* kind;   // [max_seq] 0 same base, 1 aligned hit, 2 new, 3 new + ring; bit 2: edge exists
     GWAMD_LDS uint16_t* owner; // [max_nodes + max_seq] element that claimed a node (last writer wins)
     GWAMD_LDS int* sh;         // [0] conflict
+    // batched add only: slot of an existing edge head -> curr in curr's in-list
+    // and (MSA) in head's out-list, found by the existence pass (0xff: none)
+    GWAMD_LDS uint8_t* hit  = nullptr; // [max_seq]
+    GWAMD_LDS uint8_t* ohit = nullptr; // [max_seq]
 };
 
 // writes 1 of the wave-parallel add: new nodes and aligned rings, one lane
@@ -728,7 +742,7 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
     // edge existence and edge-limit errors (kAU positions per lane and pass)
     for (int r0 = 1; r0 < L; r0 += kAU * kWave)
     {
-        int head[kAU], curr[kAU], kind[kAU], ic[kAU], oc[kAU];
+        int head[kAU], curr[kAU], kind[kAU], ic[kAU], oc[kAU], hitv[kAU], ohitv[kAU];
         bool exists[kAU];
 #pragma unroll
         for (int u = 0; u < kAU; u++)
@@ -742,6 +756,8 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
             ic[u]         = kind[u] < 2 ? int(g.in_cnt[curr[u]]) : 0;
             oc[u]         = kp >= 2 ? 0 : int(g.out_cnt[head[u]]);
             exists[u]     = false;
+            hitv[u]       = 0xff;
+            ohitv[u]      = 0xff;
         }
         for (int e0 = 0;; e0 += 4)
         {
@@ -761,7 +777,34 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
             for (int u = 0; u < kAU; u++)
 #pragma unroll
                 for (int j = 0; j < 4; j++)
-                    exists[u] |= ie[u][j] == head[u];
+                    if (!exists[u] && ie[u][j] == head[u])
+                        exists[u] = true, hitv[u] = e0 + j;
+        }
+        if (MSA)
+        {
+            // the same edge in head's out-list (its read list gets this read)
+            for (int e0 = 0;; e0 += 4)
+            {
+                bool need = false;
+#pragma unroll
+                for (int u = 0; u < kAU; u++)
+                    need |= exists[u] && ohitv[u] == 0xff && e0 < oc[u];
+                if (__builtin_amdgcn_ballot_w64(need) == 0)
+                    break;
+                int oe[kAU][4];
+#pragma unroll
+                for (int u = 0; u < kAU; u++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        oe[u][j] = (exists[u] && ohitv[u] == 0xff && e0 + j < oc[u])
+                                       ? int(g.out_e[head[u] * kMaxEdges + e0 + j]) : -1;
+#pragma unroll
+                for (int u = 0; u < kAU; u++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (ohitv[u] == 0xff && oe[u][j] >= 0 && oe[u][j] == curr[u])
+                            ohitv[u] = e0 + j;
+            }
         }
 #pragma unroll
         for (int u = 0; u < kAU; u++)
@@ -776,6 +819,8 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
             }
             else
                 X.kind[rp] = uint8_t(kind[u] | 4);
+            X.hit[rp]  = uint8_t(hitv[u]);
+            X.ohit[rp] = uint8_t(ohitv[u]);
         }
     }
     err = -wave_max(-err); // wave-wide minimum
@@ -801,49 +846,22 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
             head[u]       = (in && rp > 0) ? int(X.curr[rp - 1]) : 0;
             kind[u]       = (in && rp > 0) ? int(X.kind[rp]) : -1; // -1: no edge (rp 0 or out of range)
             wsum[u]       = (in && rp > 0) ? int(uint16_t(int(w[rp - 1]))) + int(w[rp]) : 0;
+            // existing edges: their slots from the existence pass
+            const int hs  = (in && rp > 0) ? int(X.hit[rp]) : 0xff;
+            const int os  = (in && rp > 0) ? int(X.ohit[rp]) : 0xff;
+            hit[u]        = hs == 0xff ? -1 : hs;
+            ohit[u]       = os == 0xff ? -1 : os;
             if (MSA && in && rp == 0)
                 seq_begin[s] = SizeT(curr[u]);
         }
 #pragma unroll
         for (int u = 0; u < kAU; u++)
         {
-            const int rp = r0 + u * kWave + lane;
-            ic[u]        = kind[u] >= 0 ? int(g.in_cnt[curr[u]]) : 0;
-            oc[u]        = (kind[u] >= 0 && (!(kind[u] & 4) || MSA)) ? int(g.out_cnt[head[u]]) : 0;
-            cv[u]        = rp < L ? int(g.cov[curr[u]]) : 0;
-            hit[u]       = -1;
-            ohit[u]      = -1;
-        }
-        // existing edges: their slot in curr's in-list (and, MSA, in head's out-list)
-        for (int e0 = 0;; e0 += 4)
-        {
-            bool need = false;
-#pragma unroll
-            for (int u = 0; u < kAU; u++)
-                need |= kind[u] >= 0 && (kind[u] & 4) && ((hit[u] < 0 && e0 < ic[u]) || (MSA && ohit[u] < 0 && e0 < oc[u]));
-            if (__builtin_amdgcn_ballot_w64(need) == 0)
-                break;
-            int ie[kAU][4], oe[kAU][4];
-#pragma unroll
-            for (int u = 0; u < kAU; u++)
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                {
-                    const bool ex = kind[u] >= 0 && (kind[u] & 4);
-                    ie[u][j] = (ex && hit[u] < 0 && e0 + j < ic[u]) ? int(g.in_e[curr[u] * kMaxEdges + e0 + j]) : -1;
-                    oe[u][j] = (MSA && ex && ohit[u] < 0 && e0 + j < oc[u]) ? int(g.out_e[head[u] * kMaxEdges + e0 + j])
-                                                                             : -1;
-                }
-#pragma unroll
-            for (int u = 0; u < kAU; u++)
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                {
-                    if (hit[u] < 0 && ie[u][j] >= 0 && ie[u][j] == head[u])
-                        hit[u] = e0 + j;
-                    if (MSA && ohit[u] < 0 && oe[u][j] >= 0 && oe[u][j] == curr[u])
-                        ohit[u] = e0 + j;
-                }
+            const int rp  = r0 + u * kWave + lane;
+            const bool nw = kind[u] >= 0 && !(kind[u] & 4); // a new edge
+            ic[u]         = nw ? int(g.in_cnt[curr[u]]) : 0;
+            oc[u]         = nw ? int(g.out_cnt[head[u]]) : 0;
+            cv[u]         = rp < L ? int(g.cov[curr[u]]) : 0;
         }
 #pragma unroll
         for (int u = 0; u < kAU; u++)
@@ -960,14 +978,17 @@ __device__ __forceinline__ bool topsort_racon_lds_impl(WinGraph<SizeT> g, int n,
             id          = uniform(id);
             k           = uniform(k);
             col         = uniform(col);
-            const int m = uniform(int(marks[id]));
+            // the mark and (CSR) the list word of the node are read together
+            const int mraw      = int(marks[id]);
+            const uint32_t wraw = CSR ? info[id] : 0u;
+            const int m = uniform(mraw);
             bool valid  = true;
             if ((m & 3) != 2)
             {
                 int ic, ac, bl, al;
                 if constexpr (CSR)
                 {
-                    const uint32_t w = uint32_t(uniform(int(info[id])));
+                    const uint32_t w = uint32_t(uniform(int(wraw)));
                     const int o      = int(w & 0xfffffu);
                     ic               = int((w >> 20) & 63u);
                     ac               = (m & 4) ? int(w >> 26) : 0;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 3, call m: compacted new-node writes in the parallel add (all POA
+# Round 3, call m: parallel add changes (all POA
 # kernels): the whole GPU suite, then the B, C and B_banded lines.
 cd "$(dirname "$0")/.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
