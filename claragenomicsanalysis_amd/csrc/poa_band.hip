@@ -931,7 +931,7 @@ template <typename ScoreT, typename SizeT, int CPL>
 __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int V, const uint8_t* read, int L,
                               int end_row, const Band& B, const Scores sc, const ScoreT* spill, int rowsz,
                               GWAMD_LDS uint8_t* tile, SizeT* ag, SizeT* ar, int aln_cap,
-                              int lane, BandProf& bp, bool rank)
+                              int lane, BandProf& bp, bool rank, bool strip)
 {
     X = as_global(X);
     spill = glb(spill);
@@ -1009,23 +1009,22 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
         wave_sync();
         bp.add(kBpTileCyc, BandProf::now() - tt0);
     };
-    // Move window: the moves out of kWinR x kWinC cells (rows wi0-kWinR+1..wi0,
-    // columns wj0-kWinC+1..wj0) decoded in one lane-parallel pass, two cells
-    // per lane, packed (row << 16 | column); the walk then takes them with
-    // readlane instead of one LDS round trip and its decoding per step.  Cells
-    // whose move needs more than the tile and the inline predecessor distances
-    // (row 0, column 0, outside the band, listed or escaped predecessor rows,
-    // no move) are kSlow and go through the general step.
-    constexpr int kWinR     = 16;
-    constexpr int kWinC     = 8;
+    // Move window (TbWin, poa_wave.hpp): the moves of 128 cells decoded in
+    // one lane-parallel pass, two cells per lane, packed (row << 16 |
+    // column); the walk then takes them instead of one LDS round trip and
+    // its decoding per step.  Cells whose move needs more than the tile and
+    // the inline predecessor distances (row 0, column 0, outside the band,
+    // listed or escaped predecessor rows, no move) are kSlow and go through
+    // the general step.
     constexpr uint32_t kSlow = 0xffffffffu;
     const bool win_ok       = V < 65535 && L < 65535;
-    int wi0 = -1, wj0 = -1;
+    TbWin G;
+    G.init(strip, i, L);
     uint32_t wpk0 = kSlow, wpk1 = kSlow;
     // branch-free: the row's info from the LDS table, then its code byte
     auto decode_cell = [&](int t) -> uint32_t {
-        const int r      = wi0 - t / kWinC;
-        const int c      = wj0 - t % kWinC;
+        const int r      = G.row(t);
+        const int c      = G.col(t);
         const int k      = min(max(r - ti0, 0), kWave - 1);
         const v4i_t info = rowinfo[k];
         const uint32_t x = uint32_t(info.x);
@@ -1049,19 +1048,20 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
         prev_i = uniform(prev_i);
         prev_j = uniform(prev_j);
         ti0    = uniform(ti0);
-        wi0    = uniform(wi0);
-        wj0    = uniform(wj0);
+        G.wi0   = uniform(G.wi0);
+        G.wj0   = uniform(G.wj0);
+        G.slope = uniform(G.slope);
+        G.next  = uniform(G.next);
         n      = uniform(n);
         loops  = uniform(loops);
         if (win_ok && i >= 1 && j >= 1)
         {
-            if (!(i <= wi0 && i > wi0 - kWinR && j <= wj0 && j > wj0 - kWinC))
+            if (G.index(i, j) < 0)
             {
+                G.refill(i, j);
                 // the tile must hold the window's rows (those >= 1)
-                if (i < ti0 || i >= ti0 + kBandTile || (i - (kWinR - 1) < ti0 && ti0 > 1))
+                if (i < ti0 || i >= ti0 + kBandTile || (i - G.row_span() < ti0 && ti0 > 1))
                     load_tile(i);
-                wi0  = i;
-                wj0  = j;
                 wpk0 = decode_cell(lane);
                 wpk1 = decode_cell(lane + kWave);
                 bp.add(kBpRefill, 1);
@@ -1069,12 +1069,12 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
             // walk the window: every value here is wave-uniform (SGPRs)
             int ci = i, cj = j, cn = n, cl = loops;
             if (rank)
-                walk_window_ranked<kWinR, kWinC, 1>(wpk0, wpk1, wi0, wj0, ci, cj, cn, cl, bound, lane, eg, er,
-                                                    tile + kBandTile * bw + kWave * 16 + 512, flush);
+                walk_window_ranked<1>(wpk0, wpk1, G, ci, cj, cn, cl, bound, lane, eg, er,
+                                      tile + kBandTile * bw + kWave * 16 + 512, flush);
             else
             while (true)
             {
-                const int idx     = (wi0 - ci) * kWinC + (wj0 - cj);
+                const int idx     = G.index(ci, cj);
                 const uint32_t nx = uint32_t(idx < kWave ? __builtin_amdgcn_readlane(int(wpk0), idx)
                                                          : __builtin_amdgcn_readlane(int(wpk1), idx - kWave));
                 if (nx == kSlow)
@@ -1091,12 +1091,12 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
                     flush(cn);
                 ci = pi;
                 cj = pj;
-                if ((ci == 0 && cj == 0) || cl >= bound || ci < 1 || cj < 1 || ci > wi0 ||
-                    ci <= wi0 - kWinR || cj > wj0 || cj <= wj0 - kWinC)
+                if ((ci == 0 && cj == 0) || cl >= bound || ci < 1 || cj < 1 || G.index(ci, cj) < 0)
                     break;
             }
             if (cl != loops)
             {
+                G.follow(ci, cj);
                 prev_i = i = ci;
                 prev_j = j = cj;
                 n      = cn;
@@ -1415,7 +1415,8 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             ph.lap<kPhForward>();
             const int alen = band_traceback<ScoreT, SizeT, CPL>(g, X, V, lread, L, end_row, B, sc, spill, rowsz, tile,
-                                                                ag, ar, d.aln_cap, lane, bp, d.tb_rank != 0);
+                                                                ag, ar, d.aln_cap, lane, bp, (d.tb_rank & 1) != 0,
+                                                                (d.tb_rank & 2) != 0);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             wave_sync();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");

@@ -680,12 +680,21 @@ private:
     // traceback tile, the add-alignment scratch; the topological sort also
     // reuses the read) | shared words.  Windows per CU: 4, 2 or 1, the most
     // that leave room for the work region at this batch's maximum sizes.
-    // traceback move-window walk: pointer doubling (default) or the scalar
-    // walk (GWAMD_TB_WALK=scalar, for parity tests and diagnostics)
+    // traceback move windows (TbWin, poa_wave.hpp): bit 0 walks them by
+    // pointer doubling (else the scalar walk), bit 1 shapes them as strips
+    // along the path (else 16 x 8 rectangles).  Default both;
+    // GWAMD_TB_WALK=scalar | rect | scalar_rect for parity tests and A/B runs.
     static int tb_rank_default()
     {
         const char* ev = std::getenv("GWAMD_TB_WALK");
-        return (ev && std::string(ev) == "scalar") ? 0 : 1;
+        const std::string v = ev ? ev : "";
+        if (v == "scalar")
+            return 2;
+        if (v == "rect")
+            return 1;
+        if (v == "scalar_rect")
+            return 0;
+        return 3;
     }
 
     void plan_band_kernel()

@@ -925,7 +925,7 @@ __device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, con
 template <typename SizeT>
 __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L, int end_row,
                                const uint8_t* codes, int code_stride, uint8_t* tile, SizeT* ag, SizeT* ar,
-                               int aln_cap, int lane, bool rank)
+                               int aln_cap, int lane, bool rank, bool strip)
 {
     g = as_global(g);
 
@@ -980,20 +980,18 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
         }
         wave_sync();
     };
-    // Move window (as in the banded traceback, poa_band.hip): the moves out of
-    // kWinR x kWinC cells decoded in one lane-parallel pass, two cells per
-    // lane, packed (row << 16 | column), then walked with readlane.  Cells
-    // outside the tile or with escaped predecessor lists are kSlow and take
-    // the general step.
-    constexpr int kWinR      = 16;
-    constexpr int kWinC      = 8;
+    // Move window (TbWin, as in the banded traceback, poa_band.hip): the moves
+    // of 128 cells decoded in one lane-parallel pass, two cells per lane,
+    // packed (row << 16 | column), then walked.  Cells outside the tile or
+    // with escaped predecessor lists are kSlow and take the general step.
     constexpr uint32_t kSlow = 0xffffffffu;
     const bool win_ok        = V < 65535 && L < 65535;
-    int wi0 = -1, wj0 = -1;
+    TbWin G;
+    G.init(strip, i, L);
     uint32_t wpk0 = kSlow, wpk1 = kSlow;
     auto decode_cell = [&](int t) -> uint32_t {
-        const int r  = wi0 - t / kWinC;
-        const int c  = wj0 - t % kWinC;
+        const int r  = G.row(t);
+        const int c  = G.col(t);
         const int cj = c + kColShift;
         uint32_t res = kSlow;
         if (r >= 1 && c >= 0 && r >= ti0 && r < ti0 + kTileRows && cj >= tj0 && cj < tj0 + kTileCols)
@@ -1023,30 +1021,31 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
         loops = uniform(loops);
         ti0   = uniform(ti0);
         tj0   = uniform(tj0);
-        wi0   = uniform(wi0);
-        wj0   = uniform(wj0);
+        G.wi0   = uniform(G.wi0);
+        G.wj0   = uniform(G.wj0);
+        G.slope = uniform(G.slope);
+        G.next  = uniform(G.next);
         if (win_ok && i >= 1)
         {
-            if (!(i <= wi0 && i > wi0 - kWinR && j <= wj0 && j > wj0 - kWinC))
+            if (G.index(i, j) < 0)
             {
+                G.refill(i, j);
                 const int cj = j + kColShift;
                 if (i < ti0 || i >= ti0 + kTileRows || cj < tj0 || cj >= tj0 + kTileCols ||
-                    (i - (kWinR - 1) < ti0 && ti0 > 0) || (cj - (kWinC - 1) < tj0 && tj0 > 0))
+                    (i - G.row_span() < ti0 && ti0 > 0) || (cj - G.col_span() < tj0 && tj0 > 0))
                     load_tile(i, cj);
-                wi0  = i;
-                wj0  = j;
-                wpk0 = decode_cell(lane);
-                wpk1 = decode_cell(lane + kWave);
+                wpk0  = decode_cell(lane);
+                wpk1  = decode_cell(lane + kWave);
             }
             // walk the window: every value here is wave-uniform (SGPRs)
             int ci = i, cj = j, cn = n, cl = loops;
             if (rank)
-                walk_window_ranked<kWinR, kWinC, 0>(wpk0, wpk1, wi0, wj0, ci, cj, cn, cl, bound, lane, eg, er,
-                                                    (GWAMD_LDS uint8_t*)(tile + kTileRows * kTileCols), flush);
+                walk_window_ranked<0>(wpk0, wpk1, G, ci, cj, cn, cl, bound, lane, eg, er,
+                                      (GWAMD_LDS uint8_t*)(tile + kTileRows * kTileCols), flush);
             else
             while (true)
             {
-                const int idx     = (wi0 - ci) * kWinC + (wj0 - cj);
+                const int idx     = G.index(ci, cj);
                 const uint32_t nx = uint32_t(idx < kWave ? __builtin_amdgcn_readlane(int(wpk0), idx)
                                                          : __builtin_amdgcn_readlane(int(wpk1), idx - kWave));
                 if (nx == kSlow)
@@ -1063,12 +1062,12 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
                     flush(cn);
                 ci = pi;
                 cj = pj;
-                if ((ci == 0 && cj == 0) || cl >= bound || ci < 1 || ci > wi0 || ci <= wi0 - kWinR ||
-                    cj > wj0 || cj <= wj0 - kWinC)
+                if ((ci == 0 && cj == 0) || cl >= bound || ci < 1 || G.index(ci, cj) < 0)
                     break;
             }
             if (cl != loops)
             {
+                G.follow(ci, cj);
                 i     = ci;
                 j     = cj;
                 n     = cn;
@@ -1244,7 +1243,8 @@ __global__ void __launch_bounds__(kWave * NW, NW >= 4 ? 4 : 1) poa_window_kernel
             if (wave == 0)
             {
                 const int alen_w = traceback_codes<SizeT>(g, P, V, L, end_row, codes, d.code_stride, tile, ag, ar,
-                                                          d.aln_cap, lane, d.tb_rank != 0);
+                                                          d.aln_cap, lane, (d.tb_rank & 1) != 0,
+                                                          (d.tb_rank & 2) != 0);
                 if (lane == 0)
                     sh_len = alen_w;
             }

@@ -1393,30 +1393,93 @@ __device__ __forceinline__ bool topsort_lds_big(WinGraph<SizeT> g, int n, GWAMD_
 }
 
 // ---------------------------------------------------------------------------
-// Traceback move-window walk by pointer doubling.  The window holds the moves
-// of kWinR x kWinC = 128 cells (cell t: row wi0 - t / kWinC, column
-// wj0 - t % kWinC), two per lane (wpk0: cell lane, wpk1: cell lane + 64),
-// packed (row << 16 | column) or kSlow when the general step must decide.
+// Traceback move window: 128 cells around the walk whose moves are decoded
+// lane-parallel, two per lane (cell t and t + 64).  Two shapes:
+//  * rectangle (slope == 0): 16 rows x 8 columns, cell t = a * 8 + b at row
+//    wi0 - a, column wj0 - b.  A path leaves it after ~8 diagonal steps;
+//  * strip along the path (slope > 0, round 3): 16 columns, and in column b
+//    the 8 rows around the line a = b * slope / 16 (cell t = b * 8 + o, row
+//    wi0 - (b * slope / 16 + o - kTbStripAbove)).  In topological order a
+//    diagonal move usually skips rows of other branches (on config B the
+//    path crosses ~1.5-2 rows per column), so the slope is the rows per
+//    column of the previous window's path; a path that follows it stays in
+//    the strip for up to 16 columns.
+// Only the shape changes: moves, tie order and the general step are the
+// same, so both shapes give the same path (parity tests run both).
+constexpr int kTbStripAbove = 2;  // strip rows above the line (horizontal moves)
+constexpr int kTbSlopeMin   = 4;  // 0.25 rows per column
+constexpr int kTbSlopeMax   = 56; // 3.5 rows per column: strip rows < 58 (banded tile: 64)
+
+struct TbWin
+{
+    int wi0 = -1, wj0 = -1;
+    int slope = 0; // 0: rectangle; else rows per column x 16
+    int next  = 0; // slope of the next window (taken at refill(), so the
+                   // decoded cells always match the geometry they were built for)
+    // rows above wi0 the window reaches (the tile must hold wi0 - span .. wi0)
+    __device__ __forceinline__ int row_span() const { return slope ? ((15 * slope) >> 4) + 7 - kTbStripAbove : 15; }
+    __device__ __forceinline__ int col_span() const { return slope ? 15 : 7; }
+    __device__ __forceinline__ int row(int t) const
+    {
+        return slope ? wi0 - ((((t >> 3) * slope) >> 4) + (t & 7) - kTbStripAbove) : wi0 - (t >> 3);
+    }
+    __device__ __forceinline__ int col(int t) const { return slope ? wj0 - (t >> 3) : wj0 - (t & 7); }
+    // cell of (r, c), or -1 outside the window
+    __device__ __forceinline__ int index(int r, int c) const
+    {
+        const int a = wi0 - r, b = wj0 - c;
+        if (slope)
+        {
+            const int o = a - ((b * slope) >> 4) + kTbStripAbove;
+            return (uint32_t(b) < 16u && uint32_t(o) < 8u) ? b * 8 + o : -1;
+        }
+        return (uint32_t(a) < 16u && uint32_t(b) < 8u) ? a * 8 + b : -1;
+    }
+    // next window's slope from the path the walk took through this one
+    __device__ __forceinline__ void follow(int ci, int cj)
+    {
+        const int da = wi0 - ci, db = wj0 - cj;
+        if (next && db >= 4)
+            next = min(max((16 * da + db / 2) / db, kTbSlopeMin), kTbSlopeMax);
+    }
+    // a new window with its corner at (i, j)
+    __device__ __forceinline__ void refill(int i, int j)
+    {
+        slope = next;
+        wi0   = i;
+        wj0   = j;
+    }
+    // strip windows start with the slope of the whole path (rows x 16 / cols)
+    __device__ __forceinline__ void init(bool strip, int rows, int cols)
+    {
+        next = !strip ? 0
+                      : (cols > 0 ? min(max((16 * rows + cols / 2) / cols, kTbSlopeMin), kTbSlopeMax) : kTbSlopeMin);
+        slope = next;
+    }
+};
+
+// Traceback move-window walk by pointer doubling over a TbWin window whose
+// cells hold their moves packed (row << 16 | column) or kSlow when the
+// general step must decide (wpk0: cell lane, wpk1: cell lane + 64).
 // The scalar walk takes one cell per iteration (~350 cycles of dependent
 // scalar code); here every lane finds the cell of one path step at once:
 // J0 maps a cell to the next cell in the window (kX: the move leaves the
 // window, a slow cell maps to itself), J^2, J^3, J^4, J^8, J^12 and J^16 are
 // built in LDS (4 dependent rounds), and lane L follows step
-// k = (L - cn) mod 64 by the base-4 digits of k (3 dependent reads).  A path
-// inside the window has at most kWinR + kWinC - 1 < 32 steps.  The
+// k = (L - cn) mod 64 by the base-4 digits of k (3 dependent reads), so one
+// walk takes at most 32 steps (a longer path in the window continues in the
+// next walk from the same window).  The
 // steps taken are a prefix in k; each lane writes its own (eg, er) entry
 // exactly as the scalar walk would have, with the flush at the 64-entry
 // boundary in between.  Updates (ci, cj) to the cell after the last step, cn
 // (entries) and cl (loop count, capped at bound).  kCmin: the smallest column
 // that stays in the window (0 full mode, 1 banded).  Same results as the
 // scalar walk by construction; parity is tested with both (GWAMD_TB_WALK).
-template <int kWinR, int kWinC, int kCmin, typename Flush>
-__device__ __forceinline__ void walk_window_ranked(uint32_t wpk0, uint32_t wpk1, int wi0, int wj0, int& ci, int& cj,
+template <int kCmin, typename Flush>
+__device__ __forceinline__ void walk_window_ranked(uint32_t wpk0, uint32_t wpk1, const TbWin& G, int& ci, int& cj,
                                                    int& cn, int& cl, int bound, int lane, int& eg, int& er,
                                                    GWAMD_LDS uint8_t* scratch, Flush&& flush)
 {
-    static_assert(kWinR * kWinC == 2 * kWave, "two window cells per lane");
-    static_assert(kWinR + kWinC - 1 < 32, "paths inside the window have fewer than 32 steps");
     constexpr uint32_t kSlow = 0xffffffffu;
     constexpr int kX         = 2 * kWave;
     constexpr int kS         = 144; // table stride (129 entries: index kX maps to itself)
@@ -1425,8 +1488,9 @@ __device__ __forceinline__ void walk_window_ranked(uint32_t wpk0, uint32_t wpk1,
     GWAMD_LDS uint32_t* W    = (GWAMD_LDS uint32_t*)(scratch + 7 * kS);
     auto next_cell = [&](int t, uint32_t nx) -> int {
         const int pi  = int(nx >> 16), pj = int(nx & 0xffffu);
-        const bool in = pi >= 1 && pj >= kCmin && pi <= wi0 && pi > wi0 - kWinR && pj <= wj0 && pj > wj0 - kWinC;
-        return nx == kSlow ? t : (in ? (wi0 - pi) * kWinC + (wj0 - pj) : kX);
+        const int x   = G.index(pi, pj);
+        const bool in = pi >= 1 && pj >= kCmin && x >= 0;
+        return nx == kSlow ? t : (in ? x : kX);
     };
     auto put = [&](int tab, int va, int vb) {
         J[tab * kS + lane]         = uint8_t(va);
@@ -1459,7 +1523,7 @@ __device__ __forceinline__ void walk_window_ranked(uint32_t wpk0, uint32_t wpk1,
     // step k = d0 + 4 d1 + 16 d2: three dependent reads
     const int k  = (lane - cn) & (kWave - 1);
     const int d0 = k & 3, d1 = (k >> 2) & 3, d2 = (k >> 4) & 1;
-    int c        = (wi0 - ci) * kWinC + (wj0 - cj);
+    int c        = G.index(ci, cj);
     {
         const int c2 = int(J[max(d0 - 1, 0) * kS + c]);
         c            = d0 ? c2 : c;
@@ -1477,7 +1541,7 @@ __device__ __forceinline__ void walk_window_ranked(uint32_t wpk0, uint32_t wpk1,
     const int steps   = __popcll(__builtin_amdgcn_ballot_w64(taken));
     if (steps == 0)
         return;
-    const int r = wi0 - c / kWinC, col = wj0 - c % kWinC;
+    const int r = G.row(c), col = G.col(c);
     const int pi = int(nx >> 16), pj = int(nx & 0xffffu);
     const int neg = r == pi ? -1 : r;
     const int ner = col == pj ? -1 : col - 1;

@@ -2,7 +2,8 @@
 // (topsort_lds, deg <= 1 branch) on one wave, over a chain of n nodes in LDS.
 // Variants: (a) every lane writes the same LDS words (the current loop),
 // (b) the three stores under lane 0 only, (c) only the node-word store,
-// (d) no stores (read chain alone).  Output: cycles/pop.
+// (d) no stores (read chain alone), (e) one store: queue entry when released,
+// node word otherwise.  Output: cycles/pop.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
@@ -50,6 +51,14 @@ __global__ void kpop(long long* out, int n)
         }
         else if (V == 2)
             info[o] = oi;
+        else if (V == 4)
+        {
+            // one store: the released node's queue entry, or the decremented word
+            if (rel)
+                queue[tail] = uint16_t(o);
+            else
+                info[o] = oi;
+        }
         tail += rel ? 1 : 0;
         q++;
         vinfo = oi;
@@ -73,7 +82,8 @@ int main()
         const char* name;
         void (*k)(long long*, int);
     } ks[] = {{"all lanes store (current)", kpop<0>}, {"lane 0 stores", kpop<1>}, {"node word only", kpop<2>},
-              {"no stores", kpop<3>}};
+              {"no stores", kpop<3>},
+              {"queue or word store", kpop<4>}};
     for (auto& k : ks)
     {
         hipLaunchKernelGGL(k.k, dim3(1), dim3(64), 0, 0, d, n);

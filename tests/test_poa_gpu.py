@@ -497,11 +497,13 @@ def test_persistent_grid_and_launch_order(mode, grid, monkeypatch):
             assert {(u, v): graphs[i].weight(u, v) for (u, v) in graphs[i].edges} == expect, (mode, grid, rep, i)
 
 
-# Traceback move-window walk: pointer doubling (default) and the scalar walk
-# (GWAMD_TB_WALK=scalar) give identical alignments, so identical outputs, on
-# the full-mode LDS kernel and the banded kernel (row-parallel and
-# anti-diagonal forward), consensus and MSA, against the oracle; the windows
-# include repeats, empty/one-base reads and reads shorter than the band.
+# Traceback move-window walk: pointer doubling and the scalar walk, over
+# strip windows along the path (default) and 16 x 8 rectangles
+# (GWAMD_TB_WALK=default | scalar | rect | scalar_rect) give identical
+# alignments, so identical outputs, on the full-mode LDS kernel and the banded
+# kernel (row-parallel and anti-diagonal forward), consensus and MSA, against
+# the oracle; the windows include repeats, empty/one-base reads and reads
+# shorter than the band.
 @pytest.mark.parametrize("mode", ["full", "band_row", "band_ad"])
 @pytest.mark.parametrize("out", ["consensus", "msa"])
 def test_traceback_walk_modes(mode, out, monkeypatch):
@@ -515,7 +517,7 @@ def test_traceback_walk_modes(mode, out, monkeypatch):
     wins = [w for w in wins if max(len(r) for r in w) < ms - 60]
     msa = out == "msa"
     res = {}
-    for walk in ("rank", "scalar"):
+    for walk in ("rank", "scalar", "rect", "scalar_rect"):
         monkeypatch.setenv("GWAMD_TB_WALK", walk)
         b = run_gpu(wins, ms, 60, banded=banded, bw=256, output_type=out)
         assert b.kernel_variant() == {"full": 2, "band_row": 3, "band_ad": 4}[mode]
@@ -524,6 +526,8 @@ def test_traceback_walk_modes(mode, out, monkeypatch):
     monkeypatch.delenv("GWAMD_TB_WALK", raising=False)
     monkeypatch.delenv("GWAMD_BAND_FWD", raising=False)
     assert res["rank"] == res["scalar"]
+    assert res["rank"] == res["rect"]
+    assert res["rank"] == res["scalar_rect"]
     for i, w in enumerate(wins):
         r = run_oracle(w, ms, 60, banded=banded, bw=256, msa=msa, score_bits=sbits)
         if msa:
