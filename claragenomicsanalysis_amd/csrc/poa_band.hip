@@ -931,7 +931,7 @@ template <typename ScoreT, typename SizeT, int CPL>
 __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int V, const uint8_t* read, int L,
                               int end_row, const Band& B, const Scores sc, const ScoreT* spill, int rowsz,
                               GWAMD_LDS uint8_t* tile, SizeT* ag, SizeT* ar, int aln_cap,
-                              int lane, BandProf& bp, bool rank, bool strip)
+                              int lane, BandProf& bp, bool rank, int tbmode)
 {
     X = as_global(X);
     spill = glb(spill);
@@ -1019,7 +1019,7 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
     constexpr uint32_t kSlow = 0xffffffffu;
     const bool win_ok       = V < 65535 && L < 65535;
     TbWin G;
-    G.init(strip, i, L);
+    G.init(tbmode, i, L, kBandTile);
     uint32_t wpk0 = kSlow, wpk1 = kSlow;
     // branch-free: the row's info from the LDS table, then its code byte
     auto decode_cell = [&](int t) -> uint32_t {
@@ -1416,7 +1416,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
             ph.lap<kPhForward>();
             const int alen = band_traceback<ScoreT, SizeT, CPL>(g, X, V, lread, L, end_row, B, sc, spill, rowsz, tile,
                                                                 ag, ar, d.aln_cap, lane, bp, (d.tb_rank & 1) != 0,
-                                                                (d.tb_rank & 2) != 0);
+                                                                d.tb_rank);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             wave_sync();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");

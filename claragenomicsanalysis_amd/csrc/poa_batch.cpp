@@ -682,8 +682,10 @@ private:
     // that leave room for the work region at this batch's maximum sizes.
     // traceback move windows (TbWin, poa_wave.hpp): bit 0 walks them by
     // pointer doubling (else the scalar walk), bit 1 shapes them as strips
-    // along the path (else 16 x 8 rectangles).  Default both;
-    // GWAMD_TB_WALK=scalar | rect | scalar_rect for parity tests and A/B runs.
+    // along the path (else 16 x 8 rectangles), bit 2 makes the strips 32
+    // columns x 4 rows (else 16 x 8).  Default: pointer doubling over 16 x 8
+    // strips; GWAMD_TB_WALK=scalar | rect | scalar_rect | strip32 |
+    // scalar_strip32 for parity tests and A/B runs.
     static int tb_rank_default()
     {
         const char* ev = std::getenv("GWAMD_TB_WALK");
@@ -694,6 +696,10 @@ private:
             return 1;
         if (v == "scalar_rect")
             return 0;
+        if (v == "strip32")
+            return 7;
+        if (v == "scalar_strip32")
+            return 6;
         return 3;
     }
 

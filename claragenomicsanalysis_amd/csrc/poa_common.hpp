@@ -91,7 +91,7 @@ struct Dims
     int32_t aux_recc_off;   //   | row records c (u32)
     int32_t aux_rece_off;   //   | row records e (u32)
     int32_t band_ad;        // banded kernel: waves of the anti-diagonal forward pass (0: row-parallel pass)
-    int32_t tb_rank;        // traceback move windows: bit 0 pointer-doubling walk, bit 1 strip shape (TbWin)
+    int32_t tb_rank;        // traceback move windows (TbWin): bit 0 pointer-doubling walk, bit 1 strips, bit 2 32 x 4 strips
 };
 
 // LDS bytes of the pointer-doubling traceback walk (walk_window_ranked)

@@ -925,7 +925,7 @@ __device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, con
 template <typename SizeT>
 __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L, int end_row,
                                const uint8_t* codes, int code_stride, uint8_t* tile, SizeT* ag, SizeT* ar,
-                               int aln_cap, int lane, bool rank, bool strip)
+                               int aln_cap, int lane, bool rank, int tbmode)
 {
     g = as_global(g);
 
@@ -987,7 +987,7 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
     constexpr uint32_t kSlow = 0xffffffffu;
     const bool win_ok        = V < 65535 && L < 65535;
     TbWin G;
-    G.init(strip, i, L);
+    G.init(tbmode, i, L, kTileRows);
     uint32_t wpk0 = kSlow, wpk1 = kSlow;
     auto decode_cell = [&](int t) -> uint32_t {
         const int r  = G.row(t);
@@ -1244,7 +1244,7 @@ __global__ void __launch_bounds__(kWave * NW, NW >= 4 ? 4 : 1) poa_window_kernel
             {
                 const int alen_w = traceback_codes<SizeT>(g, P, V, L, end_row, codes, d.code_stride, tile, ag, ar,
                                                           d.aln_cap, lane, (d.tb_rank & 1) != 0,
-                                                          (d.tb_rank & 2) != 0);
+                                                          d.tb_rank);
                 if (lane == 0)
                     sh_len = alen_w;
             }

@@ -1399,16 +1399,14 @@ __device__ __forceinline__ bool topsort_lds_big(WinGraph<SizeT> g, int n, GWAMD_
 //    wi0 - a, column wj0 - b.  A path leaves it after ~8 diagonal steps;
 //  * strip along the path (slope > 0, round 3): 16 columns, and in column b
 //    the 8 rows around the line a = b * slope / 16 (cell t = b * 8 + o, row
-//    wi0 - (b * slope / 16 + o - kTbStripAbove)).  In topological order a
+//    wi0 - (b * slope / 16 + o - 2)); or 32 columns x 4 rows.  In topological order a
 //    diagonal move usually skips rows of other branches (on config B the
 //    path crosses ~1.5-2 rows per column), so the slope is the rows per
 //    column of the previous window's path; a path that follows it stays in
 //    the strip for up to 16 columns.
 // Only the shape changes: moves, tie order and the general step are the
 // same, so both shapes give the same path (parity tests run both).
-constexpr int kTbStripAbove = 2;  // strip rows above the line (horizontal moves)
-constexpr int kTbSlopeMin   = 4;  // 0.25 rows per column
-constexpr int kTbSlopeMax   = 56; // 3.5 rows per column: strip rows < 58 (banded tile: 64)
+constexpr int kTbSlopeMin = 4; // 0.25 rows per column
 
 struct TbWin
 {
@@ -1416,22 +1414,29 @@ struct TbWin
     int slope = 0; // 0: rectangle; else rows per column x 16
     int next  = 0; // slope of the next window (taken at refill(), so the
                    // decoded cells always match the geometry they were built for)
+    int sh    = 3; // strip: log2 of the rows per column (3: 16 x 8, 2: 32 x 4)
+    int smax  = 0; // strip: largest slope whose strip fits the code tile
+    __device__ __forceinline__ int above() const { return sh == 3 ? 2 : 1; } // strip rows above the line
+    __device__ __forceinline__ int cols() const { return 128 >> sh; }
     // rows above wi0 the window reaches (the tile must hold wi0 - span .. wi0)
-    __device__ __forceinline__ int row_span() const { return slope ? ((15 * slope) >> 4) + 7 - kTbStripAbove : 15; }
-    __device__ __forceinline__ int col_span() const { return slope ? 15 : 7; }
+    __device__ __forceinline__ int row_span() const
+    {
+        return slope ? (((cols() - 1) * slope) >> 4) + (1 << sh) - 1 - above() : 15;
+    }
+    __device__ __forceinline__ int col_span() const { return slope ? cols() - 1 : 7; }
     __device__ __forceinline__ int row(int t) const
     {
-        return slope ? wi0 - ((((t >> 3) * slope) >> 4) + (t & 7) - kTbStripAbove) : wi0 - (t >> 3);
+        return slope ? wi0 - ((((t >> sh) * slope) >> 4) + (t & ((1 << sh) - 1)) - above()) : wi0 - (t >> 3);
     }
-    __device__ __forceinline__ int col(int t) const { return slope ? wj0 - (t >> 3) : wj0 - (t & 7); }
+    __device__ __forceinline__ int col(int t) const { return slope ? wj0 - (t >> sh) : wj0 - (t & 7); }
     // cell of (r, c), or -1 outside the window
     __device__ __forceinline__ int index(int r, int c) const
     {
         const int a = wi0 - r, b = wj0 - c;
         if (slope)
         {
-            const int o = a - ((b * slope) >> 4) + kTbStripAbove;
-            return (uint32_t(b) < 16u && uint32_t(o) < 8u) ? b * 8 + o : -1;
+            const int o = a - ((b * slope) >> 4) + above();
+            return (uint32_t(b) < uint32_t(cols()) && uint32_t(o) < uint32_t(1 << sh)) ? (b << sh) + o : -1;
         }
         return (uint32_t(a) < 16u && uint32_t(b) < 8u) ? a * 8 + b : -1;
     }
@@ -1440,7 +1445,7 @@ struct TbWin
     {
         const int da = wi0 - ci, db = wj0 - cj;
         if (next && db >= 4)
-            next = min(max((16 * da + db / 2) / db, kTbSlopeMin), kTbSlopeMax);
+            next = min(max((16 * da + db / 2) / db, kTbSlopeMin), smax);
     }
     // a new window with its corner at (i, j)
     __device__ __forceinline__ void refill(int i, int j)
@@ -1449,11 +1454,15 @@ struct TbWin
         wi0   = i;
         wj0   = j;
     }
-    // strip windows start with the slope of the whole path (rows x 16 / cols)
-    __device__ __forceinline__ void init(bool strip, int rows, int cols)
+    // mode: the tb_rank bits (bit 1 strips, bit 2 32 x 4 strips); strip
+    // windows start with the slope of the whole path (rows x 16 / cols) and
+    // keep row_span() below tile_rows
+    __device__ __forceinline__ void init(int mode, int rows, int cols_, int tile_rows)
     {
-        next = !strip ? 0
-                      : (cols > 0 ? min(max((16 * rows + cols / 2) / cols, kTbSlopeMin), kTbSlopeMax) : kTbSlopeMin);
+        sh   = (mode & 4) ? 2 : 3;
+        smax = (16 * (tile_rows - (1 << sh))) / (cols() - 1);
+        next = !(mode & 2) ? 0
+                           : (cols_ > 0 ? min(max((16 * rows + cols_ / 2) / cols_, kTbSlopeMin), smax) : kTbSlopeMin);
         slope = next;
     }
 };

@@ -498,8 +498,9 @@ def test_persistent_grid_and_launch_order(mode, grid, monkeypatch):
 
 
 # Traceback move-window walk: pointer doubling and the scalar walk, over
-# strip windows along the path (default) and 16 x 8 rectangles
-# (GWAMD_TB_WALK=default | scalar | rect | scalar_rect) give identical
+# strip windows along the path (16 x 8 default, 32 x 4) and 16 x 8 rectangles
+# (GWAMD_TB_WALK=default | scalar | rect | scalar_rect | strip32 |
+# scalar_strip32) give identical
 # alignments, so identical outputs, on the full-mode LDS kernel and the banded
 # kernel (row-parallel and anti-diagonal forward), consensus and MSA, against
 # the oracle; the windows include repeats, empty/one-base reads and reads
@@ -517,7 +518,7 @@ def test_traceback_walk_modes(mode, out, monkeypatch):
     wins = [w for w in wins if max(len(r) for r in w) < ms - 60]
     msa = out == "msa"
     res = {}
-    for walk in ("rank", "scalar", "rect", "scalar_rect"):
+    for walk in ("rank", "scalar", "rect", "scalar_rect", "strip32", "scalar_strip32"):
         monkeypatch.setenv("GWAMD_TB_WALK", walk)
         b = run_gpu(wins, ms, 60, banded=banded, bw=256, output_type=out)
         assert b.kernel_variant() == {"full": 2, "band_row": 3, "band_ad": 4}[mode]
@@ -528,6 +529,8 @@ def test_traceback_walk_modes(mode, out, monkeypatch):
     assert res["rank"] == res["scalar"]
     assert res["rank"] == res["rect"]
     assert res["rank"] == res["scalar_rect"]
+    assert res["rank"] == res["strip32"]
+    assert res["rank"] == res["scalar_strip32"]
     for i, w in enumerate(wins):
         r = run_oracle(w, ms, 60, banded=banded, bw=256, msa=msa, score_bits=sbits)
         if msa:
