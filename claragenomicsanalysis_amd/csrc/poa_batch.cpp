@@ -688,6 +688,14 @@ private:
     // scalar_strip32 for parity tests and A/B runs.
     static int tb_rank_default()
     {
+        // GWAMD_TB_ABOVE=k (0-6): strip rows above the slope line (A/B runs)
+        int above_bits = 0;
+        if (const char* ab = std::getenv("GWAMD_TB_ABOVE"))
+            above_bits = (std::min(std::max(std::atoi(ab), 0), 6) + 1) << 3;
+        return tb_walk_bits() | above_bits;
+    }
+    static int tb_walk_bits()
+    {
         const char* ev = std::getenv("GWAMD_TB_WALK");
         const std::string v = ev ? ev : "";
         if (v == "scalar")

@@ -1416,7 +1416,8 @@ struct TbWin
                    // decoded cells always match the geometry they were built for)
     int sh    = 3; // strip: log2 of the rows per column (3: 16 x 8, 2: 32 x 4)
     int smax  = 0; // strip: largest slope whose strip fits the code tile
-    __device__ __forceinline__ int above() const { return sh == 3 ? 2 : 1; } // strip rows above the line
+    int ab    = 2; // strip rows above the line (room for horizontal moves)
+    __device__ __forceinline__ int above() const { return ab; }
     __device__ __forceinline__ int cols() const { return 128 >> sh; }
     // rows above wi0 the window reaches (the tile must hold wi0 - span .. wi0)
     __device__ __forceinline__ int row_span() const
@@ -1454,12 +1455,14 @@ struct TbWin
         wi0   = i;
         wj0   = j;
     }
-    // mode: the tb_rank bits (bit 1 strips, bit 2 32 x 4 strips); strip
-    // windows start with the slope of the whole path (rows x 16 / cols) and
-    // keep row_span() below tile_rows
+    // mode: the tb_rank bits (bit 1 strips, bit 2 32 x 4 strips, bits 3-5
+    // rows above the line + 1, 0: default); strip windows start with the
+    // slope of the whole path (rows x 16 / cols) and keep row_span() below
+    // tile_rows
     __device__ __forceinline__ void init(int mode, int rows, int cols_, int tile_rows)
     {
         sh   = (mode & 4) ? 2 : 3;
+        ab   = ((mode >> 3) & 7) ? min(((mode >> 3) & 7) - 1, (1 << sh) - 1) : (sh == 3 ? 2 : 1);
         smax = (16 * (tile_rows - (1 << sh))) / (cols() - 1);
         next = !(mode & 2) ? 0
                            : (cols_ > 0 ? min(max((16 * rows + cols_ / 2) / cols_, kTbSlopeMin), smax) : kTbSlopeMin);
