@@ -688,7 +688,8 @@ private:
     // scalar_strip32 for parity tests and A/B runs.
     static int tb_rank_default()
     {
-        // GWAMD_TB_ABOVE=k (0-6): strip rows above the slope line (A/B runs)
+        // GWAMD_TB_ABOVE=k (0-6): strip rows above the slope line (A/B runs;
+        // default 3)
         int above_bits = 0;
         if (const char* ab = std::getenv("GWAMD_TB_ABOVE"))
             above_bits = (std::min(std::max(std::atoi(ab), 0), 6) + 1) << 3;

@@ -1399,7 +1399,7 @@ __device__ __forceinline__ bool topsort_lds_big(WinGraph<SizeT> g, int n, GWAMD_
 //    wi0 - a, column wj0 - b.  A path leaves it after ~8 diagonal steps;
 //  * strip along the path (slope > 0, round 3): 16 columns, and in column b
 //    the 8 rows around the line a = b * slope / 16 (cell t = b * 8 + o, row
-//    wi0 - (b * slope / 16 + o - 2)); or 32 columns x 4 rows.  In topological order a
+//    wi0 - (b * slope / 16 + o - 3)); or 32 columns x 4 rows.  In topological order a
 //    diagonal move usually skips rows of other branches (on config B the
 //    path crosses ~1.5-2 rows per column), so the slope is the rows per
 //    column of the previous window's path; a path that follows it stays in
@@ -1416,7 +1416,7 @@ struct TbWin
                    // decoded cells always match the geometry they were built for)
     int sh    = 3; // strip: log2 of the rows per column (3: 16 x 8, 2: 32 x 4)
     int smax  = 0; // strip: largest slope whose strip fits the code tile
-    int ab    = 2; // strip rows above the line (room for horizontal moves)
+    int ab    = 3; // strip rows above the line (room for horizontal moves)
     __device__ __forceinline__ int above() const { return ab; }
     __device__ __forceinline__ int cols() const { return 128 >> sh; }
     // rows above wi0 the window reaches (the tile must hold wi0 - span .. wi0)
@@ -1462,7 +1462,8 @@ struct TbWin
     __device__ __forceinline__ void init(int mode, int rows, int cols_, int tile_rows)
     {
         sh   = (mode & 4) ? 2 : 3;
-        ab   = ((mode >> 3) & 7) ? min(((mode >> 3) & 7) - 1, (1 << sh) - 1) : (sh == 3 ? 2 : 1);
+        // default 3 above (16 x 8) measured best of 1-4 (profiles/r3ad_tbabove)
+        ab   = ((mode >> 3) & 7) ? min(((mode >> 3) & 7) - 1, (1 << sh) - 1) : (sh == 3 ? 3 : 1);
         smax = (16 * (tile_rows - (1 << sh))) / (cols() - 1);
         next = !(mode & 2) ? 0
                            : (cols_ > 0 ? min(max((16 * rows + cols_ / 2) / cols_, kTbSlopeMin), smax) : kTbSlopeMin);
