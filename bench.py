@@ -38,6 +38,10 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 E_STEP_WINDOWS = 6250   # config E: windows per step (20 steps = 125k windows per GPU)
+# The N > 1 default workload is config E; its like-for-like N = 1 point is
+# `bench.py --config E` (also the secondary.E object of the default N = 1 line,
+# whose headline is config B, the reference's single-batch benchmark).
+E_ANCHOR = "N=1 like-for-like point: `python bench.py --config E` (= secondary.E of the default --gpus 1 line)"
 
 ALIGNER_CONFIGS = {
     # 100k pairs x 5 kb, ~10% difference; Hirschberg-Myers
@@ -179,9 +183,14 @@ def cpu_model():
     return None
 
 
-def cpu_fields(th, used):
-    return {"cores": int(used), "threads_requested": th, "nproc": os.cpu_count(),
-            "affinity_cpus": affinity_cpus(), "cgroup_cpu_quota": cgroup_cpu_quota(), "cpu_model": cpu_model()}
+def cpu_fields(th, used, value=None):
+    """Host facts of a CPU leg; value_per_core = the leg's rate / the threads it
+    used, so a reader can scale it to the unthrottled host's core count."""
+    f = {"cores": int(used), "threads_requested": th, "nproc": os.cpu_count(),
+         "affinity_cpus": affinity_cpus(), "cgroup_cpu_quota": cgroup_cpu_quota(), "cpu_model": cpu_model()}
+    if value is not None and used:
+        f["value_per_core"] = round(value / int(used), 4)
+    return f
 
 
 def load_traffic(kind, key, n):
@@ -367,7 +376,7 @@ def bench_aligner(ctx, key, steps, warmup, args, with_cpu):
         # bases as a match on long pairs; the oracle restatement does the same
         parity["pairs_match_states_on_equal_bases"]["invariant"] = False
     cpu = None
-    if with_cpu and ctx.world == 1:
+    if with_cpu:  # rank 0, after the timed region, at every GPU count
         th = cpu_threads()
         ns = args.cpu_sample or min(n, max(th * 12, 64) if L <= 20000 else th)
         tc = time.perf_counter()
@@ -377,7 +386,7 @@ def bench_aligner(ctx, key, steps, warmup, args, with_cpu):
         cpu = dict({"value": round(ns / cpu_s, 3), "unit": "alignments/s", "kind": "port",
                     "sample": "first %d pairs of the same workload, oracle/aligner_oracle.cpp (reference-algorithm "
                               "C++ restatement, scalar DP), OpenMP one pair per thread, %.1f s wall" % (ns, cpu_s),
-                    "matches_gpu": bool(match)}, **cpu_fields(th, used))
+                    "matches_gpu": bool(match)}, **cpu_fields(th, used, ns / cpu_s))
     grid, dev_bytes = b.config()
     traffic, tsrc = load_traffic("aligner", key, n)
     return {
@@ -526,7 +535,7 @@ def bench_poa(ctx, key, steps, warmup, args, with_cpu):
             parity["pinned_by"] = ("banded: no reference banded known-answer vector; parity is HIP == IEEE-division "
                                    "oracle restatement (SURVEY 8(c) gap (i))")
     cpu = None
-    if with_cpu and ctx.world == 1:
+    if with_cpu:  # rank 0, after the timed region, at every GPU count
         th = cpu_threads()
         ns = args.cpu_sample or min(nwin, max(th * (4 if msa else 8), 64))
         tc = time.perf_counter()
@@ -548,7 +557,7 @@ def bench_poa(ctx, key, steps, warmup, args, with_cpu):
                               "C++ restatement, not SPOA), OpenMP one window per thread, %.1f s wall" % (ns, cpu_s),
                     "matches_gpu": bool(match),
                     "compared": "status, consensus, coverage" if not msa else "status, MSA rows"},
-                   **cpu_fields(th, used))
+                   **cpu_fields(th, used, ns / cpu_s))
     traffic, tsrc = load_traffic("poa", key, nwin)
     slots, resident = batch.get_grid()
     return {
@@ -614,6 +623,37 @@ def dry_rows(first_seed, n, width):
     cons = np.where(live, np.array(list(b"ACGT"), np.uint8)[(seeds[:, None] + col) % 4], 0).astype(np.uint8)
     cov = np.where(live, (seeds[:, None] * 7 + col) % 65521, 0).astype(np.uint16)
     return np.zeros(n, np.int32), clen, cons, cov
+
+
+def stream_cpu_leg(cfg, first_seed, nwin, ns, gpu=None):
+    """CPU baseline of config E: the oracle (OpenMP, one window per thread,
+    every usable host CPU) on ns windows spread evenly over the rank's stream,
+    regenerated from their seeds (so the dry run times the same work).  gpu =
+    (status, clen, cons, cov) of the rank's stream to compare, or None."""
+    from claragenomicsanalysis_amd import synth
+    from oracle import oracle
+    th = cpu_threads()
+    sidx = sorted(set(np.linspace(0, nwin - 1, min(ns, nwin)).astype(int).tolist()))
+    wins = []
+    for i in sidx:
+        b1, l1 = synth.poa_windows_packed(first_seed + i, 1, cfg["backbone"], cfg["reads"], cfg["err"], cfg["err"],
+                                          cfg["err"])
+        wins.append(windows_from_packed(b1, l1)[0])
+    tc = time.perf_counter()
+    cc, cs, cv, _, cused = oracle.poa_batch(wins, nthreads=th, max_nodes=3 * cfg["max_seq"],
+                                            max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"], coverage=True)
+    cpu_s = time.perf_counter() - tc
+    match = None
+    if gpu is not None:
+        status, clen, cons, cov = gpu
+        match = bool(all(cs[j] == status[i] and cc[j] == cons[i, :clen[i]].tobytes().decode() and
+                         list(cv[j]) == cov[i, :clen[i]].tolist() for j, i in enumerate(sidx)))
+    value = len(sidx) / cpu_s
+    return dict({"value": round(value, 3), "unit": "windows/s", "kind": "port",
+                 "sample": "%d windows spread evenly over rank 0's stream, oracle/poa_oracle.cpp (reference-algorithm "
+                           "C++ restatement, not SPOA), OpenMP one window per thread, %.1f s wall, timed on rank 0 "
+                           "after the GPU region" % (len(sidx), cpu_s),
+                 "matches_gpu": match, "compared": "status, consensus, coverage"}, **cpu_fields(th, cused, value))
 
 
 def bench_stream(ctx, key, steps, warmup, args, with_cpu):
@@ -713,14 +753,15 @@ def bench_stream(ctx, key, steps, warmup, args, with_cpu):
             parity["gathered_rows_equal_expected"] = bool(
                 np.array_equal(gst, es) and np.array_equal(glen, el) and np.array_equal(gcons, ec[:, :width]) and
                 np.array_equal(gcov, ev[:, :width]))
+        cpu = stream_cpu_leg(cfg, first_seed, nwin, args.cpu_sample or 16) if with_cpu else None
         return {"metric": "POA windows/sec (consensus)", "value": None, "unit": "windows/s", "dry_run": True,
                 "n_gpus": ctx.world, "steps": steps, "warmup": warmup, "ms_per_step": None,
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16",
                 "data": "dry run on CPU (gloo): stand-in rows, no GPU, not a measurement",
                 "config": {"workload": "config E rehearsal", "config_key": key, "windows_per_gpu": nwin,
-                           "gather_width": width, "gather_ms": gather_ms,
+                           "gather_width": width, "gather_ms": gather_ms, "anchor": E_ANCHOR,
                            "parallelism": "dp%d (windows sharded, gloo gather)" % ctx.world},
-                "roofline": None, "cpu_baseline": None, "parity": parity}
+                "roofline": None, "cpu_baseline": cpu, "parity": parity}
 
     # oracle check of a sample spread over the rank's stream (windows from every
     # batch round) and, at N > 1, of windows the other ranks computed
@@ -777,22 +818,9 @@ def bench_stream(ctx, key, steps, warmup, args, with_cpu):
                  "timing": "HIP events on each batch's stream around every launch, one clock; kernel_ms = the "
                            "union of the launch intervals (the kernels of the two batches overlap)"})
     cpu = None
-    if with_cpu and ctx.world == 1:
-        th = cpu_threads()
-        ns = args.cpu_sample or min(nwin, max(th * 8, 64))
-        sidx = sorted(set(np.linspace(0, nwin - 1, ns).astype(int).tolist()))
-        tc = time.perf_counter()
-        cc, cs, cv, _, cused = oracle.poa_batch([window_reads(i) for i in sidx], nthreads=th, max_nodes=mn,
-                                                max_consensus=2 * cfg["max_seq"], max_seqs=cfg["reads"],
-                                                coverage=True)
-        cpu_s = time.perf_counter() - tc
-        match = all(cs[j] == status[i] and cc[j] == cons[i, :clen[i]].tobytes().decode() and
-                    list(cv[j]) == cov[i, :clen[i]].tolist() for j, i in enumerate(sidx))
-        cpu = dict({"value": round(len(sidx) / cpu_s, 3), "unit": "windows/s", "kind": "port",
-                    "sample": "%d windows spread evenly over the same stream, oracle/poa_oracle.cpp "
-                              "(reference-algorithm C++ restatement, not SPOA), OpenMP one window per thread, "
-                              "%.1f s wall" % (len(sidx), cpu_s),
-                    "matches_gpu": bool(match), "compared": "status, consensus, coverage"}, **cpu_fields(th, cused))
+    if with_cpu:  # rank 0, after the timed region and the gather, at every GPU count
+        cpu = stream_cpu_leg(cfg, first_seed, nwin, args.cpu_sample or max(cpu_threads() * 8, 64),
+                             (status, clen, cons, cov))
     total = nwin * ctx.world
     return {
         "metric": "POA windows/sec (consensus)",
@@ -813,7 +841,7 @@ def bench_stream(ctx, key, steps, warmup, args, with_cpu):
                    "windows_per_batch": per_batch, "batch_rounds": rounds, "mem_per_batch": mem,
                    "batch_size": [cfg["max_seq"], cfg["reads"]], "scores": [-8, -6, 8],
                    "parallelism": "dp%d (windows sharded, RCCL gather)" % ctx.world,
-                   "windows_ok": n_ok, "dp_cells": cells_total,
+                   "windows_ok": n_ok, "dp_cells": cells_total, "anchor": E_ANCHOR,
                    "gcups": round(cells_total / (busy_ms / 1e3) / 1e9, 3),
                    "gather_ms": gather_ms, "gather_width": width, "input_gen_s": round(gen_s, 2)},
         "roofline": roof,

@@ -12,8 +12,10 @@ _LIB = None
 
 
 def library_path():
-    # GWAMD_LIBRARY: an alternative in-tree build (diagnostic builds)
-    return os.environ.get("GWAMD_LIBRARY") or os.path.join(_HERE, "lib", "libgwamd.so")
+    # GWAMD_LIBRARY: an alternative in-tree build (diagnostic builds), honoured
+    # only with GWAMD_DIAG=1 like the library's own tuning variables
+    alt = os.environ.get("GWAMD_LIBRARY") if os.environ.get("GWAMD_DIAG") == "1" else None
+    return alt or os.path.join(_HERE, "lib", "libgwamd.so")
 
 
 def load_library():
@@ -68,6 +70,8 @@ def _declare(L):
     L.gwamd_poa_get_capacity.argtypes = [vp, P(i64), P(i32)]
     L.gwamd_poa_get_grid.restype = i32
     L.gwamd_poa_get_grid.argtypes = [vp, P(i32), P(i32)]
+    L.gwamd_poa_env_tuning.restype = i32
+    L.gwamd_poa_env_tuning.argtypes = [P(i32), P(i32), P(i32), P(i32)]
     L.gwamd_poa_set_spoa_accurate.restype = i32
     L.gwamd_poa_set_spoa_accurate.argtypes = [vp, i32]
     if hasattr(L, "gwamd_aligner_create"):

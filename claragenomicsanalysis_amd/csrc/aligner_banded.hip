@@ -418,7 +418,14 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                 else
                     return uni(E[size_t(T) * nwb + lastw].sc);
                 };
-                ed = nwb <= TLE ? sweep(std::true_type{}) : sweep(std::false_type{});
+                if (nwb <= TLE)
+                    ed = sweep(std::true_type{});
+                else
+                {
+                    if (lane == 0)
+                        atomicAdd(a.stats, 1);
+                    ed = sweep(std::false_type{});
+                }
             }
             if (ed <= est || bw == Q)
                 break;

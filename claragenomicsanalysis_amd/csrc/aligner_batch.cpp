@@ -36,6 +36,26 @@ constexpr int64_t kMyersWorkspace = int64_t(64) << 30; // resident slots within 
 // LDS, register-resident sweeps of up to 4 blocks per half) up to these sizes
 constexpr int32_t kHmShortQuery  = 16384;
 constexpr int32_t kHmShortTarget = 65535;
+// Workspace slot of the full Myers aligner (always long mode): the padded
+// (word, column) matrix of pv / mv / score (128-B rows), the stripes'
+// per-column deltas, the query patterns and, past kHmLdsTarget, the target
+// letter codes; slots start on 256-B lines.
+inline int64_t myers_slot_layout(int32_t max_q, int32_t max_t, int64_t* hbuf_off, int64_t* pat_off,
+                                 int64_t* tcod_off)
+{
+    auto a16             = [](int64_t v) { return (v + 15) & ~int64_t(15); };
+    const int64_t pw     = (int64_t(max_q) + gwamd::aln::kWordBits - 1) / gwamd::aln::kWordBits;
+    const int64_t nwp    = (pw + 31) & ~int64_t(31);
+    const bool tcod_hbm  = max_t > kHmLdsTarget;
+    const int64_t hb     = a16(nwp * (int64_t(max_t) + 1) * 12 + 64);
+    const int64_t po     = a16(hb + int64_t(max_t) + 1 + gwamd::aln::kWave + 64);
+    const int64_t to     = a16(po + pw * 32 + 64);
+    const int64_t slot   = a16(to + (tcod_hbm ? (int64_t(max_t) + 15) / 16 * 4 + 64 : 0));
+    if (hbuf_off)
+        *hbuf_off = hb, *pat_off = po, *tcod_off = to;
+    return (slot + 255) & ~int64_t(255);
+}
+
 // Length limits of this implementation (include/gwamd_cudaaligner.h).
 inline void aligner_max_lengths(int32_t algo, int32_t& max_query, int32_t& max_target)
 {
@@ -279,6 +299,7 @@ public:
         dalloc(reinterpret_cast<void**>(&d_lens_), size_t(2) * max_n_ * 4);
         dalloc(reinterpret_cast<void**>(&d_paths_), size_t(max_result_) * max_n_ + 16);
         dalloc(reinterpret_cast<void**>(&d_plen_), size_t(max_n_) * 4);
+        dalloc(reinterpret_cast<void**>(&d_stats_), 16);
         // workspace: every slot entry is written before it is read
         dalloc(reinterpret_cast<void**>(&d_ws_), size_t(slots_) * size_t(slot_bytes_), false);
         h_seqs_.reserve(size_t(2) * stride_ * max_n_ + 16, stream_);
@@ -292,7 +313,7 @@ public:
     {
         (void)hipSetDevice(device_id_);
         for (void* p : {static_cast<void*>(d_seqs_), static_cast<void*>(d_lens_), static_cast<void*>(d_paths_),
-                        static_cast<void*>(d_plen_), static_cast<void*>(d_ws_)})
+                        static_cast<void*>(d_plen_), static_cast<void*>(d_ws_), static_cast<void*>(d_stats_)})
             if (p)
                 (void)hipFree(p);
     }
@@ -416,6 +437,14 @@ public:
     const int32_t* host_path_lengths() const { return h_plen_.as<int32_t>(); }
     int32_t max_result_length() const { return max_result_; }
     int32_t grid() const { return slots_; }
+    int64_t hbm_state_sweeps()
+    {
+        ScopedDevice dev(device_id_);
+        int32_t v = 0;
+        GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
+        GWAMD_HIP_CHECK(hipMemcpy(&v, d_stats_, 4, hipMemcpyDeviceToHost));
+        return v;
+    }
     int64_t device_bytes() const { return device_bytes_; }
 
 private:
@@ -437,7 +466,7 @@ private:
     // the occupancy query's answer
     void apply_grid_override()
     {
-        const char* env = std::getenv("GWAMD_ALIGNER_GRID");
+        const char* env = gwamd::host::diag_env("GWAMD_ALIGNER_GRID");
         if (!env || !*env)
             return;
         const int per_cu = std::atoi(env);
@@ -466,8 +495,17 @@ private:
             tile_bytes_      = 4096;
             int64_t want     = std::min<int64_t>(a16(int64_t(pat_words) * 16), int64_t(48) << 10);
             want             = std::min<int64_t>(want, (65536 - lds_tile_off_) & ~int64_t(511));
-            if (const char* tb = std::getenv("GWAMD_BAND_TILE_BYTES")) // parity tests: HBM chunk state
-                want = std::atoi(tb);
+            if (const char* tb = gwamd::host::diag_env("GWAMD_BAND_TILE_BYTES")) // parity tests: HBM chunk state
+            {
+                // LDS bytes for the chunk state: 4096 (256 words, the minimum
+                // tile) up to 48 KiB, in whole 512-byte steps; anything else
+                // is a typo that would silently keep the default plan
+                char* end     = nullptr;
+                const long v  = std::strtol(tb, &end, 10);
+                if (end == tb || *end != '\0' || v < 4096 || v > (48 << 10) || v % 512 != 0)
+                    throw std::invalid_argument("GWAMD_BAND_TILE_BYTES must be 4096..49152 in steps of 512");
+                want = v;
+            }
             if (want > tile_bytes_)
                 tile_bytes_ = int32_t(want);
             lds_bytes_       = lds_tile_off_ + tile_bytes_;
@@ -516,7 +554,7 @@ private:
         // GWAMD_HM_STRIPE_BLOCKS=1..4 (parity tests): long mode at any size, with
         // stripes of that many blocks, so short pairs take the striped sweeps
         stripe_blocks_ = kMaxChunks;
-        if (const char* sb = std::getenv("GWAMD_HM_STRIPE_BLOCKS"))
+        if (const char* sb = gwamd::host::diag_env("GWAMD_HM_STRIPE_BLOCKS"))
             if (hm && std::atoi(sb) >= 1 && std::atoi(sb) <= kMaxChunks)
             {
                 stripe_blocks_ = std::atoi(sb);
@@ -570,12 +608,7 @@ private:
         {
             // full matrix: pv, mv, score per (word, column), then the stripes'
             // per-column deltas, and in long mode the patterns and target codes
-            const int64_t nwp = (int64_t(pat_words) + 31) & ~int64_t(31); // 128-B rows
-            hbuf_off_   = a16(nwp * (max_t_ + 1) * 12 + 64);
-            pat_off_    = a16(hbuf_off_ + int64_t(max_t_) + 1 + kWave + 64);
-            tcod_off_   = a16(pat_off_ + (long_mode_ ? int64_t(pat_words) * 32 + 64 : 0));
-            slot_bytes_ = a16(tcod_off_ + (tcod_hbm_ ? int64_t(max_t_ + 15) / 16 * 4 + 64 : 0));
-            slot_bytes_ = (slot_bytes_ + 255) & ~int64_t(255); // slots start on whole lines
+            slot_bytes_ = gwamd::host::myers_slot_layout(max_q_, max_t_, &hbuf_off_, &pat_off_, &tcod_off_);
             if (slot_bytes_ > gwamd::host::kMyersMaxSlot)
                 throw std::invalid_argument("max_query_length x max_target_length too large for the full Myers "
                                             "aligner's score matrix (" + std::to_string(slot_bytes_) + " bytes)");
@@ -621,6 +654,7 @@ private:
         a.lds_tile_off     = lds_tile_off_;
         a.tile_bytes       = tile_bytes_;
         a.ukkonen_p        = gwamd::aln::kUkkonenP;
+        a.stats            = d_stats_;
         return a;
     }
 
@@ -647,6 +681,7 @@ private:
     int8_t* d_paths_  = nullptr;
     int32_t* d_plen_  = nullptr;
     uint8_t* d_ws_    = nullptr;
+    int32_t* d_stats_ = nullptr;
     PinnedBuf h_seqs_, h_lens_, h_paths_, h_plen_;
     std::vector<std::shared_ptr<Alignment>> alignments_;
 };
@@ -907,6 +942,37 @@ int32_t gwamd_aligner_get_config(const gwamd_aligner* a, int32_t* grid, int64_t*
     *grid         = a->impl->grid();
     *device_bytes = a->impl->device_bytes();
     return 0;
+}
+
+int32_t gwamd_aligner_get_stats(gwamd_aligner* a, int64_t* hbm_state_sweeps)
+{
+    return guarded_aln([&] {
+        *hbm_state_sweeps = a->impl->hbm_state_sweeps();
+        return int32_t(0);
+    });
+}
+
+int32_t gwamd_aligner_pair_fits(int32_t algorithm, int32_t max_query_length, int32_t max_target_length)
+{
+    if (algorithm < GWAMD_ALIGNER_HIRSCHBERG_MYERS || algorithm > GWAMD_ALIGNER_UKKONEN || max_query_length < 0 ||
+        max_target_length < 0)
+    {
+        gwamd::host::last_error() = "gwamd_aligner_pair_fits: bad algorithm or negative length";
+        return GWAMD_E_INVALID_ARGUMENT;
+    }
+    int32_t lq = 0, lt = 0;
+    gwamd::host::aligner_max_lengths(algorithm, lq, lt);
+    if (max_query_length > lq || max_target_length > lt)
+        return 0;
+    if (algorithm == GWAMD_ALIGNER_MYERS &&
+        gwamd::host::myers_slot_layout(max_query_length, max_target_length, nullptr, nullptr, nullptr) >
+            gwamd::host::kMyersMaxSlot)
+        return 0;
+    if (algorithm == GWAMD_ALIGNER_UKKONEN &&
+        (1 + int32_t(float(max_target_length) * 0.1f) + 2 * gwamd::aln::kUkkonenP + 1) / 2 >
+            gwamd::aln::kUkChunks * gwamd::aln::kWave)
+        return 0;
+    return 1;
 }
 
 int32_t gwamd_aligner_max_lengths(int32_t algorithm, int32_t* max_query, int32_t* max_target)

@@ -73,6 +73,9 @@ struct Args
     int32_t lds_tile_off;    // backtrace staging tile
     int32_t tile_bytes;
     int32_t ukkonen_p;       // AlignerGlobalUkkonen::ukkonen_p_ (aligner_global_ukkonen.cpp:29)
+    // path counters, accumulated over the aligner's launches (gwamd_aligner_get_stats):
+    // [0] banded Myers sweeps whose chunk state went through HBM
+    int32_t* stats;
 };
 
 } // namespace aln

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -20,6 +21,18 @@ namespace gwamd
 {
 namespace host
 {
+
+// Tuning and diagnostic switches (GWAMD_POA_KERNEL, GWAMD_TB_WALK,
+// GWAMD_BAND_FWD, ...): read only when GWAMD_DIAG=1 is set, so a drop-in
+// user's environment never changes which kernel runs.  The parity tests set
+// GWAMD_DIAG=1 (tests/conftest.py).  GWAMD_SPOA_ACCURATE is not one of them:
+// it is the runtime form of the reference's spoa_accurate build option.
+inline bool diag_enabled()
+{
+    const char* d = std::getenv("GWAMD_DIAG");
+    return d && d[0] == '1' && d[1] == '\0';
+}
+inline const char* diag_env(const char* name) { return diag_enabled() ? std::getenv(name) : nullptr; }
 
 // Per-thread message of the last failed C ABI call (gwamd_last_error()).
 inline std::string& last_error()

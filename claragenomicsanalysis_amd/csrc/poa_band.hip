@@ -1470,7 +1470,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
                     rc = topsort_racon_wave<SizeT>(g, nc, cscore, cpred, 4 * d.max_nodes, lane,
                                                    (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off);
                 else if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, (GWAMD_LDS int*)(shb),
-                                             lane, tsprof) &&
+                                             lane, tsprof, (d.diag & 1) != 0) &&
                          !topsort_lds_big<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, lane))
                 {
                     if (lane == 0)

@@ -153,6 +153,7 @@ public:
             dims_.spoa_accurate = std::atoi(sa) != 0 ? 1 : 0;
         plan_lds_kernel();
         plan_band_kernel();
+        dims_.diag = diag_bits();
         // this build's footprint: graph + inputs + outputs per window, and the
         // forward/traceback scratch per slot.  The LDS and banded kernels run
         // a persistent grid of as many workgroups as are resident at once, so
@@ -167,7 +168,7 @@ public:
             GWAMD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
             resident = int64_t(gwamd_internal_poa_blocks_per_cu(&dims_, score_bits_, size_bits_, banded_ ? 1 : 0,
                                                                 msa ? 1 : 0)) * cus;
-            if (const char* ev = std::getenv("GWAMD_POA_SLOTS")) // diagnostic: a smaller persistent grid
+            if (const char* ev = gwamd::host::diag_env("GWAMD_POA_SLOTS")) // diagnostic: a smaller persistent grid
                 if (std::atoi(ev) > 0)
                     resident = std::min<int64_t>(resident > 0 ? resident : INT32_MAX, std::atoi(ev));
             if (resident > 0 && own_cap > resident)
@@ -268,7 +269,7 @@ public:
         bufs_.head  = nullptr;
         int cus     = 0;
         GWAMD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
-        if (const char* ev = std::getenv("GWAMD_LAUNCH_ORDER_CUS")) // diagnostic: plan for fewer CUs
+        if (const char* ev = gwamd::host::diag_env("GWAMD_LAUNCH_ORDER_CUS")) // diagnostic: plan for fewer CUs
             if (std::atoi(ev) > 0)
                 cus = std::atoi(ev);
         const int n           = poa_count_;
@@ -613,7 +614,7 @@ private:
     void plan_lds_kernel()
     {
         dims_.lds_kernel = 0;
-        const char* env  = std::getenv("GWAMD_POA_KERNEL");
+        const char* env  = gwamd::host::diag_env("GWAMD_POA_KERNEL");
         if (env && std::string(env) == "v1")
             return;
         if (banded_ || score_bits_ != 16 || size_bits_ != 16)
@@ -628,7 +629,7 @@ private:
         const int ms = dims_.max_seq_len;
         if (ms > 512)
             nw = 2;
-        if (const char* sh = std::getenv("GWAMD_POA_LDS_SHAPE"))
+        if (const char* sh = gwamd::host::diag_env("GWAMD_POA_LDS_SHAPE"))
         {
             int c = 0, n = 0;
             if (std::sscanf(sh, "%d,%d", &c, &n) == 2)
@@ -651,7 +652,7 @@ private:
         int64_t xl_cap       = std::max<int64_t>(1024, (target - fixed) / 2);
         xl_cap               = std::min<int64_t>(xl_cap, 65535);
         int64_t total        = fixed + a16(xl_cap * 2);
-        if (const char* pad = std::getenv("GWAMD_POA_LDS_PAD")) // diagnostic: fewer windows per CU
+        if (const char* pad = gwamd::host::diag_env("GWAMD_POA_LDS_PAD")) // diagnostic: fewer windows per CU
             total += a16(std::atoi(pad));
         if (total > 65536)
             return;
@@ -686,18 +687,26 @@ private:
     // columns x 4 rows (else 16 x 8).  Default: pointer doubling over 16 x 8
     // strips; GWAMD_TB_WALK=scalar | rect | scalar_rect | strip32 |
     // scalar_strip32 for parity tests and A/B runs.
+public:
     static int tb_rank_default()
     {
         // GWAMD_TB_ABOVE=k (0-6): strip rows above the slope line (A/B runs;
         // default 3)
         int above_bits = 0;
-        if (const char* ab = std::getenv("GWAMD_TB_ABOVE"))
+        if (const char* ab = gwamd::host::diag_env("GWAMD_TB_ABOVE"))
             above_bits = (std::min(std::max(std::atoi(ab), 0), 6) + 1) << 3;
         return tb_walk_bits() | above_bits;
     }
+    // Dims::diag: bit 0 forces the Kahn sort's ring of queued words
+    // (GWAMD_TOPSORT_RING=1, ring-mode parity tests)
+    static int diag_bits()
+    {
+        const char* r = gwamd::host::diag_env("GWAMD_TOPSORT_RING");
+        return (r && std::atoi(r) != 0) ? 1 : 0;
+    }
     static int tb_walk_bits()
     {
-        const char* ev = std::getenv("GWAMD_TB_WALK");
+        const char* ev = gwamd::host::diag_env("GWAMD_TB_WALK");
         const std::string v = ev ? ev : "";
         if (v == "scalar")
             return 2;
@@ -712,11 +721,12 @@ private:
         return 3;
     }
 
+private:
     void plan_band_kernel()
     {
         if (!banded_ || dims_.lds_kernel)
             return;
-        const char* env = std::getenv("GWAMD_POA_KERNEL");
+        const char* env = gwamd::host::diag_env("GWAMD_POA_KERNEL");
         if (env && std::string(env) == "v1")
             return;
         const int bw = dims_.band_width;
@@ -740,7 +750,7 @@ private:
         // GWAMD_BAND_FWD=ad|row forces it on (planning for it) or off.
         const int64_t ad_b    = a16(int64_t(gwamd::poa::kAdRing) * rowsz * sbytes + gwamd::poa::kWave * sbytes) +
                              a16(mn / 8 + 64); // + the real-row bitmap
-        const char* fwd_env   = std::getenv("GWAMD_BAND_FWD");
+        const char* fwd_env   = gwamd::host::diag_env("GWAMD_BAND_FWD");
         // (band widths 128 / 256 only: its ring of kAdRing rows is too large beyond)
         const bool force_ad   = fwd_env && std::string(fwd_env) == "ad" && cpl <= 4;
         const bool no_ad      = fwd_env && std::string(fwd_env) == "row";
@@ -765,7 +775,7 @@ private:
         dims_.lds_kernel     = 3;
         // the pass runs kAdMaxWaves waves per window: one window per CU
         int ad_waves = gwamd::poa::kAdMaxWaves;
-        if (const char* ev = std::getenv("GWAMD_BAND_AD_WAVES")) // diagnostic: fewer waves per window
+        if (const char* ev = gwamd::host::diag_env("GWAMD_BAND_AD_WAVES")) // diagnostic: fewer waves per window
             ad_waves = std::max(1, std::min(gwamd::poa::kAdMaxWaves, std::atoi(ev)));
         dims_.band_ad        = (!no_ad && cpl <= 4 && chosen_per_cu == 1 && work >= ad_b) ? ad_waves : 0;
         dims_.tb_rank        = tb_rank_default();
@@ -1412,6 +1422,22 @@ int32_t gwamd_poa_get_types(const gwamd_poa_batch* batch, int32_t* score_bits, i
     *score_bits = batch->impl->score_bits();
     *size_bits  = batch->impl->size_bits();
     return batch->impl->kernel_kind();
+}
+
+int32_t gwamd_poa_env_tuning(int32_t* tb_rank, int32_t* band_fwd, int32_t* force_v1, int32_t* diag)
+{
+    if (!tb_rank || !band_fwd || !force_v1 || !diag)
+    {
+        gwamd::host::last_error() = "gwamd_poa_env_tuning: NULL output";
+        return GWAMD_E_INVALID_ARGUMENT;
+    }
+    *tb_rank            = claraparabricks::genomeworks::cudapoa::PoaBatch::tb_rank_default();
+    const char* fwd     = gwamd::host::diag_env("GWAMD_BAND_FWD");
+    *band_fwd           = !fwd ? 0 : (std::string(fwd) == "ad" ? 1 : (std::string(fwd) == "row" ? 2 : 0));
+    const char* kern    = gwamd::host::diag_env("GWAMD_POA_KERNEL");
+    *force_v1           = kern && std::string(kern) == "v1" ? 1 : 0;
+    *diag               = claraparabricks::genomeworks::cudapoa::PoaBatch::diag_bits();
+    return 0;
 }
 
 int32_t gwamd_poa_set_spoa_accurate(gwamd_poa_batch* batch, int32_t on)

@@ -1281,7 +1281,8 @@ __global__ void __launch_bounds__(kWave * NW, NW >= 4 ? 4 : 1) poa_window_kernel
                         rc = topsort_racon_wave<SizeT>(g, nc, cscore, cpred, 4 * d.max_nodes, lane,
                                                        (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off);
                     // scratch: the read and the ring (both free after the add)
-                    else if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, AX.sh, lane) &&
+                    else if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, AX.sh, lane, nullptr,
+                                                       (d.diag & 1) != 0) &&
                              !topsort_lds_big<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, lane))
                     {
                         if (lane == 0)

@@ -1122,7 +1122,8 @@ __device__ __forceinline__ int topsort_racon_wave(WinGraph<SizeT> g, int n, int3
 // offsets must fit 16 bits.
 template <typename SizeT>
 __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS uint8_t* scratch, int scratch_bytes,
-                                            GWAMD_LDS int* sh, int lane, uint64_t* prof = nullptr)
+                                            GWAMD_LDS int* sh, int lane, uint64_t* prof = nullptr,
+                                            bool force_ring = false)
 {
     g = as_global(g);
 #ifdef GWAMD_TOPSORT_PROFILE
@@ -1188,12 +1189,18 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
     // then one LDS read instead of two dependent ones
     const int qinfo_off          = (head_bytes + ebase * 2 + 15) & ~15;
     // (all n of them, or for graphs too large for that a ring of the last
-    // kQRing pushes: a pop at q reads the ring while tail - q <= kQRing, the
-    // node word otherwise; the queue holds about the graph's width)
+    // kQRing pushes: a pop at q reads the ring while tail - q < kQRing, the
+    // node word otherwise; the queue holds about the graph's width.
+    // force_ring: Dims::diag bit 0, parity tests of the ring mode with a
+    // 4-entry ring: ordinary windows queue 5-6 nodes at once, so they run
+    // past it)
     constexpr int kQRing = 1024;
-    const int q_mode     = uniform(qinfo_off + (n + 1) * 4 <= scratch_bytes ? 1 : (qinfo_off + kQRing * 4 <= scratch_bytes ? 2 : 0));
+    const int qring      = force_ring ? 4 : kQRing;
+    const int q_mode     = uniform((qinfo_off + (n + 1) * 4 <= scratch_bytes && !force_ring)
+                                       ? 1
+                                       : (qinfo_off + qring * 4 <= scratch_bytes ? 2 : 0));
     const bool use_q     = q_mode != 0;
-    const uint32_t qmask = q_mode == 2 ? uint32_t(kQRing - 1) : 0xffffffffu;
+    const uint32_t qmask = q_mode == 2 ? uint32_t(qring - 1) : 0xffffffffu;
     GWAMD_LDS uint32_t* qinfo    = (GWAMD_LDS uint32_t*)(scratch + qinfo_off);
     // sources in id order
     int k = 0;
@@ -1224,10 +1231,13 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
     auto fifo = [&](auto useq_tag) -> int {
         constexpr int kMode = decltype(useq_tag)::value; // 0 node words, 1 all queued words, 2 ring
         // (a VGPR value, made uniform where it is used, so the read stays in
-        // flight next to the pop's own successor read)
+        // flight next to the pop's own successor read).  Ring mode: every pop
+        // stores at slot tail & (qring-1), released or not, so the entry at
+        // qq is intact only while no position qq + qring has been written,
+        // i.e. while tail - qq < qring.
         auto pop_info = [&](int qq, int tl) -> uint32_t {
-            if (kMode == 1 || (kMode == 2 && tl - qq <= kQRing))
-                return qinfo[uint32_t(qq) & (kMode == 2 ? uint32_t(kQRing - 1) : 0xffffffffu)];
+            if (kMode == 1 || (kMode == 2 && tl - qq < qring))
+                return qinfo[uint32_t(qq) & qmask];
             return info[int(queue[qq])];
         };
         int tail       = uniform(k);

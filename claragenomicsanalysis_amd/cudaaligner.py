@@ -48,6 +48,10 @@ def _declare(L):
     L.gwamd_aligner_get_config.argtypes = [vp, P(i32), P(i64)]
     L.gwamd_aligner_max_lengths.restype = i32
     L.gwamd_aligner_max_lengths.argtypes = [i32, P(i32), P(i32)]
+    L.gwamd_aligner_pair_fits.restype = i32
+    L.gwamd_aligner_pair_fits.argtypes = [i32, i32, i32]
+    L.gwamd_aligner_get_stats.restype = i32
+    L.gwamd_aligner_get_stats.argtypes = [vp, P(i64)]
     del i8
 
 
@@ -222,6 +226,13 @@ class CudaAlignerBatch:
         paths = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int8)), shape=(max(n, 1) * stride.value,))
         lens = np.ctypeslib.as_array(C.cast(ln, C.POINTER(C.c_int32)), shape=(max(n, 1),))
         return paths[:n * stride.value].reshape(n, stride.value).copy(), lens[:n].copy()
+
+    def stats(self):
+        """Path counters accumulated over this aligner's launches
+        (gwamd_aligner_get_stats)."""
+        v = C.c_int64()
+        _check(self._lib.gwamd_aligner_get_stats(self._handle, C.byref(v)))
+        return {"hbm_state_sweeps": v.value}
 
     def config(self):
         g, b = C.c_int32(), C.c_int64()

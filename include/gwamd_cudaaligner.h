@@ -22,6 +22,8 @@
  *                                 (AlignmentImpl over given states,        alignment_impl.cpp:75-112)
  *   gwamd_alignment_cigar         Alignment::convert_to_cigar              alignment_impl.cpp:47-73
  *   gwamd_aligner_max_lengths     (none: this implementation's length limits)
+ *   gwamd_aligner_pair_fits       (none: whether a (query, target) limit pair is accepted)
+ *   gwamd_aligner_get_stats       (none: path counters for the parity tests)
  *
  * Extra entry points (bench.py): split align_all into upload / launch /
  * download and read the raw device paths.
@@ -115,6 +117,19 @@ int32_t gwamd_aligner_get_config(const gwamd_aligner* aligner, int32_t* grid, in
  * *max_target receive the query and target limits (Ukkonen: the largest
  * target for which any query passes). */
 int32_t gwamd_aligner_max_lengths(int32_t algorithm, int32_t* max_query, int32_t* max_target);
+
+/* Whether gwamd_aligner_create(algorithm, max_query_length,
+ * max_target_length, ...) passes this implementation's length checks: the
+ * two limits of gwamd_aligner_max_lengths are not jointly valid for full
+ * Myers (its (word, column) matrix of one pair must fit a 32 GiB slot, about
+ * Q * T <= 9e10) nor for Ukkonen (band rows).  1 fits, 0 does not, or
+ * GWAMD_E_INVALID_ARGUMENT. */
+int32_t gwamd_aligner_pair_fits(int32_t algorithm, int32_t max_query_length, int32_t max_target_length);
+
+/* Path counters of this aligner, accumulated over its launches:
+ * *hbm_state_sweeps = banded Myers band sweeps whose 32-word chunk state went
+ * through HBM (bands wider than the LDS chunk-state region). */
+int32_t gwamd_aligner_get_stats(gwamd_aligner* aligner, int64_t* hbm_state_sweeps);
 
 #ifdef __cplusplus
 }

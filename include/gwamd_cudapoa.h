@@ -127,6 +127,13 @@ int32_t gwamd_poa_get_types(const gwamd_poa_batch* batch, int32_t* score_bits, i
  * generate_poa; returns the previous setting.  Default: the GWAMD_SPOA_ACCURATE
  * environment variable at create time (off when unset). */
 int32_t gwamd_poa_set_spoa_accurate(gwamd_poa_batch* batch, int32_t on);
+/* Kernel tuning a batch created now would take from the environment (no
+ * reference counterpart).  The GWAMD_* tuning variables are read only when
+ * GWAMD_DIAG=1; otherwise this reports the defaults: *tb_rank = traceback
+ * walk bits (3: pointer doubling over strips), *band_fwd = 0 (plan decides;
+ * 1 anti-diagonal forced, 2 row-parallel forced), *force_v1 = 0, *diag = 0.
+ * Host only, needs no GPU. */
+int32_t gwamd_poa_env_tuning(int32_t* tb_rank, int32_t* band_fwd, int32_t* force_v1, int32_t* diag);
 /* Device bytes allocated by the batch and its window capacity (max_poas). */
 int32_t gwamd_poa_get_capacity(const gwamd_poa_batch* batch, int64_t* device_bytes, int32_t* max_poas);
 

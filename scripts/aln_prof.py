@@ -9,6 +9,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+os.environ["GWAMD_DIAG"] = "1"
 os.environ["GWAMD_LIBRARY"] = os.path.join(ROOT, "claragenomicsanalysis_amd", "lib", "alnprof", "libgwamd.so")
 import torch  # noqa: E402,F401  (HIP runtime first)
 from claragenomicsanalysis_amd import synth  # noqa: E402

@@ -23,7 +23,7 @@ LONG = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "aligner
 OALGO = {"hirschberg_myers": oracle.ALIGN_HM, "myers": oracle.ALIGN_MYERS, "myers_banded": oracle.ALIGN_MYERS_BANDED}
 
 
-def gpu_states(pairs, algorithm, max_q=None, max_t=None):
+def gpu_states(pairs, algorithm, max_q=None, max_t=None, stats=None):
     mq = max_q or max(len(q) for q, _ in pairs)
     mt = max_t or max(len(t) for _, t in pairs)
     b = CudaAlignerBatch(mq, mt, len(pairs), algorithm=algorithm)
@@ -32,6 +32,8 @@ def gpu_states(pairs, algorithm, max_q=None, max_t=None):
     b.align_all()
     b.sync_alignments()
     paths, plen = b.raw_paths()
+    if stats is not None:
+        stats.update(b.stats())
     return [paths[i, :plen[i]][::-1].tolist() for i in range(len(pairs))], mq
 
 
@@ -101,9 +103,18 @@ def test_myers_banded_chunk_state_in_hbm(monkeypatch):
     rng = random.Random(41)
     t = rand_seq(rng, 12000)
     pairs = [(mutate(rng, t, 0.45), t), (rand_seq(rng, 11000), t)]
-    got, mq = gpu_states(pairs, "myers_banded")
+    st = {}
+    got, mq = gpu_states(pairs, "myers_banded", stats=st)
+    # the sweeps really took the HBM chunk state (not the LDS path)
+    assert st["hbm_state_sweeps"] >= len(pairs)
     for (q, tt), g in zip(pairs, got):
         assert g == oracle.align(q, tt, oracle.ALIGN_MYERS_BANDED, mq)
+
+
+def test_band_tile_bytes_checked(monkeypatch):
+    monkeypatch.setenv("GWAMD_BAND_TILE_BYTES", "4k")
+    with pytest.raises(ValueError):
+        CudaAlignerBatch(1000, 1000, 1, algorithm="myers_banded")
 
 
 def _reference_pair(c):

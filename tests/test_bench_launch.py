@@ -40,6 +40,12 @@ def test_gpus_2_launches_two_ranks_and_gathers_both():
     assert par["gathered_rows_equal_expected"] is True
     assert par["gathered_rank0_rows_equal_local"] is True
     assert par["gathered_all_status_ok"] is True
+    # the N > 1 line carries the CPU leg (rank 0, after the GPU region) with a
+    # per-core rate, and names its like-for-like N = 1 point
+    cpu = line["cpu_baseline"]
+    assert cpu is not None and cpu["value"] > 0 and cpu["unit"] == "windows/s"
+    assert cpu["value_per_core"] > 0 and cpu["cores"] >= 1
+    assert "--config E" in line["config"]["anchor"]
 
 
 def test_gpus_3_uneven_world():

@@ -85,3 +85,44 @@ def test_aligner_length_limits_are_queryable(built):
     assert max_lengths("myers_banded") == (65536, 65536)
     q, t = max_lengths("ukkonen")
     assert q == 65535 and 8000 < t < 8300
+
+
+def test_tuning_env_ignored_without_diag_switch(built, monkeypatch):
+    # the GWAMD_* tuning variables change the kernel plan
+    # only with GWAMD_DIAG=1, so a drop-in user's environment cannot
+    import ctypes as C
+    from claragenomicsanalysis_amd import load_library
+    L = load_library()
+
+    def tuning():
+        v = [C.c_int32() for _ in range(4)]
+        assert L.gwamd_poa_env_tuning(*[C.byref(x) for x in v]) == 0
+        return tuple(x.value for x in v)
+
+    monkeypatch.setenv("GWAMD_TB_WALK", "scalar")
+    monkeypatch.setenv("GWAMD_BAND_FWD", "row")
+    monkeypatch.setenv("GWAMD_POA_KERNEL", "v1")
+    monkeypatch.setenv("GWAMD_TOPSORT_RING", "1")
+    monkeypatch.delenv("GWAMD_DIAG", raising=False)
+    assert tuning() == (3, 0, 0, 0)  # defaults: pointer doubling over strips, plan decides
+    monkeypatch.setenv("GWAMD_DIAG", "0")
+    assert tuning() == (3, 0, 0, 0)
+    monkeypatch.setenv("GWAMD_DIAG", "1")
+    assert tuning() == (2, 2, 1, 1)
+
+
+def test_aligner_pair_fits(built):
+    # the two limits of max_lengths are not jointly valid for full Myers
+    # (one pair's matrix must fit a 32 GiB slot): pair_fits says which are
+    from claragenomicsanalysis_amd import load_library
+    from claragenomicsanalysis_amd.cudaaligner import ALGORITHMS
+    L = load_library()
+    fits = lambda a, q, t: L.gwamd_aligner_pair_fits(ALGORITHMS[a], q, t)
+    assert fits("myers", 65536, 65536) == 1
+    assert fits("myers", 1 << 24, 1 << 24) == 0
+    assert fits("myers", 1 << 24, 5000) == 1
+    assert fits("hirschberg_myers", 1 << 24, 1 << 24) == 1
+    assert fits("myers_banded", 65536, 65536) == 1
+    assert fits("myers_banded", 65537, 100) == 0
+    assert fits("ukkonen", 5000, 5000) == 1
+    assert L.gwamd_aligner_pair_fits(ALGORITHMS["myers"], -1, 5) < 0

@@ -538,3 +538,30 @@ def test_traceback_walk_modes(mode, out, monkeypatch):
         else:
             cons, cov, st = res["rank"]
             assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), i
+
+
+# Kahn sort ring of queued info words (topsort_lds kMode 2, graphs whose
+# words do not all fit LDS): GWAMD_TOPSORT_RING=1 forces it with a 4-entry
+# ring; these windows queue 5-6 nodes at once (oracle graphs), so pops run
+# past the ring and must fall back to the node words (a pop read a
+# slot the branch-free pop had overwritten)
+@pytest.mark.parametrize("mode", ["full", "banded", "full_msa", "banded_msa"])
+def test_topsort_queue_ring(mode, monkeypatch):
+    monkeypatch.setenv("GWAMD_TOPSORT_RING", "1")
+    banded = mode.startswith("banded")
+    msa = mode.endswith("msa")
+    wins = synth.poa_windows(7, 6, 300, 32, 40, 40, 40)
+    max_seq = 400
+    b = run_gpu(wins, max_seq, 32, banded=banded, output_type="msa" if msa else "consensus")
+    sbits = b.get_types()[0]
+    if msa:
+        got, st = b.get_msa()
+    else:
+        cons, cov, st = b.get_consensus()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, max_seq, 32, banded=banded, msa=msa, score_bits=sbits)
+        assert st[i] == r.status, i
+        if msa:
+            assert got[i] == r.msa, i
+        else:
+            assert (cons[i], cov[i]) == (r.consensus, r.coverage), i
