@@ -59,6 +59,11 @@ ALIGNER_CONFIGS = {
     # (main.cpp:85-124, 140-158): per-pair seeds here, target truncated to 65,536
     "D_myers_64k": dict(pairs=32, length=65536, algorithm="myers", recipe="BM_SingleBatchAlignment"),
     "D_banded_64k": dict(pairs=32, length=65536, algorithm="myers_banded", recipe="BM_SingleBatchAlignment"),
+    "D_ukkonen_64k": dict(pairs=32, length=65536, algorithm="ukkonen", recipe="BM_SingleBatchAlignment"),
+    # Ukkonen with bands wider than one wave (ukkonen_wide_kernel): 16 kb targets,
+    # queries ~1,400 bases shorter (200 substitutions, 100 insertions, 1,500
+    # deletions), i.e. ~800-row bands within the aligner's 10 % rule
+    "D_ukkonen_wide_16k": dict(pairs=1024, length=16384, algorithm="ukkonen", recipe="length_difference"),
 }
 
 # per algorithm: oracle id, dominant kernel
@@ -294,7 +299,10 @@ def bench_aligner(ctx, key, steps, warmup, args, with_cpu):
     n, L = cfg["pairs"], cfg["length"]
     t0 = time.time()
     recipe = cfg.get("recipe")
-    if recipe:
+    if recipe == "length_difference":
+        qs, ts = synth.pairs(1 + ctx.rank * n, n, L, L, 200, 100, 1500)
+        recipe = None
+    elif recipe:
         # the reference benchmark's pair: query = the random genome, target =
         # its 10 %-difference copy (L/30 substitutions, insertions, deletions)
         e = L // 30

@@ -750,6 +750,235 @@ __global__ void __launch_bounds__(kWave) ukkonen_kernel(Args a)
     }
 }
 
+// ---------------------------------------------------------------------------
+// Ukkonen for bands wider than one wave's kUkChunks * 64 rows (targets past
+// ~8.2 kb at the 10 % rule): the reference's own shape, one workgroup of up
+// to 1,024 threads per pair with row k on thread k % NT (ukkonen_compute_
+// score_matrix loops k += blockDim.x, ukkonen_gpu.cu:145-185,213-257), here
+// with at most kUkWideChunks rows per thread in registers.  Per anti-diagonal
+// column l: the k-1 / k+1 neighbours of column l-1 come from the lane's
+// neighbour by DPP, across 64-row groups from a double-buffered LDS edge
+// array written in the previous column; one workgroup barrier per column.
+// Cells, initial values, the int16 store and the backtrace tie order are the
+// single-wave kernel's (ukkonen_kernel above).  The backtrace runs on wave 0
+// over KT x LT tiles of the (k, l) matrix staged in LDS (the sequences'
+// region, no longer needed then).
+__global__ void __launch_bounds__(1024) ukkonen_wide_kernel(Args a)
+{
+    extern __shared__ __align__(16) uint8_t lds[];
+    const int tid           = threadIdx.x;
+    const int NT            = blockDim.x;
+    const int lane          = tid & (kWave - 1);
+    const int wave          = tid / kWave;
+    const int nwv           = NT / kWave;
+    GWAMD_LDS uint8_t* base = (GWAMD_LDS uint8_t*)(lds);
+    GWAMD_LDS uint8_t* sA   = base + a.lds_target_off; // along i (the shorter sequence)
+    GWAMD_LDS uint8_t* sB   = base + a.lds_seq2_off;   // along j
+    // edge values of column l-1 per 64-row group g: [parity][0: row 64g, 1: row 64g+63][group]
+    GWAMD_LDS int* edge     = (GWAMD_LDS int*)(base + a.lds_edge_off);
+    constexpr int kG        = kUkWideChunks * 16;
+    GWAMD_LDS int16_t* tile = (GWAMD_LDS int16_t*)(base + a.lds_tile_off);
+    int16_t* S              = reinterpret_cast<int16_t*>(a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes));
+    const int p             = a.ukkonen_p;
+    constexpr int M         = kUkMax;
+
+    for (int idx = blockIdx.x; idx < a.n; idx += gridDim.x)
+    {
+        const int Q = uni(a.lens[2 * idx]);
+        const int T = uni(a.lens[2 * idx + 1]);
+        const char* qs = a.seqs + size_t(2 * idx) * a.stride;
+        const char* ts = a.seqs + size_t(2 * idx + 1) * a.stride;
+        int m = Q + 1, n = T + 1;
+        int8_t ins = kInsertion, del = kDeletion;
+        const bool swp = m > n;
+        if (swp)
+        {
+            m   = T + 1;
+            n   = Q + 1;
+            ins = kDeletion;
+            del = kInsertion;
+        }
+        const char* A = swp ? ts : qs;
+        const char* B = swp ? qs : ts;
+        for (int k = tid; k < m - 1; k += NT)
+            sA[k] = uint8_t(A[k]);
+        for (int k = tid; k < n - 1; k += NT)
+            sB[k] = uint8_t(B[k]);
+        // column -1 (never a source of a computed cell, as in ukkonen_kernel)
+        for (int e = tid; e < 4 * kG; e += NT)
+            edge[e] = M;
+        __syncthreads();
+        const int bw        = (1 + n - m + 2 * p + 1) / 2;
+        const int cols      = n + m;
+        const int kmax_odd  = (n - m + 2 * p - 1) / 2 + 1;
+        const int kmax_even = (n - m + 2 * p) / 2 + 1;
+        const int nck       = uni((bw + NT - 1) / NT); // <= kUkWideChunks (host plan)
+        if (tid == 0)
+            atomicAdd(a.stats + 1, 1);
+
+        int V1[kUkWideChunks], V2[kUkWideChunks], V0[kUkWideChunks];
+#pragma unroll
+        for (int c = 0; c < kUkWideChunks; c++)
+        {
+            V1[c] = M;
+            V2[c] = M;
+        }
+        for (int l = 0; l < cols; l++)
+        {
+            const bool even        = ((l - p) & 1) == 0;
+            const int kmax         = even ? kmax_even : kmax_odd;
+            GWAMD_LDS int* e_prev  = edge + ((l + 1) & 1) * 2 * kG; // column l-1
+            GWAMD_LDS int* e_cur   = edge + (l & 1) * 2 * kG;       // column l
+#pragma unroll
+            for (int c = 0; c < kUkWideChunks; c++)
+            {
+                if (c < nck)
+                {
+                    const int k    = c * NT + tid;
+                    const int g    = c * nwv + wave; // 64-row group of k
+                    const int j    = k - (p + l) / 2 + l;
+                    const int i    = l - j;
+                    const int d    = even ? 2 * k : 2 * k + 1;
+                    const int lmin = d >= p ? d - p : p - d;
+                    const int lmax = d <= p ? 2 * (m - p + d) + lmin : 2 * min(m, n - d + p) + lmin;
+                    const bool cmp = k < kmax && k < bw && l >= lmin + 1 && l < lmax;
+                    int lo         = dpp_from_lower(V1[c]);
+                    int hi         = dpp_from_upper(V1[c]);
+                    if (lane == 0)
+                        lo = g > 0 ? e_prev[kG + g - 1] : M; // row 64g - 1
+                    if (lane == kWave - 1)
+                        hi = g + 1 < kG ? e_prev[g + 1] : M; // row 64g + 64
+                    const int ii  = cmp ? i - 1 : 0;
+                    const int jj  = cmp ? j - 1 : 0;
+                    const int ca  = sA[ii];
+                    const int cb  = sB[jj];
+                    const int dgv = l < 2 ? M : V2[c] + (ca == cb ? 0 : 1);
+                    int left, above;
+                    if (even)
+                    {
+                        left  = k - 1 < 0 ? M : lo + 1;
+                        above = V1[c] + 1;
+                    }
+                    else
+                    {
+                        left  = V1[c] + 1;
+                        above = k + 1 >= bw ? M : hi + 1;
+                    }
+                    const int init = i == 0 ? j : (j == 0 ? i : M);
+                    const int v    = cmp ? min(dgv, min(left, above)) : init;
+                    V0[c]          = int(int16_t(v));
+                    if (k < bw)
+                        S[size_t(k) + size_t(bw) * l] = int16_t(v);
+                    if (lane == 0)
+                        e_cur[g] = V0[c];
+                    if (lane == kWave - 1)
+                        e_cur[kG + g] = V0[c];
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < kUkWideChunks; c++)
+            {
+                V2[c] = V1[c];
+                V1[c] = V0[c];
+            }
+            __syncthreads();
+        }
+        // the matrix stores of every wave before wave 0 reads them back
+        __threadfence();
+        __syncthreads();
+        if (wave == 0)
+        {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            constexpr int KT = kUkTileRows, LT = kUkTileCols;
+            int tk0 = INT_MIN / 2, tl0 = INT_MIN / 2;
+            // rows [k - KT/2, k + KT/2) x columns [l - LT + 1, l], band edges as M
+            auto refill = [&](int kc, int lc) {
+                tk0 = kc - KT / 2;
+                tl0 = lc - LT + 1;
+                wave_sync();
+                constexpr int kPer = KT * LT / kWave, kB = 8;
+                for (int e0 = 0; e0 < kPer; e0 += kB)
+                {
+                    int16_t v[kB];
+#pragma unroll
+                    for (int u = 0; u < kB; u++)
+                    {
+                        const int e   = (e0 + u) * kWave + lane;
+                        const int kk  = tk0 + e % KT;
+                        const int ll  = tl0 + e / KT;
+                        const bool ok = kk >= 0 && kk < bw && ll >= 0 && ll < cols;
+                        v[u]          = S[ok ? size_t(kk) + size_t(bw) * ll : 0];
+                        v[u]          = ok ? v[u] : int16_t(M);
+                    }
+#pragma unroll
+                    for (int u = 0; u < kB; u++)
+                        tile[(e0 + u) * kWave + lane] = v[u];
+                }
+                wave_sync();
+            };
+            auto val = [&](int i, int j) -> int {
+                const int k = (j - i + p) / 2;
+                const int l = j + i;
+                if (k < 0 || k >= bw || l < 0 || l >= cols)
+                    return M;
+                if (k >= tk0 && k < tk0 + KT && l >= tl0 && l < tl0 + LT)
+                    return int(tile[(l - tl0) * KT + (k - tk0)]);
+                return int(S[size_t(k) + size_t(bw) * l]);
+            };
+            PathWriter pw{a.paths + size_t(idx) * a.max_path_length, a.max_path_length};
+            int i = m - 1, j = n - 1;
+            refill((j - i + p) / 2, i + j);
+            int s = uni(val(i, j));
+            // lane 0: above (i-1, j), lane 1: diagonal (i-1, j-1), lane 2: left (i, j-1)
+            const int di = lane == 2 ? 0 : 1;
+            const int dj = lane == 0 ? 0 : 1;
+            while (i > 0 && j > 0)
+            {
+                i = uni(i);
+                j = uni(j);
+                {
+                    // the three neighbours inside the tile, or refill around (k, l)
+                    const int kc = (j - i + p) / 2, lc = i + j;
+                    if (lc - 2 < tl0 || lc > tl0 + LT - 1 || kc - 1 < tk0 || kc + 1 >= tk0 + KT)
+                        refill(kc, lc);
+                }
+                const int v     = val(i - di, j - dj);
+                const int above = uni(__builtin_amdgcn_readlane(v, 0));
+                const int dg    = uni(__builtin_amdgcn_readlane(v, 1));
+                const int left  = uni(__builtin_amdgcn_readlane(v, 2));
+                int8_t r;
+                if (left + 1 == s)
+                {
+                    r = ins;
+                    s = left;
+                    --j;
+                }
+                else if (above + 1 == s)
+                {
+                    r = del;
+                    s = above;
+                    --i;
+                }
+                else
+                {
+                    r = dg == s ? kMatch : kMismatch;
+                    s = dg;
+                    --i;
+                    --j;
+                }
+                pw.put(r, lane);
+            }
+            pw.finish(lane);
+            pw.fill(del, i, lane);
+            pw.fill(ins, j, lane);
+            if (lane == 0)
+                a.path_len[idx] = pw.overflow ? -1 : pw.pos;
+        }
+        // the tile aliases the sequences: the next pair's copy waits for wave 0
+        __syncthreads();
+    }
+}
+
 } // namespace aln
 } // namespace gwamd
 
@@ -760,8 +989,30 @@ extern "C" hipError_t gwamd_internal_banded_launch(const gwamd::aln::Args* a, in
         return hipSuccess;
     if (algo == 2)
         hipLaunchKernelGGL(myers_banded_kernel, dim3(grid), dim3(kWave), size_t(a->lds_bytes), stream, *a);
+    else if (a->uk_threads > 0)
+    {
+        if (a->uk_threads % kWave != 0 || a->uk_threads > 1024)
+            return hipErrorInvalidValue;
+        if (a->lds_bytes > 65536)
+        {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(ukkonen_wide_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, a->lds_bytes);
+            if (e != hipSuccess)
+                return e;
+        }
+        hipLaunchKernelGGL(ukkonen_wide_kernel, dim3(grid), dim3(a->uk_threads), size_t(a->lds_bytes), stream, *a);
+    }
     else
+    {
+        if (a->lds_bytes > 65536)
+        {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(ukkonen_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, a->lds_bytes);
+            if (e != hipSuccess)
+                return e;
+        }
         hipLaunchKernelGGL(ukkonen_kernel, dim3(grid), dim3(kWave), size_t(a->lds_bytes), stream, *a);
+    }
     return hipGetLastError();
 }
 
@@ -771,5 +1022,26 @@ extern "C" hipError_t gwamd_internal_banded_occupancy(int algo, int lds_bytes, i
     if (algo == 2)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, myers_banded_kernel, kWave,
                                                             size_t(lds_bytes));
+    if (lds_bytes > 65536)
+    {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(ukkonen_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+        if (e != hipSuccess)
+            return e;
+    }
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ukkonen_kernel, kWave, size_t(lds_bytes));
+}
+
+extern "C" hipError_t gwamd_internal_ukkonen_wide_occupancy(int threads, int lds_bytes, int* blocks_per_cu)
+{
+    using namespace gwamd::aln;
+    if (lds_bytes > 65536)
+    {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(ukkonen_wide_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+        if (e != hipSuccess)
+            return e;
+    }
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, ukkonen_wide_kernel, threads,
+                                                        size_t(lds_bytes));
 }

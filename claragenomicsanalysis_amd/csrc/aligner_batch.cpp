@@ -80,15 +80,12 @@ inline void aligner_max_lengths(int32_t algo, int32_t& max_query, int32_t& max_t
         max_target = 65536;
         break;
     default:
-    {
-        // Ukkonen: (1 + int(0.1f * T) + 2p + 1) / 2 band rows, at most kUkChunks * 64
-        max_query = 65535;
-        int32_t t = 0;
-        while (t < 65535 && (1 + int32_t(float(t + 1) * 0.1f) + 2 * gwamd::aln::kUkkonenP + 1) / 2 <=
-                                gwamd::aln::kUkChunks * gwamd::aln::kWave)
-            t++;
-        max_target = t;
-    }
+        // Ukkonen: both sequences in LDS (ukkonen_wide_kernel: up to 2 x 64 KiB
+        // of its 160 KiB), (1 + int(0.1f * T) + 2p + 1) / 2 = 3,377 band rows
+        // at 65,536, within kUkWideChunks x 1,024; the reference benchmark's
+        // largest size (cudaaligner/benchmarks/main.cpp:140-143)
+        max_query  = 65536;
+        max_target = 65536;
     }
 }
 } // namespace host
@@ -98,6 +95,7 @@ extern "C" hipError_t gwamd_internal_align_launch(const gwamd::aln::Args* a, int
 extern "C" hipError_t gwamd_internal_align_occupancy(int algo, int lds_bytes, int* blocks_per_cu);
 extern "C" hipError_t gwamd_internal_banded_launch(const gwamd::aln::Args* a, int algo, int grid, hipStream_t stream);
 extern "C" hipError_t gwamd_internal_banded_occupancy(int algo, int lds_bytes, int* blocks_per_cu);
+extern "C" hipError_t gwamd_internal_ukkonen_wide_occupancy(int threads, int lds_bytes, int* blocks_per_cu);
 
 namespace claraparabricks
 {
@@ -263,13 +261,13 @@ public:
         // limits of this implementation (aligner_max_lengths; the reference has
         // none): the Myers state of a query segment is register-resident
         // (4 blocks of 64x32 bits), segment coordinates and split scores are
-        // 16-bit, the Ukkonen band has at most 512 diagonals
+        // 16-bit, the Ukkonen band has at most 4,096 diagonals
         int32_t lim_q = 0, lim_t = 0;
         gwamd::host::aligner_max_lengths(algo_, lim_q, lim_t);
         if (max_q_ > lim_q)
             throw std::invalid_argument("max_query_length above " + std::to_string(lim_q) +
                                         " is not supported by this aligner.");
-        if (algo_ == GWAMD_ALIGNER_UKKONEN && ukkonen_band_rows() > gwamd::aln::kUkChunks * gwamd::aln::kWave)
+        if (algo_ == GWAMD_ALIGNER_UKKONEN && ukkonen_band_rows() > gwamd::aln::kUkWideChunks * 1024)
             throw std::invalid_argument("max_target_length too large for the Ukkonen aligner's band.");
         if (max_t_ > lim_t)
             throw std::invalid_argument("max_target_length above " + std::to_string(lim_t) +
@@ -346,6 +344,7 @@ public:
             std::memcpy(td, target, size_t(target_length));
         h_lens_.as<int32_t>()[2 * n]     = query_length;
         h_lens_.as<int32_t>()[2 * n + 1] = target_length;
+        max_diff_ = std::max(max_diff_, std::abs(query_length - target_length));
         auto a = std::make_shared<AlignmentImpl>(qd, query_length, td, target_length);
         a->set_alignment_type(AlignmentType::global_alignment);
         alignments_.push_back(a);
@@ -399,7 +398,11 @@ public:
     }
 
     const std::vector<std::shared_ptr<Alignment>>& get_alignments() const override { return alignments_; }
-    void reset() override { alignments_.clear(); }
+    void reset() override
+    {
+        alignments_.clear();
+        max_diff_ = 0;
+    }
 
     // bench / C ABI helpers
     void upload()
@@ -414,6 +417,18 @@ public:
     {
         ScopedDevice dev(device_id_);
         gwamd::aln::Args a = args();
+        if (algo_ == GWAMD_ALIGNER_UKKONEN)
+        {
+            // the widest band of this batch decides the Ukkonen kernel (plan_banded)
+            const int rows = (1 + max_diff_ + 2 * gwamd::aln::kUkkonenP + 1) / 2;
+            if (rows > gwamd::aln::kUkChunks * gwamd::aln::kWave)
+            {
+                a.uk_threads   = std::min(1024, (rows + gwamd::aln::kWave - 1) / gwamd::aln::kWave * gwamd::aln::kWave);
+                a.lds_bytes    = uk_wide_lds_;
+                a.lds_tile_off = 0;
+                a.tile_bytes   = gwamd::aln::kUkTileRows * gwamd::aln::kUkTileCols * 2;
+            }
+        }
         const int grid     = std::min<int>(int(alignments_.size()), slots_);
         if (algo_ == GWAMD_ALIGNER_MYERS_BANDED || algo_ == GWAMD_ALIGNER_UKKONEN)
             GWAMD_HIP_CHECK(gwamd_internal_banded_launch(&a, algo_, grid, stream_));
@@ -437,13 +452,14 @@ public:
     const int32_t* host_path_lengths() const { return h_plen_.as<int32_t>(); }
     int32_t max_result_length() const { return max_result_; }
     int32_t grid() const { return slots_; }
-    int64_t hbm_state_sweeps()
+    void path_stats(int64_t* out)
     {
         ScopedDevice dev(device_id_);
-        int32_t v = 0;
+        int32_t v[2] = {0, 0};
         GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
-        GWAMD_HIP_CHECK(hipMemcpy(&v, d_stats_, 4, hipMemcpyDeviceToHost));
-        return v;
+        GWAMD_HIP_CHECK(hipMemcpy(v, d_stats_, 8, hipMemcpyDeviceToHost));
+        out[0] = v[0];
+        out[1] = v[1];
     }
     int64_t device_bytes() const { return device_bytes_; }
 
@@ -514,19 +530,40 @@ private:
         }
         else
         {
-            lds_target_off_  = 0;
-            lds_seq2_off_    = int32_t(a16(stride_ + 16));
-            lds_tile_off_    = int32_t(lds_seq2_off_ + a16(stride_ + 16));
-            tile_bytes_      = 8192; // 4096 int16 >= 3 columns of 512 band rows
-            lds_bytes_       = lds_tile_off_ + tile_bytes_;
-            // int16 (k, l) matrix: band rows x (n + m) columns
-            slot_bytes_ = a16(int64_t(ukkonen_band_rows()) * (int64_t(max_q_) + max_t_ + 2) * 2 + 64);
+            // Ukkonen.  The band of a pair is (1 + |n - m| + 2p + 1) / 2 rows;
+            // the workspace is sized for the largest allowed difference, but
+            // each launch runs the single-wave kernel (ukkonen_kernel, up to
+            // kUkChunks * 64 rows) when every pair of the batch fits it, and
+            // the workgroup kernel (ukkonen_wide_kernel, up to 1,024 threads
+            // of kUkWideChunks rows, as calc_good_blockdim, ukkonen_gpu.cu:
+            // 268-273) otherwise.  Both keep the sequences in LDS; the wide
+            // kernel's backtrace tile reuses them.
+            const int rows      = ukkonen_band_rows();
+            lds_target_off_     = 0;
+            lds_seq2_off_       = int32_t(a16(stride_ + 16));
+            const int64_t seqs  = lds_seq2_off_ + a16(stride_ + 16);
+            uk_narrow_tile_off_ = int32_t(seqs);
+            uk_narrow_lds_      = int32_t(seqs + 8192); // 4096 int16 >= 3 columns of 512 band rows
+            lds_edge_off_       = int32_t(std::max<int64_t>(seqs, kUkTileRows * kUkTileCols * 2));
+            uk_wide_lds_        = lds_edge_off_ + 4 * kUkWideChunks * 16 * 4;
+            slot_bytes_         = a16(int64_t(rows) * (int64_t(max_q_) + max_t_ + 2) * 2 + 64);
+            lds_bytes_          = uk_narrow_lds_;
+            tile_bytes_         = 8192;
+            lds_tile_off_       = uk_narrow_tile_off_;
         }
-        if (lds_bytes_ > 65536)
+        if (lds_bytes_ > (algo_ == GWAMD_ALIGNER_UKKONEN ? 163840 : 65536) ||
+            (algo_ == GWAMD_ALIGNER_UKKONEN && uk_wide_lds_ > 163840))
             throw std::invalid_argument("aligner problem size does not fit in LDS");
         pat_words_ = pat_words;
         int per_cu = 1, cus = 1;
         GWAMD_HIP_CHECK(gwamd_internal_banded_occupancy(algo_, lds_bytes_, &per_cu));
+        if (algo_ == GWAMD_ALIGNER_UKKONEN && ukkonen_band_rows() > kUkChunks * kWave)
+        {
+            // batches with wide bands run one workgroup per pair
+            int wide = 1;
+            GWAMD_HIP_CHECK(gwamd_internal_ukkonen_wide_occupancy(1024, uk_wide_lds_, &wide));
+            per_cu = std::max(per_cu, wide);
+        }
         GWAMD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
         slots_ = std::max(1, per_cu * cus);
         slots_ = int32_t(std::max<int64_t>(1, std::min<int64_t>(slots_, ws_cap / slot_bytes_)));
@@ -654,6 +691,8 @@ private:
         a.lds_tile_off     = lds_tile_off_;
         a.tile_bytes       = tile_bytes_;
         a.ukkonen_p        = gwamd::aln::kUkkonenP;
+        a.uk_threads       = 0; // launch(): the batch's widest band may need ukkonen_wide_kernel
+        a.lds_edge_off     = lds_edge_off_;
         a.stats            = d_stats_;
         return a;
     }
@@ -674,6 +713,8 @@ private:
     bool long_mode_    = false;
     int32_t stripe_blocks_ = gwamd::aln::kMaxChunks;
     int32_t lds_seq2_off_ = 0, lds_tile_off_ = 0, tile_bytes_ = 0;
+    int32_t lds_edge_off_ = 0, uk_narrow_tile_off_ = 0, uk_narrow_lds_ = 0, uk_wide_lds_ = 0;
+    int32_t max_diff_ = 0; // largest |query - target| of the batch
     int32_t slots_ = 1;
     int64_t slot_bytes_ = 0, device_bytes_ = 0;
     char* d_seqs_     = nullptr;
@@ -944,10 +985,13 @@ int32_t gwamd_aligner_get_config(const gwamd_aligner* a, int32_t* grid, int64_t*
     return 0;
 }
 
-int32_t gwamd_aligner_get_stats(gwamd_aligner* a, int64_t* hbm_state_sweeps)
+int32_t gwamd_aligner_get_stats(gwamd_aligner* a, int64_t* hbm_state_sweeps, int64_t* ukkonen_wide_pairs)
 {
     return guarded_aln([&] {
-        *hbm_state_sweeps = a->impl->hbm_state_sweeps();
+        int64_t v[2];
+        a->impl->path_stats(v);
+        *hbm_state_sweeps   = v[0];
+        *ukkonen_wide_pairs = v[1];
         return int32_t(0);
     });
 }
@@ -970,7 +1014,7 @@ int32_t gwamd_aligner_pair_fits(int32_t algorithm, int32_t max_query_length, int
         return 0;
     if (algorithm == GWAMD_ALIGNER_UKKONEN &&
         (1 + int32_t(float(max_target_length) * 0.1f) + 2 * gwamd::aln::kUkkonenP + 1) / 2 >
-            gwamd::aln::kUkChunks * gwamd::aln::kWave)
+            gwamd::aln::kUkWideChunks * 1024)
         return 0;
     return 1;
 }

@@ -23,7 +23,10 @@ constexpr int kLeafCols   = 128; // base-case columns kept in LDS (larger leaves
 constexpr int kSplitLds   = 512; // split segments up to this many columns keep their scores in LDS
 constexpr int kLeafColBytes = 20; // per column: pv u64, mv u64, score i32
 constexpr int kChunkWords  = 32;  // banded Myers: one reference warp of 32 words per step (myers_gpu.cu:35)
-constexpr int kUkChunks    = 8;   // Ukkonen: band rows k held 64 per chunk, up to 512
+constexpr int kUkChunks    = 8;   // Ukkonen: band rows k held 64 per chunk, up to 512 (one wave)
+constexpr int kUkWideChunks = 4;  // wider bands: rows per thread of a workgroup of up to 1,024 (4,096 rows)
+constexpr int kUkTileRows  = 64;  //   backtrace tile: band rows x
+constexpr int kUkTileCols  = 128; //   anti-diagonal columns (int16, 16 KiB)
 constexpr int kUkkonenP    = 100; // aligner_global_ukkonen.cpp:29
 constexpr int16_t kUkMax   = 32766; // numeric_limits<int16_t>::max() - 1 (ukkonen_gpu.cu:75)
 
@@ -73,8 +76,11 @@ struct Args
     int32_t lds_tile_off;    // backtrace staging tile
     int32_t tile_bytes;
     int32_t ukkonen_p;       // AlignerGlobalUkkonen::ukkonen_p_ (aligner_global_ukkonen.cpp:29)
+    int32_t uk_threads;      // Ukkonen: > 0 runs ukkonen_wide_kernel with this many threads per pair
+    int32_t lds_edge_off;    //   its 64-row-group edge values (2 x 2 x kUkWideChunks*16 int)
     // path counters, accumulated over the aligner's launches (gwamd_aligner_get_stats):
-    // [0] banded Myers sweeps whose chunk state went through HBM
+    // [0] banded Myers sweeps whose chunk state went through HBM, [1] pairs
+    // aligned by ukkonen_wide_kernel
     int32_t* stats;
 };
 

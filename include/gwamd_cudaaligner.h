@@ -112,10 +112,9 @@ int32_t gwamd_aligner_get_config(const gwamd_aligner* aligner, int32_t* grid, in
  * std::invalid_argument (GWAMD_E_INVALID_ARGUMENT) above them.  Hirschberg-
  * Myers and full Myers: 2^24 bases each (full Myers also needs one pair's
  * score matrix, 0.375 B per cell, within a 32 GiB workspace slot); banded
- * Myers: 65,536 each (patterns and target codes in LDS); Ukkonen: target
- * 65535 and a band of at most 512 diagonals.  *max_query and
- * *max_target receive the query and target limits (Ukkonen: the largest
- * target for which any query passes). */
+ * Myers and Ukkonen: 65,536 each (sequences, or patterns and target codes,
+ * in LDS; Ukkonen bands up to 4,096 rows).  *max_query and *max_target
+ * receive the query and target limits. */
 int32_t gwamd_aligner_max_lengths(int32_t algorithm, int32_t* max_query, int32_t* max_target);
 
 /* Whether gwamd_aligner_create(algorithm, max_query_length,
@@ -128,8 +127,10 @@ int32_t gwamd_aligner_pair_fits(int32_t algorithm, int32_t max_query_length, int
 
 /* Path counters of this aligner, accumulated over its launches:
  * *hbm_state_sweeps = banded Myers band sweeps whose 32-word chunk state went
- * through HBM (bands wider than the LDS chunk-state region). */
-int32_t gwamd_aligner_get_stats(gwamd_aligner* aligner, int64_t* hbm_state_sweeps);
+ * through HBM (bands wider than the LDS chunk-state region);
+ * *ukkonen_wide_pairs = Ukkonen pairs aligned by the workgroup kernel (batches
+ * whose widest band exceeds one wave's 512 rows). */
+int32_t gwamd_aligner_get_stats(gwamd_aligner* aligner, int64_t* hbm_state_sweeps, int64_t* ukkonen_wide_pairs);
 
 #ifdef __cplusplus
 }

@@ -19,7 +19,8 @@ sys.path.insert(0, ROOT)
 from claragenomicsanalysis_amd import synth  # noqa: E402
 from oracle import oracle  # noqa: E402
 
-ALGO = {"hirschberg_myers": oracle.ALIGN_HM, "myers": oracle.ALIGN_MYERS, "myers_banded": oracle.ALIGN_MYERS_BANDED}
+ALGO = {"hirschberg_myers": oracle.ALIGN_HM, "myers": oracle.ALIGN_MYERS, "myers_banded": oracle.ALIGN_MYERS_BANDED,
+        "ukkonen": oracle.ALIGN_UKKONEN}
 
 
 def reference_pair(size, truncate):
@@ -52,13 +53,21 @@ def case(name, recipe, size, truncate, algo):
 
 
 def main():
-    cases = []
-    cases.append(case("BM_SingleAlignment 100000 (main.cpp:33-60)", "BM_SingleAlignment", 100000, False,
-                      "hirschberg_myers"))
-    for algo in ("hirschberg_myers", "myers", "myers_banded"):
-        cases.append(case("BM_SingleBatchAlignment 65536, first pair (main.cpp:85-124)", "BM_SingleBatchAlignment",
-                          65536, True, algo))
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "aligner_long.json")
+    # cases already in the file are kept (the 100 kb Hirschberg-Myers oracle run is slow)
+    have = {}
+    if os.path.exists(out):
+        for c in json.load(open(out))["cases"]:
+            have[(c["recipe"], c["size"], c["algorithm"])] = c
+    want = [("BM_SingleAlignment 100000 (main.cpp:33-60)", "BM_SingleAlignment", 100000, False, "hirschberg_myers")]
+    for algo in ("hirschberg_myers", "myers", "myers_banded", "ukkonen"):
+        want.append(("BM_SingleBatchAlignment 65536, first pair (main.cpp:85-124)", "BM_SingleBatchAlignment",
+                     65536, True, algo))
+    # Ukkonen between one wave's 512-row band and the 65,536 case (BM_SingleBatchAlignment
+    # sizes 512 x 4^k: 16,384 needs a 920-row band)
+    want.append(("BM_SingleBatchAlignment 16384, first pair (main.cpp:85-124)", "BM_SingleBatchAlignment",
+                 16384, True, "ukkonen"))
+    cases = [have.get((w[1], w[2], w[4])) or case(*w) for w in want]
     json.dump({"generator": "tests/golden/make_aligner_long.py", "oracle": "oracle/aligner_oracle.cpp",
                "cases": cases}, open(out, "w"), indent=1)
 

@@ -132,3 +132,36 @@ def test_reference_benchmark_pairs_golden(c):
     assert len(p) == c["path_length"]
     assert [sum(1 for x in p if x == k) for k in range(4)] == c["counts"]
     assert hashlib.sha256(bytes(p)).hexdigest() == c["path_sha256"]
+
+
+# Ukkonen bands wider than one wave (ukkonen_wide_kernel): the reference runs
+# any band with up to 1,024 threads per pair (ukkonen_gpu.cu:213-293); pairs
+# whose length differs by up to 10 % of the target at 12 kb and 18 kb need
+# 700-1,000 band rows, a 30 kb one 1,600
+@pytest.mark.parametrize("T", [12000, 18000, 30000])
+def test_ukkonen_wide_band_matches_oracle(T):
+    rng = random.Random(T)
+    t = rand_seq(rng, T)
+    d = int(T * 0.1) - 3
+    q1 = mutate(rng, t, 0.04)[: T - d]              # query shorter by ~10 %
+    q2 = mutate(rng, t, 0.08)[: T - d // 2] + "ACGT"
+    q3 = t + rand_seq(rng, d // 3)                  # query longer (swapped roles)
+    pairs = [(q1, t), (q2, t), (q3, t)]
+    st = {}
+    got, mq = gpu_states(pairs, "ukkonen", max(len(q) for q, _ in pairs), T, stats=st)
+    assert st["ukkonen_wide_pairs"] == len(pairs)
+    for (q, tt), g in zip(pairs, got):
+        assert g == oracle.align(q, tt, oracle.ALIGN_UKKONEN, mq), (len(q), len(tt))
+
+
+def test_ukkonen_narrow_batch_keeps_single_wave_kernel():
+    # a 16 kb aligner (wide workspace) whose pairs all have narrow bands runs
+    # the single-wave kernel (stats: no wide pairs), same paths as the oracle
+    rng = random.Random(5)
+    t = rand_seq(rng, 16000)
+    pairs = [(mutate(rng, t, 0.05)[:15990], t), (t[:15900], t)]
+    st = {}
+    got, mq = gpu_states(pairs, "ukkonen", 16000, 16000, stats=st)
+    assert st["ukkonen_wide_pairs"] == 0
+    for (q, tt), g in zip(pairs, got):
+        assert g == oracle.align(q, tt, oracle.ALIGN_UKKONEN, mq)

@@ -83,8 +83,9 @@ def test_aligner_length_limits_are_queryable(built):
     assert max_lengths("hirschberg_myers") == (1 << 24, 1 << 24)
     assert max_lengths("myers") == (1 << 24, 1 << 24)  # and the pair's matrix within one 32 GiB slot
     assert max_lengths("myers_banded") == (65536, 65536)
-    q, t = max_lengths("ukkonen")
-    assert q == 65535 and 8000 < t < 8300
+    # Ukkonen: bands up to 4,096 rows (ukkonen_wide_kernel), the reference
+    # benchmark's 65,536 bp (main.cpp:140-143)
+    assert max_lengths("ukkonen") == (65536, 65536)
 
 
 def test_tuning_env_ignored_without_diag_switch(built, monkeypatch):
@@ -125,4 +126,7 @@ def test_aligner_pair_fits(built):
     assert fits("myers_banded", 65536, 65536) == 1
     assert fits("myers_banded", 65537, 100) == 0
     assert fits("ukkonen", 5000, 5000) == 1
+    assert fits("ukkonen", 18432, 18432) == 1
+    assert fits("ukkonen", 65536, 65536) == 1
+    assert fits("ukkonen", 65537, 100) == 0
     assert L.gwamd_aligner_pair_fits(ALGORITHMS["myers"], -1, 5) < 0
