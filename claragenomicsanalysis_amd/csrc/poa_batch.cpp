@@ -698,11 +698,13 @@ public:
         return tb_walk_bits() | above_bits;
     }
     // Dims::diag: bit 0 forces the Kahn sort's ring of queued words
-    // (GWAMD_TOPSORT_RING=1, ring-mode parity tests)
+    // (GWAMD_TOPSORT_RING=1, ring-mode parity tests); bit 1 keeps the LDS
+    // kernel on the round-3 forward pass (GWAMD_POA_FWD=v1, A/B runs)
     static int diag_bits()
     {
         const char* r = gwamd::host::diag_env("GWAMD_TOPSORT_RING");
-        return (r && std::atoi(r) != 0) ? 1 : 0;
+        const char* f = gwamd::host::diag_env("GWAMD_POA_FWD");
+        return ((r && std::atoi(r) != 0) ? 1 : 0) | ((f && std::string(f) == "v1") ? 2 : 0);
     }
     static int tb_walk_bits()
     {

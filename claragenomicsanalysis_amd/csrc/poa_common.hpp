@@ -92,7 +92,8 @@ struct Dims
     int32_t aux_rece_off;   //   | row records e (u32)
     int32_t band_ad;        // banded kernel: waves of the anti-diagonal forward pass (0: row-parallel pass)
     int32_t tb_rank;        // traceback move windows (TbWin): bit 0 pointer-doubling walk, bit 1 strips, bit 2 32 x 4 strips
-    int32_t diag;           // diagnostic switches (GWAMD_DIAG=1 only): bit 0 Kahn sort queued words in a ring
+    int32_t diag;           // diagnostic switches (GWAMD_DIAG=1 only): bit 0 Kahn sort queued words in a ring,
+                            // bit 1 LDS kernel on the round-3 forward pass
 };
 
 // LDS bytes of the pointer-doubling traceback walk (walk_window_ranked)

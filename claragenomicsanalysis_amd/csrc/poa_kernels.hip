@@ -17,6 +17,7 @@
 
 #include <climits>
 #include <cstdint>
+#include <type_traits>
 
 #include "poa_wave.hpp"
 
@@ -280,11 +281,19 @@ __device__ void build_row_program(WinGraph<SizeT> g, int V, uint32_t* rec, uint1
             if (valid)
             {
                 uint32_t v = uint32_t(base[u]) | (uint32_t(oc[u] == 0 ? 1 : 0) << 14);
+                // bit 7 (bases are ASCII): the forward pass must take its
+                // general path (nw_forward_lds_v2): a source, a predecessor
+                // beyond the ring, an escaped list or a base other than ACGT
+                const uint32_t ub = uint32_t(base[u]);
+                bool slow = n == 0 || !((ub & 0xc0u) == 0x40u && ((0x10008aull >> (ub & 0x3fu)) & 1u));
                 if (n == 1)
                 {
                     v |= (1u << 8) | (uint32_t(r - p0[u]) << 16);
                     if (r - p0[u] >= ring_rows)
+                    {
                         flags[p0[u]] = 1;
+                        slow         = true;
+                    }
                 }
                 else if (n >= 2)
                 {
@@ -296,11 +305,15 @@ __device__ void build_row_program(WinGraph<SizeT> g, int V, uint32_t* rec, uint1
                         if (fit)
                             xl[off + k] = uint16_t(pk);
                         if (r - pk >= ring_rows)
+                        {
                             flags[pk] = 1;
+                            slow      = true;
+                        }
                     }
                     v |= fit ? (uint32_t(n) << 8) | (uint32_t(off) << 16) : (kRecEscape << 8);
+                    slow = slow || !fit;
                 }
-                rec[r] = v;
+                rec[r] = v | (slow ? 0x80u : 0u);
             }
             xbase += total;
         }
@@ -614,7 +627,7 @@ __device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, con
             const uint32_t rec = rec_c;
             const int np       = np_c;
             const int pv       = pv_c;
-            const int base     = int(rec & 0xff);
+            const int base     = int(rec & 0x7f); // bit 7: general-path flag (build_row_program)
             const bool spill_r = (rec >> 15) & 1;
             int16_t* row       = ring + (r & mask) * ring_stride;
             const bool anyfar  = __builtin_amdgcn_ballot_w64(lane < np && pv != 0 && r - pv > mask) != 0;
@@ -1122,6 +1135,8 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
     return n;
 }
 
+#include "poa_fwd2.hpp"
+
 // LDS-resident POA kernel: one workgroup of NW waves per window.  The forward
 // pass and the traceback tile loads use every wave; the serial phases (graph
 // update, topological sort, consensus, MSA) run on wave 0 while the other
@@ -1194,6 +1209,13 @@ __global__ void __launch_bounds__(kWave * NW, NW >= 4 ? 4 : 1) poa_window_kernel
 
     PhaseTimer ph;
     FwdProf fp;
+    // round-4 forward pass unless the scores do not fit its byte table (or
+    // Dims::diag bit 1, GWAMD_POA_FWD=v1 under GWAMD_DIAG, asks for round 3's)
+#ifdef GWAMD_FWD_PROFILE
+    const bool use_v2 = false;
+#else
+    const bool use_v2 = fwd2_ok(sc) && !(d.diag & 2);
+#endif
     const WindowDesc wd = b.windows[w];
     const int nseq      = wd.num_seqs;
     int status          = kSuccess;
@@ -1236,8 +1258,17 @@ __global__ void __launch_bounds__(kWave * NW, NW >= 4 ? 4 : 1) poa_window_kernel
             __syncthreads();
             ph.lap<kPhRowProg>();
             cells += int64_t(V + 1) * (L + 1);
-            const int end_row = nw_forward_lds_pk<CPL, NW, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride,
-                                                                  codes, d.code_stride, sc, shb, carry, tid, fp);
+            int end_row;
+            // (the diagnostic 24- and 32-column shapes keep the round-3 pass)
+            if constexpr (CPL <= 16)
+                end_row = use_v2 ? nw_forward_lds_v2<CPL, NW, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride,
+                                                                     codes, d.code_stride, sc, shb, carry, tid,
+                                                                     d.lds_xl_cap)
+                                 : nw_forward_lds_pk<CPL, NW, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride,
+                                                                     codes, d.code_stride, sc, shb, carry, tid, fp);
+            else
+                end_row = nw_forward_lds_pk<CPL, NW, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride, codes,
+                                                            d.code_stride, sc, shb, carry, tid, fp);
             __syncthreads();
             ph.lap<kPhForward>();
             if (wave == 0)
