@@ -46,15 +46,82 @@ __device__ __forceinline__ int wave_incl_max_b(int v)
     return v;
 }
 
+// LDS pointer from a flat pointer into the LDS image (its low 32 bits), with
+// no null check (an addrspacecast adds one; the backend miscompiled that
+// pattern here).  The row loop addresses the ring, the read and the row
+// program through these and the code and spill rows through global
+// pointers, so no access is a flat one: a flat access counts against the LDS
+// counter too, and every LDS wait would then wait for the HBM code stores.
+template <typename T>
+__device__ __forceinline__ GWAMD_LDS T* lds_of(T* p)
+{
+    return (GWAMD_LDS T*)(uintptr_t)(uint32_t)(uintptr_t)(p);
+}
+
+#define GWAMD_GLB __attribute__((address_space(1)))
+// builtin vectors (HIP's uint4 is a class whose copy does not take a
+// qualified address space)
+typedef unsigned int fwd_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int fwd_u32x2 __attribute__((ext_vector_type(2)));
+
+template <int NR>
+__device__ __forceinline__ void load_row_glb(const GWAMD_GLB int16_t* p, uint32_t (&P)[NR], uint32_t& prev)
+{
+    static_assert(NR % 4 == 0 || NR == 2, "4 or a multiple of 8 cells per lane");
+    if constexpr (NR % 4 == 0)
+    {
+#pragma unroll
+        for (int q = 0; q < NR / 4; q++)
+        {
+            const fwd_u32x4 v = *reinterpret_cast<const GWAMD_GLB fwd_u32x4*>(p + 1 + 8 * q);
+            P[4 * q] = v.x, P[4 * q + 1] = v.y, P[4 * q + 2] = v.z, P[4 * q + 3] = v.w;
+        }
+    }
+    else
+    {
+        const fwd_u32x2 v = *reinterpret_cast<const GWAMD_GLB fwd_u32x2*>(p + 1);
+        P[0] = v.x, P[1] = v.y;
+    }
+    prev = uint32_t(uint16_t(p[0]));
+}
+
+template <int NR>
+__device__ __forceinline__ void load_row_lds(const GWAMD_LDS int16_t* p, uint32_t (&P)[NR], uint32_t& prev)
+{
+    static_assert(NR % 4 == 0 || NR == 2, "4 or a multiple of 8 cells per lane");
+    if constexpr (NR % 4 == 0)
+    {
+#pragma unroll
+        for (int q = 0; q < NR / 4; q++)
+        {
+            const fwd_u32x4 v = *reinterpret_cast<const GWAMD_LDS fwd_u32x4*>(p + 1 + 8 * q);
+            P[4 * q] = v.x, P[4 * q + 1] = v.y, P[4 * q + 2] = v.z, P[4 * q + 3] = v.w;
+        }
+    }
+    else
+    {
+        const fwd_u32x2 v = *reinterpret_cast<const GWAMD_LDS fwd_u32x2*>(p + 1);
+        P[0] = v.x, P[1] = v.y;
+    }
+    prev = uint32_t(uint16_t(p[0]));
+}
+
 template <int CPL, int NW, bool FIRST, bool FEED, typename SizeT>
-__device__ __forceinline__ void fwd2_rows(WinGraph<SizeT> g, const RowProg& P, int V, const uint8_t* read, int L,
-                                          int16_t* ring, int ring_stride, int16_t* spill, int stride,
-                                          uint8_t* codes, int code_stride, const Scores sc,
-                                          GWAMD_LDS uint8_t* shb, int16_t* carry_hbm, int lane, int wave, int cb,
+__device__ __forceinline__ void fwd2_rows(WinGraph<SizeT> g, const RowProg& P, int V, const uint8_t* read_f, int L,
+                                          int16_t* ring_f, int ring_stride, int16_t* spill_f, int stride,
+                                          uint8_t* codes_f, int code_stride, const Scores sc,
+                                          GWAMD_LDS uint8_t* shb, int16_t* carry_f, int lane, int wave, int cb,
                                           bool to_hbm, bool from_hbm, bool owner, int xl_cap, int& best_row,
                                           int& best_val)
 {
     g = as_global(g);
+    GWAMD_LDS int16_t* ring          = lds_of(ring_f);
+    const GWAMD_LDS uint8_t* read    = lds_of(read_f);
+    const GWAMD_LDS uint32_t* prec   = lds_of(P.rec);
+    const GWAMD_LDS uint16_t* pxl    = lds_of(P.xl);
+    GWAMD_GLB int16_t* spill         = (GWAMD_GLB int16_t*)(spill_f);
+    GWAMD_GLB uint8_t* codes         = (GWAMD_GLB uint8_t*)(codes_f);
+    GWAMD_GLB int16_t* carry_hbm     = (GWAMD_GLB int16_t*)(carry_f);
     constexpr int NR    = CPL / 2;
     const int gap       = sc.gap;
     const int s_eq      = sc.match - gap;
@@ -95,24 +162,24 @@ __device__ __forceinline__ void fwd2_rows(WinGraph<SizeT> g, const RowProg& P, i
         Eprev[i] = 0;
     int cin_prev = 0;
     int hbm_c    = 0;
-    uint32_t rec_c = uint32_t(uniform(int(P.rec[1])));
-    uint32_t rec_n = uint32_t(uniform(int(P.rec[min(2, V)])));
+    uint32_t rec_c = uint32_t(uniform(int(prec[1])));
+    uint32_t rec_n = uint32_t(uniform(int(prec[min(2, V)])));
     // lanes k < np: predecessor rows of row r (rows with a list in LDS)
-    auto xls_at = [&](int i) { return int(P.xl[i]); };
+    auto xls_at = [&](int i) { return int(pxl[i]); };
     int pv_c = xls_at(min(int(rec_c >> 16), xl_last) + lane);
-    uint8_t* crow = codes + code_stride;
-    int16_t* srow = spill + stride;
+    GWAMD_GLB uint8_t* crow = codes + code_stride;
+    GWAMD_GLB int16_t* srow = spill + stride;
     for (int r = 1; r <= V; r++, crow += code_stride, srow += stride)
     {
         const uint32_t rec = rec_c;
         // next rows: the record of row r+2, the predecessor list of row r+1
-        const uint32_t rec_nn = P.rec[min(r + 2, V)];
+        const uint32_t rec_nn = prec[min(r + 2, V)];
         // (read for every row: rows without a list get garbage they never
         // use; the offset is clamped into the list region)
         const int pv_n = xls_at(min(int(rec_n >> 16), xl_last) + lane);
         const int np       = int((rec >> 8) & 63);
         const bool spill_r = (rec >> 15) & 1;
-        int16_t* row       = ring + (r & mask) * ring_stride;
+        GWAMD_LDS int16_t* row = ring + (r & mask) * ring_stride;
         uint32_t sig[NR];
         {
             const uint32_t bsel = 0x0c040c00u + ((rec >> 1) & 3u) * 0x00010001u;
@@ -226,24 +293,24 @@ __device__ __forceinline__ void fwd2_rows(WinGraph<SizeT> g, const RowProg& P, i
 #pragma unroll
                     for (int q = 0; q < NR / 4; q++)
                     {
-                        const uint4 ev = make_uint4(E[4 * q], E[4 * q + 1], E[4 * q + 2], E[4 * q + 3]);
-                        *reinterpret_cast<uint4*>(row + jb + kColShift + 1 + 8 * q) = ev;
+                        const fwd_u32x4 ev = {E[4 * q], E[4 * q + 1], E[4 * q + 2], E[4 * q + 3]};
+                        *reinterpret_cast<GWAMD_LDS fwd_u32x4*>(row + jb + kColShift + 1 + 8 * q) = ev;
                         if (spill_r)
-                            *reinterpret_cast<uint4*>(srow + jb + kColShift + 1 + 8 * q) = ev;
+                            *reinterpret_cast<GWAMD_GLB fwd_u32x4*>(srow + jb + kColShift + 1 + 8 * q) = ev;
                         const uint32_t w0 = __builtin_amdgcn_perm(code[4 * q + 1], code[4 * q], 0x06040200u);
                         const uint32_t w1 = __builtin_amdgcn_perm(code[4 * q + 3], code[4 * q + 2], 0x06040200u);
                         __builtin_nontemporal_store(uint64_t(w0) | (uint64_t(w1) << 32),
-                                                    reinterpret_cast<uint64_t*>(crow + jb + kColShift + 1 + 8 * q));
+                                                    reinterpret_cast<GWAMD_GLB uint64_t*>(crow + jb + kColShift + 1 + 8 * q));
                     }
                 }
                 else
                 {
-                    const uint2 ev = make_uint2(E[0], E[1]);
-                    *reinterpret_cast<uint2*>(row + jb + kColShift + 1) = ev;
+                    const fwd_u32x2 ev = {E[0], E[1]};
+                    *reinterpret_cast<GWAMD_LDS fwd_u32x2*>(row + jb + kColShift + 1) = ev;
                     if (spill_r)
-                        *reinterpret_cast<uint2*>(srow + jb + kColShift + 1) = ev;
+                        *reinterpret_cast<GWAMD_GLB fwd_u32x2*>(srow + jb + kColShift + 1) = ev;
                     __builtin_nontemporal_store(__builtin_amdgcn_perm(code[1], code[0], 0x06040200u),
-                                                reinterpret_cast<uint32_t*>(crow + jb + kColShift + 1));
+                                                reinterpret_cast<GWAMD_GLB uint32_t*>(crow + jb + kColShift + 1));
                 }
             }
             if ((rec & (1u << 14)) && owner)
@@ -279,7 +346,7 @@ __device__ __forceinline__ void fwd2_rows(WinGraph<SizeT> g, const RowProg& P, i
             else
             {
                 const int ps = (r - d) & mask;
-                load_row_pk<NR>(ring + ps * ring_stride + ja + kColShift, Eprev, prev);
+                load_row_lds<NR>(ring + ps * ring_stride + ja + kColShift, Eprev, prev);
                 if (!FIRST)
                 {
                     const uint32_t bv = uint32_t(uint16_t(bnd[ps]));
@@ -329,12 +396,12 @@ __device__ __forceinline__ void fwd2_rows(WinGraph<SizeT> g, const RowProg& P, i
                         }
                         if (r - p > mask)
                         {
-                            load_row_pk<NR>(spill + size_t(p) * stride + ja + kColShift, Q, qprev);
+                            load_row_glb<NR>(spill + size_t(p) * stride + ja + kColShift, Q, qprev);
                             settle_vm<NR>(Q, qprev);
                             return;
                         }
                     }
-                    load_row_pk<NR>(ring + (p & mask) * ring_stride + ja + kColShift, Q, qprev);
+                    load_row_lds<NR>(ring + (p & mask) * ring_stride + ja + kColShift, Q, qprev);
                     if (!FIRST)
                     {
                         const uint32_t bv = uint32_t(uint16_t(bnd[p & mask]));
@@ -406,7 +473,7 @@ __device__ __forceinline__ void fwd2_rows(WinGraph<SizeT> g, const RowProg& P, i
                 const uint32_t ub = rec & 0x7fu;
                 if (!((ub & 0xc0u) == 0x40u && ((0x10008aull >> (ub & 0x3fu)) & 1u)))
                 {
-                    const uint32_t* rw = reinterpret_cast<const uint32_t*>(read + ja);
+                    const GWAMD_LDS uint32_t* rw = reinterpret_cast<const GWAMD_LDS uint32_t*>(read + ja);
 #pragma unroll
                     for (int i = 0; i < NR; i++)
                     {
