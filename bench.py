@@ -86,6 +86,13 @@ CONFIGS = {
     "B_banded_512": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=True, bw=512, windows=1024),
     "C_512": dict(backbone=10000, reads=16, err=500, max_seq=10600, banded=True, bw=512, windows=128, msa=True,
                   mem_per_window=600e6),
+    # shapes only the global-memory kernel takes (measured):
+    # band widths 384 and 1024, and full alignment with 32-bit scores (4 kb
+    # reads, 16 per window: use32bitScore, cudapoa_limits.hpp:28-53)
+    "B_banded_384": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=True, bw=384, windows=1024),
+    "B_banded_1024": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=True, bw=1024, windows=1024),
+    "F_int32_4k": dict(backbone=4000, reads=16, err=200, max_seq=4400, banded=False, bw=256, windows=128,
+                       mem_per_window=300e6),
 }
 # the config-B generator, seeds 1..1e6, 125k per GPU
 STREAM_CONFIGS = {"E": dict(CONFIGS["B"], windows_per_step=E_STEP_WINDOWS)}

@@ -8,6 +8,7 @@
 #include "aligner_common.hpp"
 
 #define GWAMD_LDS __attribute__((address_space(3)))
+#define GWAMD_GLB __attribute__((address_space(1)))
 
 namespace gwamd
 {

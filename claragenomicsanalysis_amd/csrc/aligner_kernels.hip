@@ -671,8 +671,10 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
     GWAMD_LDS SC* rvl               = fwl + kSplitLds;
     GWAMD_LDS PackSeg* pack         = (GWAMD_LDS PackSeg*)(base + a.lds_stack_off);
     uint8_t* ws                     = a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes);
-    SC* fwg       = reinterpret_cast<SC*>(ws + a.ws_split_off);
-    SC* rvg       = fwg + (a.stride + 1 + kWave);
+    // (global-typed: the split sweeps are called, not inlined, and a flat
+    // store there makes every LDS wait of the sweep wait for it)
+    GWAMD_GLB SC* fwg = (GWAMD_GLB SC*)(ws + a.ws_split_off);
+    GWAMD_GLB SC* rvg = fwg + (a.stride + 1 + kWave);
     int8_t* hbuf  = reinterpret_cast<int8_t*>(ws + a.ws_hbuf_off); // LONG: stripe hand-over
     uint32_t* patw = reinterpret_cast<uint32_t*>(ws + a.ws_pat_off); // LONG: query patterns
     PatPtr pat;
@@ -688,10 +690,12 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
         pat  = (GWAMD_LDS uint32_t*)(base + a.lds_pat_off);
         tcod = (GWAMD_LDS uint32_t*)(base + a.lds_target_off);
     }
-    uint4* front[2];
-    front[0]      = reinterpret_cast<uint4*>(ws + a.ws_front_off);
-    front[1]      = front[0] + a.front_cap;
-    int32_t* spl  = reinterpret_cast<int32_t*>(front[1] + a.front_cap); // split column per entry
+    // the two frontier buffers by select, not through an array of pointers
+    // (which would leave their accesses flat)
+    uint4* const front0 = reinterpret_cast<uint4*>(ws + a.ws_front_off);
+    uint4* const front1 = front0 + a.front_cap;
+    auto front          = [&](int c) { return c ? front1 : front0; };
+    int32_t* spl  = reinterpret_cast<int32_t*>(front1 + a.front_cap); // split column per entry
     // per-lane base cases: column state (pv, mv, score) and paths; (path
     // offset, length) per frontier entry
     uint64_t* lcol_pv = reinterpret_cast<uint64_t*>(ws + a.ws_leaf_off);
@@ -718,7 +722,7 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
             build_patterns((GWAMD_LDS uint32_t*)(base + a.lds_pat_off), q, Q, lane);
         const int pat_words = (Q + kWordBits - 1) / kWordBits;
         if (lane == 0)
-            front[0][0] = seg_pack(0, Q, 0, T);
+            front(0)[0] = seg_pack(0, Q, 0, T);
         __threadfence_block();
         wave_sync();
         int cur = 0, nf = 1;
@@ -747,7 +751,7 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
             };
             for (int f = 0; f < nf; f++)
             {
-                const uint4 v  = front[cur][f];
+                const uint4 v  = front(cur)[f];
                 const int qb   = uni(int(v.x)), qe = uni(int(v.y));
                 const int tb   = uni(int(v.z)), te = uni(int(v.w));
                 const int m    = qe - qb;
@@ -817,7 +821,7 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
             {
                 const int f      = f0 + lane;
                 const bool in    = f < nf;
-                const uint4 v    = in ? front[cur][f] : make_uint4(0, 0, 0, 0);
+                const uint4 v    = in ? front(cur)[f] : make_uint4(0, 0, 0, 0);
                 const int qb     = int(v.x), qe = int(v.y);
                 const int tb     = int(v.z), te = int(v.w);
                 const bool split = in && base_kind(qe - qb, te - tb, a.max_matrix_elems) == 0;
@@ -837,11 +841,11 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
                     {
                         const int qm = qb + (qe - qb) / 2;
                         const int tm = tb + int(spl[f]);
-                        front[cur ^ 1][pos]     = seg_pack(qb, qm, tb, tm);
-                        front[cur ^ 1][pos + 1] = seg_pack(qm, qe, tm, te);
+                        front(cur ^ 1)[pos]     = seg_pack(qb, qm, tb, tm);
+                        front(cur ^ 1)[pos + 1] = seg_pack(qm, qe, tm, te);
                     }
                     else
-                        front[cur ^ 1][pos] = v;
+                        front(cur ^ 1)[pos] = v;
                 }
                 nn += uni(__shfl(x, kWave - 1));
             }
@@ -861,7 +865,7 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
             {
                 const int f   = f0 + lane;
                 const bool in = f < nf;
-                const uint4 v = in ? front[cur][f] : make_uint4(0, 0, 0, 0);
+                const uint4 v = in ? front(cur)[f] : make_uint4(0, 0, 0, 0);
                 const int qb = int(v.x), qe = int(v.y);
                 const int tb = int(v.z), te = int(v.w);
                 const bool full_myers = in && base_kind(qe - qb, te - tb, a.max_matrix_elems) == 4;
@@ -895,7 +899,7 @@ __global__ void __launch_bounds__(kWave) hm_kernel(Args a)
         int len = 0;
         for (int f = nf - 1; f >= 0; f--)
         {
-            const uint4 v = front[cur][f];
+            const uint4 v = front(cur)[f];
             const int qb  = uni(int(v.x)), qe = uni(int(v.y));
             const int tb  = uni(int(v.z)), te = uni(int(v.w));
             const int kind = base_kind(qe - qb, te - tb, a.max_matrix_elems);

@@ -937,10 +937,17 @@ __device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, con
 // rows become node ids at the store.
 template <typename SizeT>
 __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L, int end_row,
-                               const uint8_t* codes, int code_stride, uint8_t* tile, SizeT* ag, SizeT* ar,
+                               const uint8_t* codes_f, int code_stride, uint8_t* tile_f, SizeT* ag_f, SizeT* ar_f,
                                int aln_cap, int lane, bool rank, int tbmode)
 {
     g = as_global(g);
+    // typed pointers: this function is called, not inlined (lds_of)
+    const GWAMD_GLB uint8_t* codes = glb_of(codes_f);
+    GWAMD_LDS uint8_t* tile        = lds_of(tile_f);
+    GWAMD_GLB SizeT* ag            = glb_of(ag_f);
+    GWAMD_GLB SizeT* ar            = glb_of(ar_f);
+    const GWAMD_LDS uint32_t* prec = lds_of(P.rec);
+    const GWAMD_LDS uint16_t* pxl  = lds_of(P.xl);
 
     V       = uniform(V);
     L       = uniform(L);
@@ -969,7 +976,7 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
 #pragma unroll
         for (int b0 = 0; b0 < kPer; b0 += kB)
         {
-            uint4 v[kB];
+            u32x4 v[kB];
 #pragma unroll
             for (int u = 0; u < kB; u++)
             {
@@ -978,9 +985,9 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
                 const int tc  = (t % (kTileCols / 16)) * 16;
                 const int rr  = ti0 + tr;
                 const bool ok = rr <= V && tj0 + tc + 16 <= code_stride;
-                v[u] = *reinterpret_cast<const uint4*>(codes + size_t(ok ? rr : 0) * code_stride +
-                                                       (ok ? tj0 + tc : 0));
-                v[u] = ok ? v[u] : make_uint4(0, 0, 0, 0);
+                v[u] = *reinterpret_cast<const GWAMD_GLB u32x4*>(codes + size_t(ok ? rr : 0) * code_stride +
+                                                                 (ok ? tj0 + tc : 0));
+                v[u] = ok ? v[u] : u32x4{0, 0, 0, 0};
             }
 #pragma unroll
             for (int u = 0; u < kB; u++)
@@ -988,7 +995,7 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
                 const int t  = (b0 + u) * kWave + lane;
                 const int tr = t / (kTileCols / 16);
                 const int tc = (t % (kTileCols / 16)) * 16;
-                *reinterpret_cast<uint4*>(tile + tr * kTileCols + tc) = v[u];
+                *reinterpret_cast<GWAMD_LDS u32x4*>(tile + tr * kTileCols + tc) = v[u];
             }
         }
         wave_sync();
@@ -1010,7 +1017,7 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
         if (r >= 1 && c >= 0 && r >= ti0 && r < ti0 + kTileRows && cj >= tj0 && cj < tj0 + kTileCols)
         {
             const int code     = int(tile[(r - ti0) * kTileCols + (cj - tj0)]);
-            const uint32_t rec = P.rec[r];
+            const uint32_t rec = prec[r];
             const int dir      = code & 3;
             const int np       = int((rec >> 8) & 63);
             const int pj       = dir == 1 ? c : c - 1;
@@ -1020,7 +1027,7 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
                 res = (uint32_t(r) << 16) | uint32_t(pj);
             else if (np != int(kRecEscape))
             {
-                const int p = np == 0 ? 0 : (np == 1 ? r - int(rec >> 16) : int(P.xl[(rec >> 16) + (code >> 2)]));
+                const int p = np == 0 ? 0 : (np == 1 ? r - int(rec >> 16) : int(pxl[(rec >> 16) + (code >> 2)]));
                 res         = (uint32_t(p) << 16) | uint32_t(pj);
             }
         }
@@ -1054,7 +1061,7 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
             int ci = i, cj = j, cn = n, cl = loops;
             if (rank)
                 walk_window_ranked<0>(wpk0, wpk1, G, ci, cj, cn, cl, bound, lane, eg, er,
-                                      (GWAMD_LDS uint8_t*)(tile + kTileRows * kTileCols), flush);
+                                      tile + kTileRows * kTileCols, flush);
             else
             while (true)
             {
@@ -1101,7 +1108,7 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
             if (i < ti0 || i >= ti0 + kTileRows || cj < tj0 || cj >= tj0 + kTileCols)
                 load_tile(i, cj);
             const int code_v   = int(tile[(i - ti0) * kTileCols + (cj - tj0)]);
-            const int rec_v    = int(P.rec[i]);
+            const int rec_v    = int(prec[i]);
             const int code     = uniform(code_v);
             const uint32_t rec = uint32_t(uniform(rec_v));
             const int dir      = code & 3;
@@ -1112,7 +1119,11 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
             }
             else
             {
-                pi = uniform(prog_pred(P, g, i, rec, code >> 2));
+                const int np = int((rec >> 8) & 63), k = code >> 2;
+                pi = np == 0 ? 0
+                             : (np == 1 ? i - int(rec >> 16)
+                                        : (np == int(kRecEscape) ? uniform(pred_row(g, int(g.sorted[i - 1]), k))
+                                                                 : uniform(int(pxl[(rec >> 16) + k]))));
                 pj = dir == 0 ? j - 1 : j;
             }
         }

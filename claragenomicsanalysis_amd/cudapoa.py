@@ -302,6 +302,7 @@ class CudaPoaBatch:
         self._lib.gwamd_poa_get_types(self._handle, C.byref(sb), C.byref(zb))
         return sb.value, zb.value
 
+
     def kernel_variant(self):
         """1: global-memory kernel, 2: LDS-resident kernel (full), 3: banded kernel,
         4: banded kernel with the anti-diagonal forward pass (poa_band_ad.hpp)."""

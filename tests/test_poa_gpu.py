@@ -113,6 +113,33 @@ def test_banded_parity_synthetic(bw):
         assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), i
 
 
+@pytest.mark.parametrize("bw", [384, 640, 1024])
+def test_banded_other_widths(bw):
+    # band widths the reference accepts beyond the LDS band kernel's 128 / 256 /
+    # 512 (any multiple of 128, batch.hpp:85-94): the global-memory kernel
+    wins = synth.poa_windows(23, 6, 1000, 12, 40, 40, 40)
+    max_seq = 1100
+    b = run_gpu(wins, max_seq, 12, banded=True, bw=bw)
+    assert b.kernel_variant() == 1
+    sbits = b.get_types()[0]
+    cons, cov, st = b.get_consensus()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, max_seq, 12, banded=True, bw=bw, score_bits=sbits)
+        assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), i
+
+
+def test_full_int32_long_reads():
+    # full alignment with 32-bit scores (4 kb reads: use32bitScore,
+    # cudapoa_limits.hpp:28-53): the global-memory kernel
+    wins = synth.poa_windows(27, 3, 4000, 6, 150, 150, 150)
+    b = run_gpu(wins, 4400, 6, mem=8 << 30)
+    assert b.get_types()[0] == 32 and b.kernel_variant() == 1
+    cons, cov, st = b.get_consensus()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 4400, 6, score_bits=32)
+        assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), i
+
+
 def test_msa_parity_synthetic():
     wins = synth.poa_windows(31, 8, 300, 8, 15, 15, 15)
     b = run_gpu(wins, 400, 8, output_type="msa")
