@@ -1469,8 +1469,12 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
                 if (d.spoa_accurate)
                     rc = topsort_racon_wave<SizeT>(g, nc, cscore, cpred, 4 * d.max_nodes, lane,
                                                    (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off);
+                // (no ring-forcing diagnostic here: that runtime flag doubled
+                // this kernel's SGPR spill reloads, 6,364 -> 13,364, and slowed
+                // config C's forward pass 64 -> 79 ms per window; the ring mode
+                // is the same topsort_lds code, tested through the LDS kernel)
                 else if (!topsort_lds<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, (GWAMD_LDS int*)(shb),
-                                             lane, tsprof, (d.diag & 1) != 0) &&
+                                             lane, tsprof) &&
                          !topsort_lds_big<SizeT>(g, nc, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, lane))
                 {
                     if (lane == 0)

@@ -1224,56 +1224,6 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
     const bool use_q     = q_mode != 0;
     const uint32_t qmask = q_mode == 2 ? uint32_t(qring - 1) : 0xffffffffu;
     GWAMD_LDS uint32_t* qinfo    = (GWAMD_LDS uint32_t*)(scratch + qinfo_off);
-    // Chain runs.  A link v -> w is a node v with one successor w whose only
-    // predecessor is v.  Popping v while v is the only queued node releases
-    // exactly w, and so on to the end of the chain: the FIFO order is fixed
-    // along it.  Such a run is emitted in one step (its queue slots are
-    // reserved, the end node is popped next) and its nodes are written into
-    // the reserved slots by a lane-parallel pass after the loop.  Per node:
-    // chain word cw = (distance to the chain end << 16) | chain end, by
-    // pointer jumping; bit 22 of the node word marks a link.
-    const int cw_off            = (qinfo_off + (q_mode == 1 ? (n + 1) : (q_mode == 2 ? qring : 0)) * 4 + 15) & ~15;
-#ifdef GWAMD_NO_TOPSORT_CHAINS
-    const bool chains = false;
-#else
-    const bool chains           = uniform(q_mode != 0 && n < 65535 && cw_off + (n + 1) * 4 <= scratch_bytes) != 0;
-#endif
-    GWAMD_LDS uint32_t* cw      = (GWAMD_LDS uint32_t*)(scratch + cw_off);
-    if (chains)
-    {
-        for (int v = lane; v < n; v += kWave)
-        {
-            const uint32_t vi = info[v];
-            bool link         = ((vi >> 16) & 63u) == 1u;
-            const int w       = int(vi & 0xffffu);
-            if (link)
-                link = (info[w] >> 24) == 1u;
-            cw[v] = link ? ((1u << 16) | uint32_t(w)) : uint32_t(v);
-            if (link)
-                info[v] = vi | (1u << 22);
-        }
-        wave_sync();
-        // in place: every word is (distance, target) with target `distance`
-        // links down the chain, so any mix of old and new words composes
-        while (true)
-        {
-            bool changed = false;
-            for (int v = lane; v < n; v += kWave)
-            {
-                const uint32_t a = cw[v];
-                const int t      = int(a & 0xffffu);
-                const uint32_t b = cw[t];
-                if ((b >> 16) != 0u)
-                {
-                    cw[v]   = (((a >> 16) + (b >> 16)) << 16) | (b & 0xffffu);
-                    changed = true;
-                }
-            }
-            wave_sync();
-            if (__builtin_amdgcn_ballot_w64(changed) == 0)
-                break;
-        }
-    }
     // sources in id order
     int k = 0;
     for (int v0 = 0; v0 < n; v0 += kWave)
@@ -1315,7 +1265,6 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
         int tail       = uniform(k);
         int q          = 0;
         uint32_t vinfo = tail > 0 ? uint32_t(uniform(int(info[int(queue[0])]))) : 0u;
-        bool after_run = false; // the pop right after a run is its end node
         while (q < tail)
         {
             // the loop state is wave-uniform; saying so keeps it in SGPRs with
@@ -1323,24 +1272,6 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
             tail      = uniform(tail);
             q         = uniform(q);
             vinfo     = uint32_t(uniform(int(vinfo)));
-            if (kMode != 0 && chains && (vinfo & (1u << 22)) && q + 1 == tail && !after_run)
-            {
-                // the only queued node starts a chain run: reserve the slots
-                // of the m nodes after it (its end last), pop the end next;
-                // the run is recorded in the end's chain word (slot, m)
-                const uint32_t a = uint32_t(uniform(int(cw[int(queue[q])])));
-                const int m      = int(a >> 16);
-                const int e      = int(a & 0xffffu);
-                const int slot   = tail;
-                tail += m;
-                queue[tail - 1] = uint16_t(e);
-                cw[e]           = (uint32_t(m) << 16) | uint32_t(slot);
-                q               = tail - 1;
-                vinfo           = uint32_t(uniform(int(info[e])));
-                after_run       = true;
-                continue;
-            }
-            after_run     = false;
             const int deg = int((vinfo >> 16) & 63u);
             // The word of the next queue entry, when it is queued already, is
             // final (a queued node is never decremented again), so its read is
@@ -1411,25 +1342,6 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
     const uint64_t tp2 = __builtin_amdgcn_s_memtime();
 #endif
     const int m = sh[0];
-    if (chains)
-    {
-        // nodes inside chain runs: slot = run slot + m - 1 - distance to end.
-        // Linked nodes (bit 22) are the ones that are not chain ends; an end's
-        // word holds (m, slot) if a run reached it, else (0, itself).
-        for (int v = lane; v < n; v += kWave)
-        {
-            if (info[v] & (1u << 22))
-            {
-                const uint32_t a = cw[v];
-                const int dv     = int(a >> 16);
-                const uint32_t r = cw[int(a & 0xffffu)];
-                const int mr     = int(r >> 16);
-                if (dv < mr)
-                    queue[int(r & 0xffffu) + mr - 1 - dv] = uint16_t(v);
-            }
-        }
-        wave_sync();
-    }
     for (int q = lane; q < m; q += kWave)
     {
         const int v = int(queue[q]);
