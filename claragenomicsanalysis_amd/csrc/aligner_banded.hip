@@ -120,6 +120,43 @@ __device__ __forceinline__ int chunk_step(uint32_t& pv, uint32_t& mv, uint32_t e
     return out;
 }
 
+// chunk_step on two independent 32-word chunks at once, one in each half of
+// the wave (lanes 0..31 and 32..63; act covers both).  hin is per lane (the
+// carry into its half's lane 0); the carry-lookahead and the one-bit shifts
+// stop at the half boundary, so each half computes exactly what chunk_step
+// computes for it alone.
+__device__ __forceinline__ int chunk_step2(uint32_t& pv, uint32_t& mv, uint32_t eq, int hin, uint32_t hbit,
+                                           uint64_t act, int lane)
+{
+    constexpr uint64_t kLo = 0xffffffffull;
+    const uint32_t first   = (lane & 31) == 0 ? 1u : 0u;
+    const uint32_t xv      = eq | mv;
+    if (hin < 0)
+        eq |= first;
+    uint32_t s;
+    const bool ov     = __builtin_add_overflow(eq & pv, pv, &s);
+    const uint64_t G  = ballot(ov) & act;
+    const uint64_t P  = ballot(s == 0xffffffffu) & act;
+    const uint64_t GP = G | P;
+    const uint64_t cs = (((GP & kLo) + (G & kLo)) & kLo) | ((GP & ~kLo) + (G & ~kLo));
+    s += uint32_t((cs ^ GP ^ G) >> lane) & 1u; // carry into this word
+    const uint32_t xh = (s ^ pv) | eq;
+    uint32_t ph       = mv | ~(xh | pv);
+    uint32_t mh       = pv & xh;
+    const int out     = int((ph & hbit) != 0u) - int((mh & hbit) != 0u);
+    const uint64_t PH = (ballot((ph >> 31) != 0u) << 1) & ~(1ull << 32);
+    const uint64_t MH = (ballot((mh >> 31) != 0u) << 1) & ~(1ull << 32);
+    ph                = (ph << 1) | (uint32_t(PH >> lane) & 1u);
+    mh                = (mh << 1) | (uint32_t(MH >> lane) & 1u);
+    if (hin < 0)
+        mh |= first;
+    if (hin > 0)
+        ph |= first;
+    pv = mh | ~(xv | ph);
+    mv = ph & xv;
+    return out;
+}
+
 } // namespace
 
 // ---------------------------------------------------------------------------
@@ -159,6 +196,18 @@ __device__ __forceinline__ void lds_put(GWAMD_LDS BandEntry* p, const BandEntry&
     p->mv  = e.mv;
     p->sc  = e.sc;
     p->pad = 0;
+}
+
+// HBM copies of a band entry: one 16-byte global load / store
+typedef uint32_t be_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ BandEntry glb_get(const GWAMD_GLB BandEntry* p)
+{
+    const be_u32x4 v = *(const GWAMD_GLB be_u32x4*)(p);
+    return BandEntry{v.x, v.y, int32_t(v.z), 0};
+}
+__device__ __forceinline__ void glb_put(GWAMD_GLB BandEntry* p, const BandEntry& e)
+{
+    *(GWAMD_GLB be_u32x4*)(p) = be_u32x4{e.pv, e.mv, uint32_t(e.sc), 0u};
 }
 
 __device__ void build_patterns_lm(GWAMD_LDS uint32_t* patL, int pat_words, const char* q, int Q, int lane)
@@ -208,7 +257,8 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
     GWAMD_LDS uint32_t* patL = (GWAMD_LDS uint32_t*)(base + a.lds_pat_off);
     GWAMD_LDS BandEntry* reg = (GWAMD_LDS BandEntry*)(base + a.lds_tile_off); // chunk state / tile
     const int TLE            = a.tile_bytes / int(sizeof(BandEntry));
-    BandEntry* E             = reinterpret_cast<BandEntry*>(a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes));
+    // global-typed: flat stores would hold every LDS wait of the sweep behind them
+    GWAMD_GLB BandEntry* E   = (GWAMD_GLB BandEntry*)(a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes));
     const int pw_stride      = a.pat_words;
 
     for (int idx = blockIdx.x; idx < a.n; idx += gridDim.x)
@@ -276,7 +326,7 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                 uint32_t pv = ~0u, mv = 0u;
                 int sc      = min((lane + 1) * kWordBits, bw);
                 if (act_l)
-                    E[lane] = BandEntry{pv, mv, sc, 0};
+                    glb_put(E + (lane), BandEntry{pv, mv, sc, 0});
                 uint32_t eqn = band_pattern(patL, pw_stride, nwq, col_off(1), lane, code_of(1));
                 for (int t = 1; t <= T; t++)
                 {
@@ -309,7 +359,7 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                         sc += right + down;
                     }
                     if (act_l)
-                        E[size_t(t) * nwb + lane] = BandEntry{pv, mv, sc, 0};
+                        glb_put(E + (size_t(t) * nwb + lane), BandEntry{pv, mv, sc, 0});
                 }
                 ed = uni(__builtin_amdgcn_readlane(sc, lastw));
             }
@@ -328,10 +378,85 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                     const BandEntry e0{~0u, 0u, min((w + 1) * kWordBits, bw), 0};
                     if constexpr (lds_state)
                         lds_put(reg + w, e0);
-                    E[w] = e0;
+                    glb_put(E + (w), e0);
                 }
                 __threadfence_block();
                 wave_sync();
+                if constexpr (lds_state)
+                {
+                    // two columns per pass: half hf = lane / 32 runs column
+                    // t0 + hf, the second half two chunks behind the first (its
+                    // chunk c needs chunks c and c+1 of column t0 and its own
+                    // chunk c-1), so a column's nch dependent chunk steps are
+                    // shared by two columns (nch + 2 steps per pair of columns)
+                    const int hf = lane >> 5;
+                    const int hl = lane & 31;
+                    for (int t0 = 1; t0 <= T; t0 += 2)
+                    {
+                        const int tt    = t0 + hf; // this half's column
+                        const bool hcol = tt <= T;
+                        const int tc    = min(tt, T);
+                        const int code  = int((tcod[(tc - 1) >> 4] >> (2 * ((tc - 1) & 15))) & 3u);
+                        const int off   = col_off(tc);
+                        const bool diag = tc >= db && tc < de;
+                        int carry       = 1; // +1 into the band's top row
+                        for (int st = 0; st < nch + 2; st++)
+                        {
+                            const int c        = st - 2 * hf;
+                            const bool cin     = hcol && c >= 0 && c < nch;
+                            const int w        = c * kChunkWords + hl;
+                            const bool valid   = cin && w < nwb;
+                            const uint64_t act = ballot(valid);
+                            const int wr       = valid ? w : 0;
+                            const BandEntry e  = lds_get(reg + wr);
+                            uint32_t pv = e.pv, mv = e.mv;
+                            int sc            = e.sc;
+                            const uint32_t eq = band_pattern(patL, pw_stride, nwq, off, wr, code);
+                            const bool last   = w == lastw;
+                            uint32_t hb;
+                            if (diag)
+                            {
+                                // the previous column moves up one row; word 31
+                                // takes bit 0 of the next chunk's first word
+                                const uint64_t PB = ((ballot(pv & 1u) & act) >> 1) & ~(1ull << 31);
+                                const uint64_t MB = ((ballot(mv & 1u) & act) >> 1) & ~(1ull << 31);
+                                pv                = (pv >> 1) | ((uint32_t(PB >> lane) & 1u) << 31);
+                                mv                = (mv >> 1) | ((uint32_t(MB >> lane) & 1u) << 31);
+                                if (hl == kChunkWords - 1 && cin && c + 1 < nch)
+                                {
+                                    const BandEntry nx = lds_get(reg + (c + 1) * kChunkWords);
+                                    pv |= (nx.pv & 1u) << 31;
+                                    mv |= (nx.mv & 1u) << 31;
+                                }
+                                hb = last ? 1u << max(top_last - 2, 0) : 0x40000000u;
+                                if (last)
+                                {
+                                    pv |= hb << 1;
+                                    mv &= ~(hb << 1);
+                                }
+                            }
+                            else
+                                hb = last ? 1u << (top_last - 1) : 0x80000000u;
+                            const int r    = chunk_step2(pv, mv, eq, carry, hb, act, lane);
+                            const int down = int((pv & (hb << 1)) != 0u) - int((mv & (hb << 1)) != 0u);
+                            const int hout = diag ? down : r;
+                            sc += diag ? r + down : r;
+                            // chunk hand-over within each half (:527-532, :605-611)
+                            const int c0 = __builtin_amdgcn_readlane(hout, kChunkWords - 1);
+                            const int c1 = __builtin_amdgcn_readlane(hout, kWave - 1);
+                            carry        = cin ? (hf ? c1 : c0) : carry;
+                            if (valid)
+                            {
+                                const BandEntry o{pv, mv, sc, 0};
+                                lds_put(reg + w, o);
+                                glb_put(E + (size_t(tt) * nwb + w), o);
+                            }
+                        }
+                    }
+                    __threadfence_block();
+                    wave_sync();
+                    return uni(lds_get(reg + lastw).sc);
+                }
                 for (int t = 1; t <= T; t++)
                 {
                     const int code  = code_of(t);
@@ -347,7 +472,7 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                         if constexpr (lds_state)
                             e = lds_get(reg + (valid ? w : 0));
                         else
-                            e = E[size_t(t - 1) * nwb + (valid ? w : 0)];
+                            e = glb_get(E + (size_t(t - 1) * nwb + (valid ? w : 0)));
                         uint32_t pv = e.pv, mv = e.mv;
                         int sc            = e.sc;
                         const uint32_t eq = band_pattern(patL, pw_stride, nwq, off, w, code);
@@ -373,7 +498,7 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                                 if constexpr (lds_state)
                                     nx = lds_get(reg + (c + 1) * kChunkWords);
                                 else
-                                    nx = E[size_t(t - 1) * nwb + (c + 1) * kChunkWords];
+                                    nx = glb_get(E + (size_t(t - 1) * nwb + (c + 1) * kChunkWords));
                                 if (lane == kChunkWords - 1)
                                 {
                                     p2 |= (nx.pv & 1u) << 31;
@@ -401,7 +526,7 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                             const BandEntry o{pv, mv, sc, 0};
                             if constexpr (lds_state)
                                 lds_put(reg + w, o);
-                            E[size_t(t) * nwb + w] = o;
+                            glb_put(E + (size_t(t) * nwb + w), o);
                         }
                     }
                     if constexpr (!lds_state)
@@ -416,7 +541,7 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                 if constexpr (lds_state)
                     return uni(lds_get(reg + lastw).sc);
                 else
-                    return uni(E[size_t(T) * nwb + lastw].sc);
+                    return uni(glb_get(E + (size_t(T) * nwb + lastw)).sc);
                 };
                 if (nwb <= TLE)
                     ed = sweep(std::true_type{});
@@ -450,7 +575,7 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
             const int64_t lo = max<int64_t>(0, hi - TLE);
             wave_sync();
             for (int64_t e = lane; e < hi - lo; e += kWave)
-                lds_put(reg + e, E[lo + e]);
+                lds_put(reg + e, glb_get(E + (lo + e)));
             wave_sync();
             tb = lo;
             te = hi;
@@ -462,7 +587,7 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
             refill(j);
         // start from the band's last word: the reference reads word
         // band_width / 32 (:393), one past the band when band_width % 32 == 0
-        int s = uni(E[int64_t((bw - 1) / kWordBits) + int64_t(nwb) * j].sc);
+        int s = uni(glb_get(E + (int64_t((bw - 1) / kWordBits) + int64_t(nwb) * j)).sc);
         while (j > 0 && (i > 0 || j >= db))
         {
             const int phase = j >= de ? 3 : (j >= db ? 2 : 1);
@@ -500,7 +625,7 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
             if (o >= tb && o < te)
                 e = lds_get(reg + (o - tb));
             else if (inr)
-                e = E[o];
+                e = glb_get(E + (o));
             uint32_t mask = shl_ptx(~1u, bi);
             if (wi == nwb - 1)
                 mask &= lem;
@@ -988,7 +1113,16 @@ extern "C" hipError_t gwamd_internal_banded_launch(const gwamd::aln::Args* a, in
     if (a->n <= 0)
         return hipSuccess;
     if (algo == 2)
+    {
+        if (a->lds_bytes > 65536)
+        {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(myers_banded_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, a->lds_bytes);
+            if (e != hipSuccess)
+                return e;
+        }
         hipLaunchKernelGGL(myers_banded_kernel, dim3(grid), dim3(kWave), size_t(a->lds_bytes), stream, *a);
+    }
     else if (a->uk_threads > 0)
     {
         if (a->uk_threads % kWave != 0 || a->uk_threads > 1024)
@@ -1020,8 +1154,17 @@ extern "C" hipError_t gwamd_internal_banded_occupancy(int algo, int lds_bytes, i
 {
     using namespace gwamd::aln;
     if (algo == 2)
+    {
+        if (lds_bytes > 65536)
+        {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(myers_banded_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+            if (e != hipSuccess)
+                return e;
+        }
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, myers_banded_kernel, kWave,
                                                             size_t(lds_bytes));
+    }
     if (lds_bytes > 65536)
     {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(ukkonen_kernel),

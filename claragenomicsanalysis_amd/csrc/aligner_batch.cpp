@@ -506,11 +506,13 @@ private:
             lds_pat_off_     = int32_t(a16((max_t_ + 15) / 16 * 4 + 16));
             lds_tile_off_    = int32_t(lds_pat_off_ + a16(int64_t(pat_words) * 16 + 16));
             // at least 256 16-byte band entries (two columns of 128 words, or
-            // 256 chunk words); up to the whole band's chunk state while it
-            // fits 48 KiB of LDS (wider bands keep it in HBM)
+            // 256 chunk words); up to the whole band's chunk state while the
+            // workgroup's LDS stays within the CU's 160 KiB (a 65,536 bp query:
+            // 16 KiB target + 32 KiB patterns + 32 KiB state; wider bands keep
+            // the state in HBM and wait on it every column)
             tile_bytes_      = 4096;
-            int64_t want     = std::min<int64_t>(a16(int64_t(pat_words) * 16), int64_t(48) << 10);
-            want             = std::min<int64_t>(want, (65536 - lds_tile_off_) & ~int64_t(511));
+            int64_t want     = a16(int64_t(pat_words) * 16);
+            want             = std::min<int64_t>(want, (163840 - lds_tile_off_) & ~int64_t(511));
             if (const char* tb = gwamd::host::diag_env("GWAMD_BAND_TILE_BYTES")) // parity tests: HBM chunk state
             {
                 // LDS bytes for the chunk state: 4096 (256 words, the minimum
@@ -551,7 +553,7 @@ private:
             tile_bytes_         = 8192;
             lds_tile_off_       = uk_narrow_tile_off_;
         }
-        if (lds_bytes_ > (algo_ == GWAMD_ALIGNER_UKKONEN ? 163840 : 65536) ||
+        if (lds_bytes_ > 163840 ||
             (algo_ == GWAMD_ALIGNER_UKKONEN && uk_wide_lds_ > 163840))
             throw std::invalid_argument("aligner problem size does not fit in LDS");
         pat_words_ = pat_words;

@@ -111,6 +111,22 @@ def test_myers_banded_chunk_state_in_hbm(monkeypatch):
         assert g == oracle.align(q, tt, oracle.ALIGN_MYERS_BANDED, mq)
 
 
+def test_myers_banded_two_column_sweep():
+    # bands of several 32-word chunks with their state in LDS run two target
+    # columns per pass (one per half wave, the second two chunks behind):
+    # odd and even target lengths (the last pass with one column), stripes
+    # and diagonal bands, up to the whole query (375 words, 12 chunks)
+    rng = random.Random(43)
+    t = rand_seq(rng, 12000)
+    pairs = [(mutate(rng, t, 0.45), t), (rand_seq(rng, 11000), t[:11001]),
+             (mutate(rng, t[:9001], 0.2), t[:9001]), (mutate(rng, t, 0.12), t[:11500])]
+    st = {}
+    got, mq = gpu_states(pairs, "myers_banded", stats=st)
+    assert st["hbm_state_sweeps"] == 0
+    for (q, tt), g in zip(pairs, got):
+        assert g == oracle.align(q, tt, oracle.ALIGN_MYERS_BANDED, mq), (len(q), len(tt))
+
+
 def test_band_tile_bytes_checked(monkeypatch):
     monkeypatch.setenv("GWAMD_BAND_TILE_BYTES", "4k")
     with pytest.raises(ValueError):
