@@ -248,10 +248,24 @@ __device__ __forceinline__ uint32_t band_pattern(const GWAMD_LDS uint32_t* patL,
 
 } // namespace
 
-__global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
+// LDS-only workgroup barrier for the multi-wave sweep: the waves exchange
+// band chunks through LDS only, so the step barrier waits for the LDS queue
+// and not for the band matrix's HBM stores (a workgroup fence would)
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// NWV waves per pair: wave 0 does everything; waves 1..NWV-1 join the sweeps of
+// bands of several chunks whose state fits LDS (2 * NWV target columns in
+// flight, see sweep_multi)
+template <int NWV>
+__global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
 {
     extern __shared__ __align__(16) uint8_t lds[];
-    const int lane           = threadIdx.x;
+    __shared__ int ed_slot;
+    const int lane           = threadIdx.x & (kWave - 1);
+    const int wv             = threadIdx.x / kWave;
     GWAMD_LDS uint8_t* base  = (GWAMD_LDS uint8_t*)(lds);
     GWAMD_LDS uint32_t* tcod = (GWAMD_LDS uint32_t*)(base + a.lds_target_off);
     GWAMD_LDS uint32_t* patL = (GWAMD_LDS uint32_t*)(base + a.lds_pat_off);
@@ -271,16 +285,22 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
         if (Q == 0 || T == 0)
         {
             // the reference asserts non-empty sequences; the only path
-            pw.fill(kDeletion, Q, lane);
-            pw.fill(kInsertion, T, lane);
-            if (lane == 0)
-                a.path_len[idx] = pw.overflow ? -1 : pw.pos;
+            if (wv == 0)
+            {
+                pw.fill(kDeletion, Q, lane);
+                pw.fill(kInsertion, T, lane);
+                if (lane == 0)
+                    a.path_len[idx] = pw.overflow ? -1 : pw.pos;
+            }
             continue;
         }
-        wave_sync();
-        pack_target(tcod, tg, T, lane);
-        build_patterns_lm(patL, pw_stride, q, Q, lane);
-        wave_sync();
+        if (wv == 0)
+        {
+            wave_sync();
+            pack_target(tcod, tg, T, lane);
+            build_patterns_lm(patL, pw_stride, q, Q, lane);
+            wave_sync();
+        }
         const int nwq  = (Q + kWordBits - 1) / kWordBits;
         const int dlen = Q > T ? Q - T : T - Q;
         int est        = max(1, dlen + min(T, Q) / 20); // initial_distance_guess_factor (:36, :749)
@@ -314,7 +334,91 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
             // band), Q - bw (bottom stripe)
             auto col_off = [&](int t) { return t < db ? 0 : (t < de ? t - db + 1 : Q - bw); };
             int ed       = 0;
-            if (nch == 1)
+            // all NWV waves: several chunks with their state in LDS, 2 * NWV
+            // columns in flight; column g of a group runs chunk c at step
+            // c + 2g (it needs chunks c and c+1 of column g-1 and its own
+            // chunk c-1), one LDS barrier per step
+            auto sweep_multi = [&]() -> int {
+                lds_barrier(); // this pair's target and patterns (wave 0), previous backtrace done
+                for (int w = int(threadIdx.x); w < nwb; w += kWave * NWV)
+                {
+                    const BandEntry e0{~0u, 0u, min((w + 1) * kWordBits, bw), 0};
+                    lds_put(reg + w, e0);
+                    glb_put(E + (w), e0);
+                }
+                lds_barrier();
+                constexpr int G = 2 * NWV;
+                const int g     = 2 * wv + (lane >> 5);
+                const int hl    = lane & 31;
+                const int nst   = nch + 2 * (G - 1);
+                for (int t0 = 1; t0 <= T; t0 += G)
+                {
+                    const int tt    = t0 + g; // this half wave's column
+                    const bool hcol = tt <= T;
+                    const int tc    = min(tt, T);
+                    const int code  = int((tcod[(tc - 1) >> 4] >> (2 * ((tc - 1) & 15))) & 3u);
+                    const int off   = col_off(tc);
+                    const bool diag = tc >= db && tc < de;
+                    int carry       = 1; // +1 into the band's top row
+                    for (int st = 0; st < nst; st++)
+                    {
+                        const int c        = st - 2 * g;
+                        const bool cin     = hcol && c >= 0 && c < nch;
+                        const int w        = c * kChunkWords + hl;
+                        const bool valid   = cin && w < nwb;
+                        const uint64_t act = ballot(valid);
+                        const int wr       = valid ? w : 0;
+                        const BandEntry e  = lds_get(reg + wr);
+                        uint32_t pv = e.pv, mv = e.mv;
+                        int sc            = e.sc;
+                        const uint32_t eq = band_pattern(patL, pw_stride, nwq, off, wr, code);
+                        const bool last   = w == lastw;
+                        uint32_t hb;
+                        if (diag)
+                        {
+                            const uint64_t PB = ((ballot(pv & 1u) & act) >> 1) & ~(1ull << 31);
+                            const uint64_t MB = ((ballot(mv & 1u) & act) >> 1) & ~(1ull << 31);
+                            pv                = (pv >> 1) | ((uint32_t(PB >> lane) & 1u) << 31);
+                            mv                = (mv >> 1) | ((uint32_t(MB >> lane) & 1u) << 31);
+                            if (hl == kChunkWords - 1 && cin && c + 1 < nch)
+                            {
+                                const BandEntry nx = lds_get(reg + (c + 1) * kChunkWords);
+                                pv |= (nx.pv & 1u) << 31;
+                                mv |= (nx.mv & 1u) << 31;
+                            }
+                            hb = last ? 1u << max(top_last - 2, 0) : 0x40000000u;
+                            if (last)
+                            {
+                                pv |= hb << 1;
+                                mv &= ~(hb << 1);
+                            }
+                        }
+                        else
+                            hb = last ? 1u << (top_last - 1) : 0x80000000u;
+                        const int r    = chunk_step2(pv, mv, eq, carry, hb, act, lane);
+                        const int down = int((pv & (hb << 1)) != 0u) - int((mv & (hb << 1)) != 0u);
+                        const int hout = diag ? down : r;
+                        sc += diag ? r + down : r;
+                        const int c0 = __builtin_amdgcn_readlane(hout, kChunkWords - 1);
+                        const int c1 = __builtin_amdgcn_readlane(hout, kWave - 1);
+                        carry        = cin ? ((lane >> 5) ? c1 : c0) : carry;
+                        if (valid)
+                        {
+                            const BandEntry o{pv, mv, sc, 0};
+                            lds_put(reg + w, o);
+                            glb_put(E + (size_t(tt) * nwb + w), o);
+                        }
+                        lds_barrier();
+                    }
+                }
+                __syncthreads(); // every wave's band-matrix stores before wave 0's backtrace
+                return uni(lds_get(reg + lastw).sc);
+            };
+            if (NWV > 1 && nch > 1 && nwb <= TLE)
+                ed = sweep_multi();
+            else if (wv != 0)
+                ;
+            else if (nch == 1)
             {
                 // one chunk: the band's words live in lanes 0..nwb-1 for the whole sweep
                 const bool act_l   = lane < nwb;
@@ -552,10 +656,24 @@ __global__ void __launch_bounds__(kWave) myers_banded_kernel(Args a)
                     ed = sweep(std::false_type{});
                 }
             }
+            if constexpr (NWV > 1)
+            {
+                if (!(nch > 1 && nwb <= TLE))
+                {
+                    // wave 0's distance to every wave (the band loop is uniform)
+                    if (threadIdx.x == 0)
+                        ed_slot = ed;
+                    __syncthreads();
+                    ed = uni(ed_slot);
+                    __syncthreads();
+                }
+            }
             if (ed <= est || bw == Q)
                 break;
             est *= 2;
         }
+        if (wv != 0)
+            continue; // the backtrace is wave 0's
         __threadfence_block();
         wave_sync();
 #ifdef GWAMD_ALN_NO_BACKTRACE // timing experiment only: forward sweep alone
@@ -1114,14 +1232,24 @@ extern "C" hipError_t gwamd_internal_banded_launch(const gwamd::aln::Args* a, in
         return hipSuccess;
     if (algo == 2)
     {
+        const int nwv = a->band_waves;
+        if (nwv != 1 && nwv != 4 && nwv != 8)
+            return hipErrorInvalidValue;
+        const void* k = nwv == 4   ? reinterpret_cast<const void*>(myers_banded_kernel<4>)
+                        : nwv == 8 ? reinterpret_cast<const void*>(myers_banded_kernel<8>)
+                                   : reinterpret_cast<const void*>(myers_banded_kernel<1>);
         if (a->lds_bytes > 65536)
         {
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(myers_banded_kernel),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, a->lds_bytes);
+            const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, a->lds_bytes);
             if (e != hipSuccess)
                 return e;
         }
-        hipLaunchKernelGGL(myers_banded_kernel, dim3(grid), dim3(kWave), size_t(a->lds_bytes), stream, *a);
+        if (nwv == 4)
+            hipLaunchKernelGGL(myers_banded_kernel<4>, dim3(grid), dim3(kWave * 4), size_t(a->lds_bytes), stream, *a);
+        else if (nwv == 8)
+            hipLaunchKernelGGL(myers_banded_kernel<8>, dim3(grid), dim3(kWave * 8), size_t(a->lds_bytes), stream, *a);
+        else
+            hipLaunchKernelGGL(myers_banded_kernel<1>, dim3(grid), dim3(kWave), size_t(a->lds_bytes), stream, *a);
     }
     else if (a->uk_threads > 0)
     {
@@ -1150,20 +1278,26 @@ extern "C" hipError_t gwamd_internal_banded_launch(const gwamd::aln::Args* a, in
     return hipGetLastError();
 }
 
-extern "C" hipError_t gwamd_internal_banded_occupancy(int algo, int lds_bytes, int* blocks_per_cu)
+extern "C" hipError_t gwamd_internal_banded_occupancy(int algo, int lds_bytes, int band_waves, int* blocks_per_cu)
 {
     using namespace gwamd::aln;
     if (algo == 2)
     {
-        if (lds_bytes > 65536)
-        {
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(myers_banded_kernel),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
-            if (e != hipSuccess)
-                return e;
-        }
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, myers_banded_kernel, kWave,
-                                                            size_t(lds_bytes));
+        auto occ = [&](auto kern, int threads) -> hipError_t {
+            if (lds_bytes > 65536)
+            {
+                const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+                if (e != hipSuccess)
+                    return e;
+            }
+            return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, kern, threads, size_t(lds_bytes));
+        };
+        if (band_waves == 4)
+            return occ(myers_banded_kernel<4>, kWave * 4);
+        if (band_waves == 8)
+            return occ(myers_banded_kernel<8>, kWave * 8);
+        return occ(myers_banded_kernel<1>, kWave);
     }
     if (lds_bytes > 65536)
     {

@@ -94,7 +94,7 @@ inline void aligner_max_lengths(int32_t algo, int32_t& max_query, int32_t& max_t
 extern "C" hipError_t gwamd_internal_align_launch(const gwamd::aln::Args* a, int algo, int grid, hipStream_t stream);
 extern "C" hipError_t gwamd_internal_align_occupancy(int algo, int lds_bytes, int* blocks_per_cu);
 extern "C" hipError_t gwamd_internal_banded_launch(const gwamd::aln::Args* a, int algo, int grid, hipStream_t stream);
-extern "C" hipError_t gwamd_internal_banded_occupancy(int algo, int lds_bytes, int* blocks_per_cu);
+extern "C" hipError_t gwamd_internal_banded_occupancy(int algo, int lds_bytes, int band_waves, int* blocks_per_cu);
 extern "C" hipError_t gwamd_internal_ukkonen_wide_occupancy(int threads, int lds_bytes, int* blocks_per_cu);
 
 namespace claraparabricks
@@ -512,7 +512,7 @@ private:
             // the state in HBM and wait on it every column)
             tile_bytes_      = 4096;
             int64_t want     = a16(int64_t(pat_words) * 16);
-            want             = std::min<int64_t>(want, (163840 - lds_tile_off_) & ~int64_t(511));
+            want             = std::min<int64_t>(want, (163840 - 512 - lds_tile_off_) & ~int64_t(511)); // static LDS
             if (const char* tb = gwamd::host::diag_env("GWAMD_BAND_TILE_BYTES")) // parity tests: HBM chunk state
             {
                 // LDS bytes for the chunk state: 4096 (256 words, the minimum
@@ -526,6 +526,17 @@ private:
             }
             if (want > tile_bytes_)
                 tile_bytes_ = int32_t(want);
+            // long queries (bands of many 32-word chunks) run 4 waves per pair,
+            // 8 target columns in flight; short ones keep one wave per pair
+            // and their occupancy
+            band_waves_ = max_q_ > 8192 ? 4 : 1;
+            if (const char* bwv = gwamd::host::diag_env("GWAMD_BAND_WAVES"))
+            {
+                const std::string v(bwv);
+                if (v != "1" && v != "4" && v != "8")
+                    throw std::invalid_argument("GWAMD_BAND_WAVES must be 1, 4 or 8");
+                band_waves_ = std::stoi(v);
+            }
             lds_bytes_       = lds_tile_off_ + tile_bytes_;
             // band entries (pv, mv, score, pad) of the widest band (the whole query)
             slot_bytes_ = a16(int64_t(pat_words) * (max_t_ + 1) * 16 + 64);
@@ -558,7 +569,7 @@ private:
             throw std::invalid_argument("aligner problem size does not fit in LDS");
         pat_words_ = pat_words;
         int per_cu = 1, cus = 1;
-        GWAMD_HIP_CHECK(gwamd_internal_banded_occupancy(algo_, lds_bytes_, &per_cu));
+        GWAMD_HIP_CHECK(gwamd_internal_banded_occupancy(algo_, lds_bytes_, band_waves_, &per_cu));
         if (algo_ == GWAMD_ALIGNER_UKKONEN && ukkonen_band_rows() > kUkChunks * kWave)
         {
             // batches with wide bands run one workgroup per pair
@@ -694,6 +705,7 @@ private:
         a.tile_bytes       = tile_bytes_;
         a.ukkonen_p        = gwamd::aln::kUkkonenP;
         a.uk_threads       = 0; // launch(): the batch's widest band may need ukkonen_wide_kernel
+        a.band_waves       = band_waves_;
         a.lds_edge_off     = lds_edge_off_;
         a.stats            = d_stats_;
         return a;
@@ -714,7 +726,7 @@ private:
     bool tcod_hbm_     = false;
     bool long_mode_    = false;
     int32_t stripe_blocks_ = gwamd::aln::kMaxChunks;
-    int32_t lds_seq2_off_ = 0, lds_tile_off_ = 0, tile_bytes_ = 0;
+    int32_t lds_seq2_off_ = 0, lds_tile_off_ = 0, tile_bytes_ = 0, band_waves_ = 1;
     int32_t lds_edge_off_ = 0, uk_narrow_tile_off_ = 0, uk_narrow_lds_ = 0, uk_wide_lds_ = 0;
     int32_t max_diff_ = 0; // largest |query - target| of the batch
     int32_t slots_ = 1;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: banded Myers chunk state in LDS up to 160 KiB: long-pair parity,
+# Round 4: banded Myers chunk state in LDS up to 160 KiB, multi-wave sweep: long-pair parity,
 # then the D_banded_64k and D_banded lines.
 cd "$(dirname "$0")/.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0

@@ -111,11 +111,14 @@ def test_myers_banded_chunk_state_in_hbm(monkeypatch):
         assert g == oracle.align(q, tt, oracle.ALIGN_MYERS_BANDED, mq)
 
 
-def test_myers_banded_two_column_sweep():
+@pytest.mark.parametrize("waves", ["1", "4", "8"])
+def test_myers_banded_two_column_sweep(waves, monkeypatch):
     # bands of several 32-word chunks with their state in LDS run two target
-    # columns per pass (one per half wave, the second two chunks behind):
-    # odd and even target lengths (the last pass with one column), stripes
-    # and diagonal bands, up to the whole query (375 words, 12 chunks)
+    # columns per wave (one per half wave, each column two chunks behind the
+    # previous one; 4 or 8 waves per pair: 8 or 16 columns in flight): target
+    # lengths that leave partial last groups, stripes and diagonal bands, up
+    # to the whole query (375 words, 12 chunks)
+    monkeypatch.setenv("GWAMD_BAND_WAVES", waves)
     rng = random.Random(43)
     t = rand_seq(rng, 12000)
     pairs = [(mutate(rng, t, 0.45), t), (rand_seq(rng, 11000), t[:11001]),
