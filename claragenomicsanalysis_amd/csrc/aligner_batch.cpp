@@ -526,10 +526,10 @@ private:
             }
             if (want > tile_bytes_)
                 tile_bytes_ = int32_t(want);
-            // long queries (bands of many 32-word chunks) run 4 waves per pair,
-            // 8 target columns in flight; short ones keep one wave per pair
+            // long queries (bands of many 32-word chunks) run 8 waves per pair,
+            // 16 target columns in flight; short ones keep one wave per pair
             // and their occupancy
-            band_waves_ = max_q_ > 8192 ? 4 : 1;
+            band_waves_ = max_q_ > 8192 ? 8 : 1;
             if (const char* bwv = gwamd::host::diag_env("GWAMD_BAND_WAVES"))
             {
                 const std::string v(bwv);
