@@ -1233,11 +1233,12 @@ extern "C" hipError_t gwamd_internal_banded_launch(const gwamd::aln::Args* a, in
     if (algo == 2)
     {
         const int nwv = a->band_waves;
-        if (nwv != 1 && nwv != 4 && nwv != 8)
+        if (nwv != 1 && nwv != 4 && nwv != 8 && nwv != 16)
             return hipErrorInvalidValue;
-        const void* k = nwv == 4   ? reinterpret_cast<const void*>(myers_banded_kernel<4>)
-                        : nwv == 8 ? reinterpret_cast<const void*>(myers_banded_kernel<8>)
-                                   : reinterpret_cast<const void*>(myers_banded_kernel<1>);
+        const void* k = nwv == 4    ? reinterpret_cast<const void*>(myers_banded_kernel<4>)
+                        : nwv == 8  ? reinterpret_cast<const void*>(myers_banded_kernel<8>)
+                        : nwv == 16 ? reinterpret_cast<const void*>(myers_banded_kernel<16>)
+                                    : reinterpret_cast<const void*>(myers_banded_kernel<1>);
         if (a->lds_bytes > 65536)
         {
             const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, a->lds_bytes);
@@ -1248,6 +1249,8 @@ extern "C" hipError_t gwamd_internal_banded_launch(const gwamd::aln::Args* a, in
             hipLaunchKernelGGL(myers_banded_kernel<4>, dim3(grid), dim3(kWave * 4), size_t(a->lds_bytes), stream, *a);
         else if (nwv == 8)
             hipLaunchKernelGGL(myers_banded_kernel<8>, dim3(grid), dim3(kWave * 8), size_t(a->lds_bytes), stream, *a);
+        else if (nwv == 16)
+            hipLaunchKernelGGL(myers_banded_kernel<16>, dim3(grid), dim3(kWave * 16), size_t(a->lds_bytes), stream, *a);
         else
             hipLaunchKernelGGL(myers_banded_kernel<1>, dim3(grid), dim3(kWave), size_t(a->lds_bytes), stream, *a);
     }
@@ -1297,6 +1300,8 @@ extern "C" hipError_t gwamd_internal_banded_occupancy(int algo, int lds_bytes, i
             return occ(myers_banded_kernel<4>, kWave * 4);
         if (band_waves == 8)
             return occ(myers_banded_kernel<8>, kWave * 8);
+        if (band_waves == 16)
+            return occ(myers_banded_kernel<16>, kWave * 16);
         return occ(myers_banded_kernel<1>, kWave);
     }
     if (lds_bytes > 65536)

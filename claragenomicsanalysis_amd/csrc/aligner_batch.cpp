@@ -533,8 +533,8 @@ private:
             if (const char* bwv = gwamd::host::diag_env("GWAMD_BAND_WAVES"))
             {
                 const std::string v(bwv);
-                if (v != "1" && v != "4" && v != "8")
-                    throw std::invalid_argument("GWAMD_BAND_WAVES must be 1, 4 or 8");
+                if (v != "1" && v != "4" && v != "8" && v != "16")
+                    throw std::invalid_argument("GWAMD_BAND_WAVES must be 1, 4, 8 or 16");
                 band_waves_ = std::stoi(v);
             }
             lds_bytes_       = lds_tile_off_ + tile_bytes_;

@@ -78,7 +78,7 @@ struct Args
     int32_t ukkonen_p;       // AlignerGlobalUkkonen::ukkonen_p_ (aligner_global_ukkonen.cpp:29)
     int32_t uk_threads;      // Ukkonen: > 0 runs ukkonen_wide_kernel with this many threads per pair
     int32_t lds_edge_off;    //   its 64-row-group edge values (2 x 2 x kUkWideChunks*16 int)
-    int32_t band_waves;      // banded Myers: waves per pair (1, 4 or 8; myers_banded_kernel<NWV>)
+    int32_t band_waves;      // banded Myers: waves per pair (1, 4, 8 or 16; myers_banded_kernel<NWV>)
     // path counters, accumulated over the aligner's launches (gwamd_aligner_get_stats):
     // [0] banded Myers sweeps whose chunk state went through HBM, [1] pairs
     // aligned by ukkonen_wide_kernel

@@ -111,7 +111,7 @@ def test_myers_banded_chunk_state_in_hbm(monkeypatch):
         assert g == oracle.align(q, tt, oracle.ALIGN_MYERS_BANDED, mq)
 
 
-@pytest.mark.parametrize("waves", ["1", "4", "8"])
+@pytest.mark.parametrize("waves", ["1", "4", "8", "16"])
 def test_myers_banded_two_column_sweep(waves, monkeypatch):
     # bands of several 32-word chunks with their state in LDS run two target
     # columns per wave (one per half wave, each column two chunks behind the
