@@ -654,8 +654,12 @@ __device__ int leaf_lane(PatPtr pat, int pat_words, int qb, int qe,
 // LONG (queries over 16,384 or targets over 65,535 bases): query patterns in
 // the HBM slot instead of LDS, 32-bit split scores, and halves taller than
 // kMaxChunks blocks swept in stripes (half_sweep_striped).
+// 4 waves per SIMD: 120 VGPRs instead of 152 (3 waves), no VGPR spills; the
+// LDS image (~9.4 KB at 5 kb pairs) allows 17 workgroups per CU.  Measured
+// (gpurun_out/r4l): 243.6k -> 261.6k alignments/s on config D; 5 waves per
+// SIMD (96 VGPRs, spills) 202k.
 template <bool LONG>
-__global__ void __launch_bounds__(kWave) hm_kernel(Args a)
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) hm_kernel(Args a)
 {
     using SC = typename std::conditional<LONG, uint32_t, uint16_t>::type; // split score
     using PatPtr = typename std::conditional<LONG, const uint32_t*, const GWAMD_LDS uint32_t*>::type;
