@@ -556,12 +556,23 @@ private:
             lds_seq2_off_       = int32_t(a16(stride_ + 16));
             const int64_t seqs  = lds_seq2_off_ + a16(stride_ + 16);
             uk_narrow_tile_off_ = int32_t(seqs);
-            uk_narrow_lds_      = int32_t(seqs + 8192); // 4096 int16 >= 3 columns of 512 band rows
+            // ukkonen_kernel's backtrace tile (the narrow kernel's only use of
+            // it; any size is correct, reads outside it go to HBM)
+            int32_t uk_tile     = 8192;
+            if (const char* tb = gwamd::host::diag_env("GWAMD_UK_TILE_BYTES"))
+            {
+                char* end    = nullptr;
+                const long v = std::strtol(tb, &end, 10);
+                if (end == tb || *end != '\0' || v < 1024 || v > 65536 || v % 512 != 0)
+                    throw std::invalid_argument("GWAMD_UK_TILE_BYTES must be 1024..65536 in steps of 512");
+                uk_tile = int32_t(v);
+            }
+            uk_narrow_lds_      = int32_t(seqs + uk_tile);
             lds_edge_off_       = int32_t(std::max<int64_t>(seqs, kUkTileRows * kUkTileCols * 2));
             uk_wide_lds_        = lds_edge_off_ + 4 * kUkWideChunks * 16 * 4;
             slot_bytes_         = a16(int64_t(rows) * (int64_t(max_q_) + max_t_ + 2) * 2 + 64);
             lds_bytes_          = uk_narrow_lds_;
-            tile_bytes_         = 8192;
+            tile_bytes_         = uk_tile;
             lds_tile_off_       = uk_narrow_tile_off_;
         }
         if (lds_bytes_ > 163840 ||
