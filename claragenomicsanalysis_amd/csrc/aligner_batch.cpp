@@ -505,24 +505,27 @@ private:
             lds_target_off_  = 0;
             lds_pat_off_     = int32_t(a16((max_t_ + 15) / 16 * 4 + 16));
             lds_tile_off_    = int32_t(lds_pat_off_ + a16(int64_t(pat_words) * 16 + 16));
-            // at least 256 16-byte band entries (two columns of 128 words, or
-            // 256 chunk words); up to the whole band's chunk state while the
+            // at least 128 16-byte band entries (two columns of 64 words, or
+            // 128 chunk words: a smaller LDS image keeps more short pairs
+            // resident, D_banded 372.8k -> 451.7k alignments/s with 2 KiB
+            // against 4 KiB, gpurun_out/r4o); up to the whole band's chunk state while the
             // workgroup's LDS stays within the CU's 160 KiB (a 65,536 bp query:
             // 16 KiB target + 32 KiB patterns + 32 KiB state; wider bands keep
             // the state in HBM and wait on it every column)
-            tile_bytes_      = 4096;
+            tile_bytes_      = 2048;
             int64_t want     = a16(int64_t(pat_words) * 16);
             want             = std::min<int64_t>(want, (163840 - 512 - lds_tile_off_) & ~int64_t(511)); // static LDS
             if (const char* tb = gwamd::host::diag_env("GWAMD_BAND_TILE_BYTES")) // parity tests: HBM chunk state
             {
-                // LDS bytes for the chunk state: 4096 (256 words, the minimum
-                // tile) up to 48 KiB, in whole 512-byte steps; anything else
+                // LDS bytes for the chunk state / backtrace tile: 2048 (128
+                // words) up to 48 KiB, in whole 512-byte steps; anything else
                 // is a typo that would silently keep the default plan
                 char* end     = nullptr;
                 const long v  = std::strtol(tb, &end, 10);
-                if (end == tb || *end != '\0' || v < 4096 || v > (48 << 10) || v % 512 != 0)
-                    throw std::invalid_argument("GWAMD_BAND_TILE_BYTES must be 4096..49152 in steps of 512");
-                want = v;
+                if (end == tb || *end != '\0' || v < 2048 || v > (48 << 10) || v % 512 != 0)
+                    throw std::invalid_argument("GWAMD_BAND_TILE_BYTES must be 2048..49152 in steps of 512");
+                tile_bytes_ = int32_t(v);
+                want        = v;
             }
             if (want > tile_bytes_)
                 tile_bytes_ = int32_t(want);
