@@ -151,6 +151,9 @@ def parse():
     p.add_argument("--stream-step-windows", type=int, default=None,
                    help="E: windows per step (default %d; 20 steps = 125k windows per GPU)" % E_STEP_WINDOWS)
     p.add_argument("--secondary-c-steps", type=int, default=3, help="timed steps of the default run's C object")
+    p.add_argument("--cpus", type=int, default=None,
+                   help="pin each rank to K host CPUs (rank r: the r-th K of its affinity set) before any GPU "
+                        "call, to predict a host-bound multi-GPU run on one GPU")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU rehearsal of the multi-rank launch (gloo): config E with stand-in rows instead of the "
                         "GPU engine; prints a line marked dry_run that is not a measurement")
@@ -894,10 +897,24 @@ def relaunch(args):
     return subprocess.call(cmd, env=env)
 
 
+def pin_cpus(k):
+    """--cpus K: restrict this rank (and the batch host threads it starts) to
+    K CPUs of its affinity set, rank r taking the r-th group of K, so that one
+    GPU can rehearse the host share a rank gets at N GPUs (the driver's cgroup
+    grants 16 CPUs: 2 per rank at N = 8).  Called before any GPU call."""
+    cpus = sorted(os.sched_getaffinity(0))
+    r = int(os.environ.get("LOCAL_RANK", "0"))
+    pick = cpus[r * k:(r + 1) * k] or cpus[:k]
+    os.sched_setaffinity(0, pick)
+    os.environ["OMP_NUM_THREADS"] = str(len(pick))
+    return pick
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(relaunch(args))
+    pinned = pin_cpus(args.cpus) if args.cpus else None
     ctx = Ctx(dry=args.dry_run)
     if args.gpus > 1 and ctx.world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, ctx.world))
@@ -915,6 +932,8 @@ def main():
         if line is not None:
             line["secondary"] = sec
     if ctx.rank == 0 and line is not None:
+        if pinned is not None:
+            line.setdefault("config", {})["pinned_cpus"] = pinned
         print(json.dumps(line), flush=True)
     if ctx.world > 1:
         dist.destroy_process_group()

@@ -6,6 +6,7 @@ fails loudly: there is no fallback implementation.
 """
 import ctypes as C
 import os
+import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
@@ -14,7 +15,11 @@ _LIB = None
 def library_path():
     # GWAMD_LIBRARY: an alternative in-tree build (diagnostic builds), honoured
     # only with GWAMD_DIAG=1 like the library's own tuning variables
-    alt = os.environ.get("GWAMD_LIBRARY") if os.environ.get("GWAMD_DIAG") == "1" else None
+    alt = os.environ.get("GWAMD_LIBRARY")
+    if alt and os.environ.get("GWAMD_DIAG") != "1":
+        sys.stderr.write("gwamd: GWAMD_LIBRARY=%s ignored without GWAMD_DIAG=1; loading the default "
+                         "lib/libgwamd.so\n" % alt)
+        alt = None
     return alt or os.path.join(_HERE, "lib", "libgwamd.so")
 
 

@@ -652,7 +652,7 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
                 else
                 {
                     if (lane == 0)
-                        atomicAdd(a.stats, 1);
+                        atomicAdd(a.stats, 1ull);
                     ed = sweep(std::false_type{});
                 }
             }
@@ -1057,7 +1057,10 @@ __global__ void __launch_bounds__(1024) ukkonen_wide_kernel(Args a)
         const int kmax_even = (n - m + 2 * p) / 2 + 1;
         const int nck       = uni((bw + NT - 1) / NT); // <= kUkWideChunks (host plan)
         if (tid == 0)
-            atomicAdd(a.stats + 1, 1);
+        {
+            atomicAdd(a.stats + 1, 1ull);
+            atomicMax(a.stats + 2, (unsigned long long)nck);
+        }
 
         int V1[kUkWideChunks], V2[kUkWideChunks], V0[kUkWideChunks];
 #pragma unroll

@@ -297,7 +297,7 @@ public:
         dalloc(reinterpret_cast<void**>(&d_lens_), size_t(2) * max_n_ * 4);
         dalloc(reinterpret_cast<void**>(&d_paths_), size_t(max_result_) * max_n_ + 16);
         dalloc(reinterpret_cast<void**>(&d_plen_), size_t(max_n_) * 4);
-        dalloc(reinterpret_cast<void**>(&d_stats_), 16);
+        dalloc(reinterpret_cast<void**>(&d_stats_), 32);
         // workspace: every slot entry is written before it is read
         dalloc(reinterpret_cast<void**>(&d_ws_), size_t(slots_) * size_t(slot_bytes_), false);
         h_seqs_.reserve(size_t(2) * stride_ * max_n_ + 16, stream_);
@@ -455,11 +455,11 @@ public:
     void path_stats(int64_t* out)
     {
         ScopedDevice dev(device_id_);
-        int32_t v[2] = {0, 0};
+        unsigned long long v[3] = {0, 0, 0};
         GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
-        GWAMD_HIP_CHECK(hipMemcpy(v, d_stats_, 8, hipMemcpyDeviceToHost));
-        out[0] = v[0];
-        out[1] = v[1];
+        GWAMD_HIP_CHECK(hipMemcpy(v, d_stats_, sizeof(v), hipMemcpyDeviceToHost));
+        for (int i = 0; i < 3; i++)
+            out[i] = int64_t(v[i]);
     }
     int64_t device_bytes() const { return device_bytes_; }
 
@@ -750,7 +750,7 @@ private:
     int8_t* d_paths_  = nullptr;
     int32_t* d_plen_  = nullptr;
     uint8_t* d_ws_    = nullptr;
-    int32_t* d_stats_ = nullptr;
+    unsigned long long* d_stats_ = nullptr;
     PinnedBuf h_seqs_, h_lens_, h_paths_, h_plen_;
     std::vector<std::shared_ptr<Alignment>> alignments_;
 };
@@ -1013,13 +1013,20 @@ int32_t gwamd_aligner_get_config(const gwamd_aligner* a, int32_t* grid, int64_t*
     return 0;
 }
 
-int32_t gwamd_aligner_get_stats(gwamd_aligner* a, int64_t* hbm_state_sweeps, int64_t* ukkonen_wide_pairs)
+int32_t gwamd_aligner_get_stats(gwamd_aligner* a, int64_t* hbm_state_sweeps, int64_t* ukkonen_wide_pairs,
+                                int64_t* ukkonen_max_rows_per_thread)
 {
+    if (!a || !hbm_state_sweeps || !ukkonen_wide_pairs || !ukkonen_max_rows_per_thread)
+    {
+        gwamd::host::last_error() = "gwamd_aligner_get_stats: null argument";
+        return GWAMD_E_INVALID_ARGUMENT;
+    }
     return guarded_aln([&] {
-        int64_t v[2];
+        int64_t v[3];
         a->impl->path_stats(v);
-        *hbm_state_sweeps   = v[0];
-        *ukkonen_wide_pairs = v[1];
+        *hbm_state_sweeps            = v[0];
+        *ukkonen_wide_pairs          = v[1];
+        *ukkonen_max_rows_per_thread = v[2];
         return int32_t(0);
     });
 }

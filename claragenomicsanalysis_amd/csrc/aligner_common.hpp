@@ -81,8 +81,9 @@ struct Args
     int32_t band_waves;      // banded Myers: waves per pair (1, 4, 8 or 16; myers_banded_kernel<NWV>)
     // path counters, accumulated over the aligner's launches (gwamd_aligner_get_stats):
     // [0] banded Myers sweeps whose chunk state went through HBM, [1] pairs
-    // aligned by ukkonen_wide_kernel
-    int32_t* stats;
+    // aligned by ukkonen_wide_kernel, [2] the most band rows one thread of
+    // ukkonen_wide_kernel held (64-bit: long-lived aligners do not wrap)
+    unsigned long long* stats;
 };
 
 } // namespace aln

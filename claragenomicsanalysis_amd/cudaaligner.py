@@ -51,7 +51,7 @@ def _declare(L):
     L.gwamd_aligner_pair_fits.restype = i32
     L.gwamd_aligner_pair_fits.argtypes = [i32, i32, i32]
     L.gwamd_aligner_get_stats.restype = i32
-    L.gwamd_aligner_get_stats.argtypes = [vp, P(i64), P(i64)]
+    L.gwamd_aligner_get_stats.argtypes = [vp, P(i64), P(i64), P(i64)]
     del i8
 
 
@@ -230,9 +230,9 @@ class CudaAlignerBatch:
     def stats(self):
         """Path counters accumulated over this aligner's launches
         (gwamd_aligner_get_stats)."""
-        v, w = C.c_int64(), C.c_int64()
-        _check(self._lib.gwamd_aligner_get_stats(self._handle, C.byref(v), C.byref(w)))
-        return {"hbm_state_sweeps": v.value, "ukkonen_wide_pairs": w.value}
+        v, w, r = C.c_int64(), C.c_int64(), C.c_int64()
+        _check(self._lib.gwamd_aligner_get_stats(self._handle, C.byref(v), C.byref(w), C.byref(r)))
+        return {"hbm_state_sweeps": v.value, "ukkonen_wide_pairs": w.value, "ukkonen_max_rows_per_thread": r.value}
 
     def config(self):
         g, b = C.c_int32(), C.c_int64()

@@ -129,8 +129,12 @@ int32_t gwamd_aligner_pair_fits(int32_t algorithm, int32_t max_query_length, int
  * *hbm_state_sweeps = banded Myers band sweeps whose 32-word chunk state went
  * through HBM (bands wider than the LDS chunk-state region);
  * *ukkonen_wide_pairs = Ukkonen pairs aligned by the workgroup kernel (batches
- * whose widest band exceeds one wave's 512 rows). */
-int32_t gwamd_aligner_get_stats(gwamd_aligner* aligner, int64_t* hbm_state_sweeps, int64_t* ukkonen_wide_pairs);
+ * whose widest band exceeds one wave's 512 rows);
+ * *ukkonen_max_rows_per_thread = the most band rows one thread of that kernel
+ * held (1-4).  Counters are 64-bit on the device.  NULL outputs:
+ * GWAMD_E_INVALID_ARGUMENT. */
+int32_t gwamd_aligner_get_stats(gwamd_aligner* aligner, int64_t* hbm_state_sweeps, int64_t* ukkonen_wide_pairs,
+                                int64_t* ukkonen_max_rows_per_thread);
 
 #ifdef __cplusplus
 }

@@ -63,8 +63,11 @@ def main():
     for algo in ("hirschberg_myers", "myers", "myers_banded", "ukkonen"):
         want.append(("BM_SingleBatchAlignment 65536, first pair (main.cpp:85-124)", "BM_SingleBatchAlignment",
                      65536, True, algo))
-    # Ukkonen between one wave's 512-row band and the 65,536 case (BM_SingleBatchAlignment
-    # sizes 512 x 4^k: 16,384 needs a 920-row band)
+    # Ukkonen at the 16,384 BM_SingleBatchAlignment size (512 x 4^k).  The
+    # recipe's pairs have equal lengths, so the band is ~101 rows and the
+    # single-wave kernel runs; the aligner only *sizes* its workspace for the
+    # 920-row band a 10 % length difference would need.  The wide kernel's
+    # 1-4 rows per thread are covered by test_ukkonen_wide_band_matches_oracle.
     want.append(("BM_SingleBatchAlignment 16384, first pair (main.cpp:85-124)", "BM_SingleBatchAlignment",
                  16384, True, "ukkonen"))
     cases = [have.get((w[1], w[2], w[4])) or case(*w) for w in want]

@@ -156,19 +156,23 @@ def test_reference_benchmark_pairs_golden(c):
 # Ukkonen bands wider than one wave (ukkonen_wide_kernel): the reference runs
 # any band with up to 1,024 threads per pair (ukkonen_gpu.cu:213-293); pairs
 # whose length differs by up to 10 % of the target at 12 kb and 18 kb need
-# 700-1,000 band rows, a 30 kb one 1,600
-@pytest.mark.parametrize("T", [12000, 18000, 30000])
+# 700-1,000 band rows (1 row per thread), a 30 kb one 1,600 (2 rows); at 45 kb
+# and 64 kb a ~9-10 % shorter query needs ~2,300 / ~3,300 rows, so each of the
+# 1,024 threads holds 3 / 4 rows (64-row edge groups 32-63)
+@pytest.mark.parametrize("T", [12000, 18000, 30000, 45000, 64000])
 def test_ukkonen_wide_band_matches_oracle(T):
     rng = random.Random(T)
     t = rand_seq(rng, T)
     d = int(T * 0.1) - 3
     q1 = mutate(rng, t, 0.04)[: T - d]              # query shorter by ~10 %
     q2 = mutate(rng, t, 0.08)[: T - d // 2] + "ACGT"
-    q3 = t + rand_seq(rng, d // 3)                  # query longer (swapped roles)
+    q3 = t + rand_seq(rng, min(d // 3, 65536 - T))  # query longer (swapped roles)
     pairs = [(q1, t), (q2, t), (q3, t)]
     st = {}
     got, mq = gpu_states(pairs, "ukkonen", max(len(q) for q, _ in pairs), T, stats=st)
     assert st["ukkonen_wide_pairs"] == len(pairs)
+    if T >= 45000:
+        assert st["ukkonen_max_rows_per_thread"] >= (3 if T < 60000 else 4)
     for (q, tt), g in zip(pairs, got):
         assert g == oracle.align(q, tt, oracle.ALIGN_UKKONEN, mq), (len(q), len(tt))
 

@@ -594,3 +594,49 @@ def test_topsort_queue_ring(mode, monkeypatch):
             assert got[i] == r.msa, i
         else:
             assert (cons[i], cov[i]) == (r.consensus, r.coverage), i
+
+
+@pytest.mark.parametrize("fwd", ["v2", "v1"])
+def test_marked_rows_multi_source_fwd2(fwd, monkeypatch):
+    # Pins the round-4 workaround of a ROCm 7.2 miscompile ("A
+    # backend miscompile worked around"): rows marked for the general path
+    # (sources, non-ACGT bases, far predecessors) read the virtual row 0 or the
+    # ring through their own loader.  These windows are built to have several
+    # source nodes (reads that start with bases the graph does not have, so
+    # the alignment inserts them before the first node) and non-ACGT bases (N,
+    # lower case), and run on the LDS kernel with the default scores, for
+    # which the row-program forward pass (fwd2) is selected; GWAMD_POA_FWD=v1
+    # (diagnostic) runs the round-3 pass on the same windows.  Both must equal
+    # the oracle; the oracle's graphs show the windows really have >= 2 sources.
+    monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    if fwd == "v1":
+        monkeypatch.setenv("GWAMD_DIAG", "1")
+        monkeypatch.setenv("GWAMD_POA_FWD", "v1")
+    else:
+        monkeypatch.delenv("GWAMD_POA_FWD", raising=False)
+    import random
+    rng = random.Random(5)
+    wins = []
+    for k in range(12):
+        bb = "".join(rng.choice("ACGT") for _ in range(300 + 40 * k))
+        reads = [bb]
+        for j in range(10):
+            r = list(bb[rng.randrange(0, 20):len(bb) - rng.randrange(0, 20)])
+            for _ in range(12):
+                p = rng.randrange(len(r))
+                r[p] = rng.choice("ACGTN" if j % 3 == 0 else "ACGT")
+            head = "".join(rng.choice("ACGT") for _ in range(rng.randrange(3, 30))) if j % 2 == 0 else ""
+            reads.append((head + "".join(r)).encode())
+        reads[0] = reads[0].encode()
+        if k % 4 == 3:
+            reads[3] = reads[3].lower()  # lower-case bases are not ACGT either
+        wins.append(reads)
+    b = run_gpu(wins, 900, 12)
+    assert b.kernel_variant() == 2
+    cons, cov, st = b.get_consensus()
+    multi = 0
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 900, 12, want_graph=True)
+        assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), (fwd, i)
+        multi += sum(1 for ins in r.graph["in"] if not ins) >= 2
+    assert multi >= 10
