@@ -236,8 +236,19 @@ __device__ __forceinline__ int band_row_program(WinGraph<SizeT> g, int V, const 
                 p2 = pred_row(g, node[u], 2);
                 p3 = n == 4 ? pred_row(g, node[u], 3) : r;
             }
-            const bool near2 = n <= 4 && (n < 1 || r - p0[u] < 32768) && (n < 2 || r - p1[u] < 32768) &&
-                               (n < 3 || (r - p2 < 32768 && r - p3 < 32768));
+            bool near2 = n <= 4 && (n < 1 || r - p0[u] < 32768) && (n < 2 || r - p1[u] < 32768) &&
+                         (n < 3 || (r - p2 < 32768 && r - p3 < 32768));
+            if (B.bw > 1016 && near2 && valid)
+            {
+                // rec_e holds band shifts / 4 clamped to 255, which stands for
+                // "cuts every group" only while bw + 4 <= 1,020: rows of wider
+                // bands with a shift that large list their predecessors instead
+                const int bsr = B.start(r);
+                auto big      = [&](int pk) { return bsr - (pk == 0 ? 0 : B.start(pk)) >= 1020; };
+                if ((n == 0 && big(0)) || (n >= 1 && big(p0[u])) || (n >= 2 && big(p1[u])) ||
+                    (n >= 3 && big(p2)) || (n >= 4 && big(p3)))
+                    near2 = false;
+            }
             const int listed = near2 ? 0 : n;
             int total        = 0;
             const int excl   = wave_excl_sum(listed, lane, total);
@@ -420,8 +431,19 @@ __device__ __forceinline__ void band_fetch(int p, int d, int r, const int (&Hp)[
 // predecessor loops.  Row records and read bytes are software-pipelined: the
 // record of row r+2 and the read bytes of row r+1 are requested while row r is
 // computed.
+// Band widths 128 / 256 / 512 (CPL 2, 4, 8) keep their read bytes in one
+// integer; the wider classes (CPL 6, 10, 12, 14, 16: band widths 384 - 1,024,
+// any multiple of 128 the reference accepts, batch.hpp:85-94) in CPL/2
+// 16-bit pieces (band starts are multiples of 4, CPL*lane is even).
 template <int CPL>
-using ReadBytesT = typename std::conditional<(CPL > 4), uint64_t, uint32_t>::type;
+struct ReadPieces
+{
+    uint32_t h[CPL / 2];
+};
+template <int CPL>
+using ReadBytesT = typename std::conditional<
+    (CPL == 2 || CPL == 4), uint32_t,
+    typename std::conditional<(CPL == 8), uint64_t, ReadPieces<CPL>>::type>::type;
 
 template <typename ScoreT, int CPL>
 __device__ __forceinline__ ReadBytesT<CPL> band_read_bytes(GWAMD_LDS const uint8_t* read, int bs, int lane)
@@ -434,8 +456,27 @@ __device__ __forceinline__ ReadBytesT<CPL> band_read_bytes(GWAMD_LDS const uint8
     }
     else if constexpr (CPL == 4)
         return *reinterpret_cast<GWAMD_LDS const uint32_t*>(read + bs + 4 * lane);
-    else
+    else if constexpr (CPL == 2)
         return uint32_t(*reinterpret_cast<GWAMD_LDS const uint16_t*>(read + bs + 2 * lane));
+    else
+    {
+        ReadPieces<CPL> r;
+        const GWAMD_LDS uint16_t* p = reinterpret_cast<GWAMD_LDS const uint16_t*>(read + bs + CPL * lane);
+#pragma unroll
+        for (int k = 0; k < CPL / 2; k++)
+            r.h[k] = p[k];
+        return r;
+    }
+}
+
+// read byte c of a lane's CPL bytes
+template <int CPL>
+__device__ __forceinline__ int band_read_byte(const ReadBytesT<CPL>& rb, int c)
+{
+    if constexpr (CPL == 2 || CPL == 4 || CPL == 8)
+        return int((rb >> (8 * c)) & 0xffu);
+    else
+        return int((rb.h[c / 2] >> (8 * (c & 1))) & 0xffu);
 }
 
 template <typename ScoreT, typename SizeT, int CPL>
@@ -540,7 +581,7 @@ __device__ __forceinline__ int band_forward(WinGraph<SizeT> g, BandAux X, int V,
             int sig[CPL];
 #pragma unroll
             for (int c = 0; c < CPL; c++)
-                sig[c] = (int((rbw >> (8 * c)) & 0xffu) == gb) ? sc.match : sc.mismatch;
+                sig[c] = (band_read_byte<CPL>(rbw, c) == gb) ? sc.match : sc.mismatch;
 
             int v[CPL];
             int carry;
@@ -803,10 +844,26 @@ __device__ __forceinline__ int band_forward(WinGraph<SizeT> g, BandAux X, int V,
                                         (uint32_t(code[3]) << 24);
                     *reinterpret_cast<uint32_t*>(crow) = w4;
                 }
-                else
+                else if constexpr (CPL == 2)
                 {
                     const uint16_t w2 = uint16_t(code[0] | (code[1 % CPL] << 8));
                     *reinterpret_cast<uint16_t*>(crow) = w2;
+                }
+                else if constexpr (CPL % 4 == 0)
+                {
+                    // CPL 12, 16: 4-byte aligned (bw and CPL*lane are multiples of 4)
+#pragma unroll
+                    for (int k = 0; k < CPL / 4; k++)
+                        reinterpret_cast<uint32_t*>(crow)[k] =
+                            uint32_t(code[4 * k]) | (uint32_t(code[4 * k + 1]) << 8) |
+                            (uint32_t(code[4 * k + 2]) << 16) | (uint32_t(code[4 * k + 3]) << 24);
+                }
+                else
+                {
+                    // CPL 6, 10, 14: 2-byte aligned pieces
+#pragma unroll
+                    for (int k = 0; k < CPL / 2; k++)
+                        reinterpret_cast<uint16_t*>(crow)[k] = uint16_t(code[2 * k] | (code[2 * k + 1] << 8));
                 }
             }
             // end cell candidates (sinks in topological order, strict >)
@@ -970,28 +1027,35 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
         const uint64_t tt0 = BandProf::now();
         ti0 = max(1, ii - (kBandTile - 1));
         wave_sync();
-        // 4*CPL 16-B pieces per lane, all loads issued before the first store waits
+        // 4*CPL 16-B pieces per lane, all loads of a chunk issued before its
+        // first store waits (band widths past 512: chunks of 16 pieces, so the
+        // staging stays within 64 VGPRs)
         constexpr int kPer    = 4 * CPL;
         constexpr int kPerRow = 4 * CPL; // 16-B pieces per code row
-        v4i_t q[kPer];
-#pragma unroll
-        for (int u = 0; u < kPer; u++)
-        {
-            const int t  = u * kWave + lane;
-            const int rr = min(ti0 + t / kPerRow, V); // rows past V: never read
-            q[u]         = *reinterpret_cast<const v4i_t*>(X.codes + size_t(rr) * bw + (t % kPerRow) * 16);
-        }
+        constexpr int kCh     = kPer > 32 ? (kPer % 16 == 0 ? 16 : 8) : kPer;
+        static_assert(kPer % kCh == 0, "whole chunks");
         {
             const int rr = min(ti0 + lane, V); // kBandTile == kWave: one record per lane
             ta           = X.reca[rr];
             tb           = X.recb[rr];
             tcw          = X.recc[rr];
         }
-#pragma unroll
-        for (int u = 0; u < kPer; u++)
+        for (int u0 = 0; u0 < kPer; u0 += kCh)
         {
-            const int t = u * kWave + lane;
-            *reinterpret_cast<GWAMD_LDS v4i_t*>(tile + (t / kPerRow) * bw + (t % kPerRow) * 16) = q[u];
+            v4i_t q[kCh];
+#pragma unroll
+            for (int u = 0; u < kCh; u++)
+            {
+                const int t  = (u0 + u) * kWave + lane;
+                const int rr = min(ti0 + t / kPerRow, V); // rows past V: never read
+                q[u]         = *reinterpret_cast<const v4i_t*>(X.codes + size_t(rr) * bw + (t % kPerRow) * 16);
+            }
+#pragma unroll
+            for (int u = 0; u < kCh; u++)
+            {
+                const int t = (u0 + u) * kWave + lane;
+                *reinterpret_cast<GWAMD_LDS v4i_t*>(tile + (t / kPerRow) * bw + (t % kPerRow) * 16) = q[u];
+            }
         }
         {
             // per tile row (lane k: row ti0 + k), what a move decode needs:
@@ -1583,7 +1647,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
 // GWAMD_BAND_TU_CPL) so the three instantiation sets build in parallel;
 // poa_band_dispatch.cpp picks the one the plan needs.
 #ifndef GWAMD_BAND_TU_CPL
-#error "poa_band.hip is built through poa_band_c2.hip, poa_band_c4.hip and poa_band_c8.hip"
+#error "poa_band.hip is built through poa_band_c<CPL>.hip (CPL 2, 4, 6, 8, 10, 12, 14, 16)"
 #endif
 #define GWAMD_BAND_CAT2(a, b) a##b
 #define GWAMD_BAND_CAT(a, b) GWAMD_BAND_CAT2(a, b)

@@ -675,8 +675,8 @@ private:
         dims_.aux_stride     = code_b + cr_b;
     }
 
-    // Banded kernel (poa_window_kernel_band, poa_band.hip): band widths of 128
-    // or 256 (2 or 4 cells per lane), gap <= 0.  LDS image per window: staged
+    // Banded kernel (poa_window_kernel_band, poa_band.hip): band widths 128 to
+    // 1,024 in steps of 128 (2 to 16 cells per lane), gap <= 0.  LDS image per window: staged
     // read | work region (row-program flags, the 16-row ring of band rows, the
     // traceback tile, the add-alignment scratch; the topological sort also
     // reuses the read) | shared words.  Windows per CU: 4, 2 or 1, the most
@@ -732,12 +732,16 @@ private:
         if (env && std::string(env) == "v1")
             return;
         const int bw = dims_.band_width;
-        if ((bw != 128 && bw != 256 && bw != 512) || gap_ > 0)
+        // every band width the reference accepts up to 1,024 (multiples of
+        // 128, batch.hpp:85-94): CPL = bw / 64 cells per lane, one translation
+        // unit per CPL (poa_band_c<CPL>.hip)
+        if (bw % 128 != 0 || bw < 128 || bw > 1024 || gap_ > 0)
             return;
         auto a16          = [](int64_t v) { return (v + 15) & ~int64_t(15); };
         const int cpl     = bw / 64;
         const int sbytes  = score_bits_ / 8;
-        const int rowsz   = bw + gwamd::poa::kBandPad + cpl;
+        // band row: position idx + cpl - 1, whole cpl-cell groups (66-67 of them)
+        const int rowsz   = (bw + gwamd::poa::kBandPad + cpl + cpl - 1) / cpl * cpl;
         const int64_t ms  = dims_.max_seq_len, mn = dims_.max_nodes;
         const int64_t read_b  = a16(gwamd::poa::kReadGuard + ms + bw + 48);
         const int64_t sh_b    = 64;

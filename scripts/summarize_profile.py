@@ -50,7 +50,7 @@ def main(src, name, config="B", windows=1024, kernel="poa_window_kernel"):
         json.dump({"config": config, "windows": windows, "hbm_bytes_per_window": tot / windows,
                    "source": "profiles/" + name}, open(os.path.join(ROOT, "profiles", "traffic_poa_E.json"), "w"),
                   indent=1)
-    elif kernel == "poa_window_kernel":
+    elif kernel.startswith("poa_window_kernel"):
         json.dump({"config": config, "windows": windows, "hbm_bytes_per_launch": hbm, "source": "profiles/" + name},
                   open(os.path.join(ROOT, "profiles", "traffic_poa_%s.json" % config), "w"), indent=1)
     else:

@@ -113,19 +113,45 @@ def test_banded_parity_synthetic(bw):
         assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), i
 
 
-@pytest.mark.parametrize("bw", [384, 640, 1024])
-def test_banded_other_widths(bw):
-    # band widths the reference accepts beyond the LDS band kernel's 128 / 256 /
-    # 512 (any multiple of 128, batch.hpp:85-94): the global-memory kernel
+@pytest.mark.parametrize("variant", ["band", "v1"])
+@pytest.mark.parametrize("bw", [384, 640, 768, 896, 1024])
+def test_banded_other_widths(bw, variant, monkeypatch):
+    # every other band width the reference accepts up to 1,024 (multiples of
+    # 128, batch.hpp:85-94): the LDS band kernel with bw / 64 cells per lane
+    # (poa_band_c<CPL>.hip), and the global-memory kernel on the same windows;
+    # the windows include reads much shorter than the band, empty and
+    # one-base reads and a 60-read window (nodes with many predecessors)
+    if variant == "v1":
+        monkeypatch.setenv("GWAMD_POA_KERNEL", "v1")
+    else:
+        monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
     wins = synth.poa_windows(23, 6, 1000, 12, 40, 40, 40)
+    wins += synth.poa_windows(29, 2, 200, 8, 10, 10, 10)
+    wins.append([b"ACGTTGCA" * 20, b"ACGTTGCA" * 120, b"", b"A", b"GGGG" * 100, b"ACGTTGCA" * 20])
+    wins += synth.poa_windows(31, 1, 300, 60, 30, 30, 30)
     max_seq = 1100
-    b = run_gpu(wins, max_seq, 12, banded=True, bw=bw)
-    assert b.kernel_variant() == 1
+    b = run_gpu(wins, max_seq, 60, banded=True, bw=bw)
+    assert b.kernel_variant() == (1 if variant == "v1" else 3)
     sbits = b.get_types()[0]
     cons, cov, st = b.get_consensus()
     for i, w in enumerate(wins):
-        r = run_oracle(w, max_seq, 12, banded=True, bw=bw, score_bits=sbits)
-        assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), i
+        r = run_oracle(w, max_seq, 60, banded=True, bw=bw, score_bits=sbits)
+        assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), (bw, variant, i)
+
+
+@pytest.mark.parametrize("bw", [384, 1024])
+@pytest.mark.parametrize("spoa", [False, True])
+def test_banded_wide_msa_int32(bw, spoa, monkeypatch):
+    # wide bands with 32-bit scores (max_sequence_size 6000), MSA output and
+    # SPOA_ACCURATE, on the band kernel, against the oracle
+    monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    wins = synth.poa_windows(733, 4, 1500, 8, 75, 75, 75)
+    b = run_gpu(wins, 6000, 8, banded=True, bw=bw, output_type="msa", spoa_accurate=spoa)
+    assert b.kernel_variant() == 3 and b.get_types()[0] == 32
+    msa, st = b.get_msa()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, 6000, 8, banded=True, bw=bw, msa=True, score_bits=32, spoa_accurate=spoa)
+        assert (st[i], msa[i]) == (r.status, r.msa), (bw, spoa, i)
 
 
 def test_full_int32_long_reads():
