@@ -81,14 +81,15 @@ CONFIGS = {
     # BatchSize(10600, 16, 256) -> int32 scores and node ids
     "C": dict(backbone=10000, reads=16, err=500, max_seq=10600, banded=True, bw=256, windows=128, msa=True,
               mem_per_window=400e6),
-    # band widths past the LDS band kernel's 128 / 256 (the reference accepts any
-    # multiple of 128, batch.hpp:85-94): the global-memory kernel
+    # band widths past 256 (the reference accepts any multiple of 128,
+    # batch.hpp:85-94): the band kernel with bw / 64 cells per lane
     "B_banded_512": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=True, bw=512, windows=1024),
     "C_512": dict(backbone=10000, reads=16, err=500, max_seq=10600, banded=True, bw=512, windows=128, msa=True,
                   mem_per_window=600e6),
-    # shapes only the global-memory kernel takes (measured):
-    # band widths 384 and 1024, and full alignment with 32-bit scores (4 kb
-    # reads, 16 per window: use32bitScore, cudapoa_limits.hpp:28-53)
+    # shapes the global-memory kernel took until round 5: band widths 384 and
+    # 1024 (band kernel, 6 / 16 cells per lane), and full alignment with
+    # 32-bit scores (4 kb reads, 16 per window: use32bitScore,
+    # cudapoa_limits.hpp:28-53; the LDS kernel's 32-bit pass)
     "B_banded_384": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=True, bw=384, windows=1024),
     "B_banded_1024": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=True, bw=1024, windows=1024),
     "F_int32_4k": dict(backbone=4000, reads=16, err=200, max_seq=4400, banded=False, bw=256, windows=128,

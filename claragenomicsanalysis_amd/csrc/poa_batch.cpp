@@ -617,44 +617,84 @@ private:
         const char* env  = gwamd::host::diag_env("GWAMD_POA_KERNEL");
         if (env && std::string(env) == "v1")
             return;
-        if (banded_ || score_bits_ != 16 || size_bits_ != 16)
+        // 16-bit node ids; 16-bit scores, or 32-bit ones (the reference's
+        // use32bitScore batches: nw_forward_lds_w)
+        if (banded_ || size_bits_ != 16 || (score_bits_ != 16 && score_bits_ != 32))
             return;
+        const bool wide      = score_bits_ == 32;
         auto a16             = [](int64_t v) { return (v + 15) & ~int64_t(15); };
-        const int ring_rows  = 8;
+        int ring_rows        = 8;
         const int64_t read_b = a16(int64_t(dims_.max_seq_len) + 48);
         // forward pass shape: CPL columns per lane on NW waves; a sweep covers
         // NW*64*CPL read columns, longer reads take several sweeps
-        // (GWAMD_POA_LDS_SHAPE="cpl,waves")
+        // (GWAMD_POA_LDS_SHAPE="cpl,waves").  32-bit scores: one sweep up to
+        // 4,096 columns (8 waves), 8,192 with 16 columns per lane
         int cpl = 8, nw = 1;
         const int ms = dims_.max_seq_len;
-        if (ms > 512)
+        if (!wide && ms > 512)
             nw = 2;
+        if (wide)
+        {
+            nw  = ms <= 512 ? 1 : (ms <= 1024 ? 2 : (ms <= 2048 ? 4 : 8));
+            cpl = ms <= 4096 ? 8 : 16;
+        }
         if (const char* sh = gwamd::host::diag_env("GWAMD_POA_LDS_SHAPE"))
         {
             int c = 0, n = 0;
             if (std::sscanf(sh, "%d,%d", &c, &n) == 2)
             {
-                const bool known = (n == 1 && (c == 8 || c == 16 || c == 24 || c == 32)) ||
-                                   (c == 8 && n >= 2 && n <= 4) || (c == 16 && n == 4) || (c == 4 && n == 4);
+                const bool known =
+                    wide ? ((c == 8 && (n == 1 || n == 2 || n == 4 || n == 8)) || (c == 16 && n == 8))
+                         : ((n == 1 && (c == 8 || c == 16 || c == 24 || c == 32)) || (c == 8 && n >= 2 && n <= 4) ||
+                            (c == 16 && n == 4) || (c == 4 && n == 4));
                 if (!known)
                     throw std::invalid_argument("GWAMD_POA_LDS_SHAPE: unsupported columns/waves pair");
                 cpl = c, nw = n;
             }
         }
+        const int ebytes     = wide ? 4 : 2;
         const int64_t add_b  = 5 * a16(dims_.max_seq_len + 16) + 2 * (int64_t(dims_.max_nodes) + dims_.max_seq_len);
         const int64_t tile_b = int64_t(gwamd::poa::kTileRows) * gwamd::poa::kTileCols + gwamd::poa::kTbRankBytes;
-        const int64_t ring_b = a16(std::max<int64_t>({int64_t(ring_rows) * dims_.score_stride * 2, tile_b, add_b}));
         const int64_t rec_b  = a16(int64_t(dims_.max_nodes + 2) * 4);
-        const int64_t sh_b   = a16(gwamd::poa::kShBytes(nw));
-        const int64_t fixed  = read_b + ring_b + rec_b + sh_b;
-        const int64_t target = 40960 - 16; // 4 workgroups per CU incl. static LDS: one batch of
+        const int64_t sh_b   = a16(wide ? gwamd::poa::kShBytesW(nw) : gwamd::poa::kShBytes(nw));
+        auto ring_bytes      = [&](int rows) {
+            return a16(std::max<int64_t>({int64_t(rows) * dims_.score_stride * ebytes, tile_b, add_b}));
+        };
+        int64_t ring_b       = ring_bytes(ring_rows);
+        int64_t fixed        = read_b + ring_b + rec_b + sh_b;
+        int64_t target       = 40960 - 16; // 4 workgroups per CU incl. static LDS: one batch of
                                            // 1024 windows is resident on the 256 CUs at once
+        if (wide)
+        {
+            // 32-bit rows are twice as wide: two windows per CU when their
+            // images fit, else one; an 8-row ring when it fits, else 4 rows
+            // (predecessors farther back go through the HBM spill rows)
+            int64_t chosen = 0;
+            for (int64_t budget : {int64_t(81920 - 16), int64_t(163840 - 64)})
+            {
+                for (int rows : {8, 4})
+                {
+                    const int64_t rb = ring_bytes(rows);
+                    const int64_t fx = read_b + rb + rec_b + sh_b;
+                    if (fx + 2048 <= budget)
+                    {
+                        ring_rows = rows, ring_b = rb, fixed = fx, chosen = budget;
+                        break;
+                    }
+                }
+                if (chosen)
+                    break;
+            }
+            if (!chosen)
+                return;
+            target = chosen;
+        }
         int64_t xl_cap       = std::max<int64_t>(1024, (target - fixed) / 2);
         xl_cap               = std::min<int64_t>(xl_cap, 65535);
         int64_t total        = fixed + a16(xl_cap * 2);
         if (const char* pad = gwamd::host::diag_env("GWAMD_POA_LDS_PAD")) // diagnostic: fewer windows per CU
             total += a16(std::atoi(pad));
-        if (total > 65536)
+        if (total > (wide ? 163840 - 64 : 65536))
             return;
         dims_.lds_kernel    = 1;
         dims_.tb_rank       = tb_rank_default();
@@ -670,7 +710,7 @@ private:
         dims_.code_stride   = int32_t(a16(int64_t(dims_.max_seq_len) + 48));
         // HBM side buffer per window: traceback codes, span carries
         const int64_t code_b = int64_t(dims_.score_rows) * dims_.code_stride;
-        const int64_t cr_b   = a16(int64_t(dims_.max_nodes + 2) * 2);
+        const int64_t cr_b   = a16(int64_t(dims_.max_nodes + 2) * ebytes);
         dims_.aux_carry_off  = int32_t(code_b);
         dims_.aux_stride     = code_b + cr_b;
     }

@@ -110,6 +110,15 @@ constexpr int kShChan    = 128;
 constexpr int kChanRows  = 64;
 constexpr int kMaxWaves  = 4;
 constexpr int kShBytes(int waves) { return kShChan + (waves - 1) * kChanRows * 4; }
+// ... of the 32-bit pass (nw_forward_lds_w): end row, progress words (one per
+// wave, up to 8), the carries of the ring rows per wave, then the channels
+// ([waves-1][kChanRows] 64-bit words: row | carry << 32)
+constexpr int kShEndW   = 32;
+constexpr int kShProgW  = 64;
+constexpr int kShBndW   = 128; // [8 waves][8 ring rows] int32
+constexpr int kShChanW  = 384;
+constexpr int kMaxRingW = 8;
+constexpr int kShBytesW(int waves) { return kShChanW + (waves - 1) * kChanRows * 8; }
 
 constexpr int kTileRows = 128; // traceback tile (codes) rows
 constexpr int kTileCols = 128; // traceback tile columns (bytes)

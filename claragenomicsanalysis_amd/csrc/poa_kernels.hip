@@ -1147,15 +1147,19 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
 }
 
 #include "poa_fwd2.hpp"
+#include "poa_fwd_w.hpp"
 
 // LDS-resident POA kernel: one workgroup of NW waves per window.  The forward
 // pass and the traceback tile loads use every wave; the serial phases (graph
 // update, topological sort, consensus, MSA) run on wave 0 while the other
-// waves wait at the next barrier.
-template <bool MSA, int CPL, int NW>
-__global__ void __launch_bounds__(kWave * NW, NW >= 4 ? 4 : 1) poa_window_kernel_lds(Buffers b, Dims d, Scores sc)
+// waves wait at the next barrier.  W: 32-bit scores (nw_forward_lds_w, the
+// reference's use32bitScore batches), else 16-bit.
+template <bool MSA, int CPL, int NW, bool W>
+__global__ void __launch_bounds__(kWave * NW, W ? (NW >= 8 ? 2 : 1) : (NW >= 4 ? 4 : 1))
+    poa_window_kernel_lds(Buffers b, Dims d, Scores sc)
 {
     using SizeT  = int16_t;
+    using RowT   = typename std::conditional<W, int32_t, int16_t>::type; // E-domain row element
     extern __shared__ __align__(16) uint8_t lds[];
     __shared__ int sh_status;
     __shared__ int sh_len;
@@ -1170,7 +1174,7 @@ __global__ void __launch_bounds__(kWave * NW, NW >= 4 ? 4 : 1) poa_window_kernel
     const size_t slot  = blockIdx.x; // scratch slot (grid <= slots)
 
     uint8_t* lread   = lds;
-    int16_t* ring    = reinterpret_cast<int16_t*>(lds + d.lds_ring_off);
+    RowT* ring       = reinterpret_cast<RowT*>(lds + d.lds_ring_off);
     uint8_t* tile    = lds + d.lds_ring_off; // traceback tiles reuse the ring
     const int rstride = d.score_stride;      // ring / spill row stride (elements)
     GWAMD_LDS uint8_t* shb = (GWAMD_LDS uint8_t*)(lds) + d.lds_sh_off;
@@ -1206,11 +1210,11 @@ __global__ void __launch_bounds__(kWave * NW, NW >= 4 ? 4 : 1) poa_window_kernel
 
     SizeT* ag        = static_cast<SizeT*>(b.ag) + slot * d.aln_cap;
     SizeT* ar        = static_cast<SizeT*>(b.ar) + slot * d.aln_cap;
-    int16_t* spill   = static_cast<int16_t*>(b.scores) + slot * d.score_rows * size_t(rstride);
+    RowT* spill      = static_cast<RowT*>(b.scores) + slot * d.score_rows * size_t(rstride);
     uint8_t* codes   = b.codes + slot * size_t(d.aux_stride);
     uint32_t* rec    = reinterpret_cast<uint32_t*>(lds + d.lds_rec_off);
     uint16_t* xl     = reinterpret_cast<uint16_t*>(lds + d.lds_xl_off);
-    int16_t* carry   = reinterpret_cast<int16_t*>(codes + d.aux_carry_off);
+    RowT* carry      = reinterpret_cast<RowT*>(codes + d.aux_carry_off);
     RowProg P{rec, xl, d.lds_ring_rows - 1};
     int32_t* cscore  = b.cscore + slot * mn;
     SizeT* cpred     = static_cast<SizeT*>(b.cpred) + slot * mn * 4;
@@ -1225,7 +1229,7 @@ __global__ void __launch_bounds__(kWave * NW, NW >= 4 ? 4 : 1) poa_window_kernel
 #ifdef GWAMD_FWD_PROFILE
     const bool use_v2 = false;
 #else
-    const bool use_v2 = fwd2_ok(sc) && !(d.diag & 2);
+    const bool use_v2 = !W && fwd2_ok(sc) && !(d.diag & 2);
 #endif
     const WindowDesc wd = b.windows[w];
     const int nseq      = wd.num_seqs;
@@ -1263,15 +1267,20 @@ __global__ void __launch_bounds__(kWave * NW, NW >= 4 ? 4 : 1) poa_window_kernel
             if (NW > 1)
             {
                 // forward-pass channels and progress words start empty
-                for (int t = tid; t < (kShBytes(NW) - kShProg) / 4; t += kThr)
-                    reinterpret_cast<GWAMD_LDS int*>(shb + kShProg)[t] = 0;
+                constexpr int kP = W ? kShProgW : kShProg;
+                constexpr int kB = W ? kShBytesW(NW) : kShBytes(NW);
+                for (int t = tid; t < (kB - kP) / 4; t += kThr)
+                    reinterpret_cast<GWAMD_LDS int*>(shb + kP)[t] = 0;
             }
             __syncthreads();
             ph.lap<kPhRowProg>();
             cells += int64_t(V + 1) * (L + 1);
             int end_row;
             // (the diagnostic 24- and 32-column shapes keep the round-3 pass)
-            if constexpr (CPL <= 16)
+            if constexpr (W)
+                end_row = nw_forward_lds_w<CPL, NW, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride, codes,
+                                                           d.code_stride, sc, shb, carry, tid);
+            else if constexpr (CPL <= 16)
                 end_row = use_v2 ? nw_forward_lds_v2<CPL, NW, SizeT>(g, P, V, lread, L, ring, rstride, spill, rstride,
                                                                      codes, d.code_stride, sc, shb, carry, tid,
                                                                      d.lds_xl_cap)
@@ -1423,13 +1432,27 @@ extern "C" int gwamd_internal_poa_blocks_per_cu(const gwamd::poa::Dims* d, int s
     using namespace gwamd::poa;
     if (d->lds_kernel == 3 && banded)
         return gwamd_internal_poa_band_blocks_per_cu(d, score_bits, size_bits, msa);
-    if (d->lds_kernel != 1 || banded || score_bits != 16 || size_bits != 16)
+    if (d->lds_kernel != 1 || banded || size_bits != 16 || (score_bits != 16 && score_bits != 32))
         return 0;
     const size_t lb = size_t(d->lds_bytes);
-#define GWAMD_LDS_OCC(CPL, NW)                                                                                 \
-    if (d->lds_cpl == CPL && d->lds_waves == NW)                                                               \
-        return msa ? blocks_per_cu(poa_window_kernel_lds<true, CPL, NW>, kWave * NW, lb)                       \
-                   : blocks_per_cu(poa_window_kernel_lds<false, CPL, NW>, kWave * NW, lb);
+#define GWAMD_LDS_OCC_W(CPL, NW, WD)                                                                          \
+    if (d->lds_cpl == CPL && d->lds_waves == NW && (score_bits == 32) == WD)                                   \
+    {                                                                                                          \
+        auto kt = poa_window_kernel_lds<true, CPL, NW, WD>;                                                    \
+        auto kf = poa_window_kernel_lds<false, CPL, NW, WD>;                                                   \
+        if (lb > 65536 &&                                                                                      \
+            (hipFuncSetAttribute(reinterpret_cast<const void*>(msa ? kt : kf),                                 \
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, int(lb)) != hipSuccess))          \
+            return 0;                                                                                          \
+        return msa ? blocks_per_cu(kt, kWave * NW, lb) : blocks_per_cu(kf, kWave * NW, lb);                    \
+    }
+#define GWAMD_LDS_OCC(CPL, NW) GWAMD_LDS_OCC_W(CPL, NW, false)
+    // 32-bit scores: (columns per lane, waves) planned by poa_batch.cpp
+    GWAMD_LDS_OCC_W(8, 1, true)
+    GWAMD_LDS_OCC_W(8, 2, true)
+    GWAMD_LDS_OCC_W(8, 4, true)
+    GWAMD_LDS_OCC_W(8, 8, true)
+    GWAMD_LDS_OCC_W(16, 8, true)
     GWAMD_LDS_OCC(8, 1)
     GWAMD_LDS_OCC(16, 1)
     GWAMD_LDS_OCC(24, 1)
@@ -1440,6 +1463,7 @@ extern "C" int gwamd_internal_poa_blocks_per_cu(const gwamd::poa::Dims* d, int s
     GWAMD_LDS_OCC(16, 4)
     GWAMD_LDS_OCC(4, 4)
 #undef GWAMD_LDS_OCC
+#undef GWAMD_LDS_OCC_W
     return 0;
 }
 
@@ -1456,20 +1480,35 @@ extern "C" hipError_t gwamd_internal_poa_launch(const gwamd::poa::Buffers* b, co
         grid = dim3(b->num_slots); // persistent grid: one workgroup per scratch slot
     if (d->lds_kernel == 3 && banded)
         return gwamd_internal_poa_band_launch(b, d, sc, score_bits, size_bits, msa, stream);
-    if (d->lds_kernel == 1 && !banded && score_bits == 16 && size_bits == 16)
+    if (d->lds_kernel == 1 && !banded && size_bits == 16 && (score_bits == 16 || score_bits == 32))
     {
         const size_t lb = size_t(d->lds_bytes);
-#define GWAMD_LDS_LAUNCH(CPL, NW)                                                                              \
-    if (d->lds_cpl == CPL && d->lds_waves == NW)                                                               \
+#define GWAMD_LDS_LAUNCH_W(CPL, NW, WD)                                                                        \
+    if (d->lds_cpl == CPL && d->lds_waves == NW && (score_bits == 32) == WD)                                   \
     {                                                                                                          \
         const dim3 blk(kWave * NW);                                                                            \
+        auto kt = poa_window_kernel_lds<true, CPL, NW, WD>;                                                    \
+        auto kf = poa_window_kernel_lds<false, CPL, NW, WD>;                                                   \
+        if (lb > 65536)                                                                                        \
+        {                                                                                                      \
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(msa ? kt : kf),             \
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lb));     \
+            if (e != hipSuccess)                                                                               \
+                return e;                                                                                      \
+        }                                                                                                      \
         if (msa)                                                                                               \
-            hipLaunchKernelGGL((poa_window_kernel_lds<true, CPL, NW>), grid, blk, lb, stream, *b, *d, *sc);    \
+            hipLaunchKernelGGL(kt, grid, blk, lb, stream, *b, *d, *sc);                                        \
         else                                                                                                   \
-            hipLaunchKernelGGL((poa_window_kernel_lds<false, CPL, NW>), grid, blk, lb, stream, *b, *d, *sc);   \
+            hipLaunchKernelGGL(kf, grid, blk, lb, stream, *b, *d, *sc);                                        \
         return hipGetLastError();                                                                              \
     }
+#define GWAMD_LDS_LAUNCH(CPL, NW) GWAMD_LDS_LAUNCH_W(CPL, NW, false)
         // (columns per lane, waves per window) pairs planned by poa_batch.cpp
+        GWAMD_LDS_LAUNCH_W(8, 1, true)
+        GWAMD_LDS_LAUNCH_W(8, 2, true)
+        GWAMD_LDS_LAUNCH_W(8, 4, true)
+        GWAMD_LDS_LAUNCH_W(8, 8, true)
+        GWAMD_LDS_LAUNCH_W(16, 8, true)
         GWAMD_LDS_LAUNCH(8, 1)
         GWAMD_LDS_LAUNCH(16, 1)
         GWAMD_LDS_LAUNCH(24, 1)
@@ -1481,6 +1520,7 @@ extern "C" hipError_t gwamd_internal_poa_launch(const gwamd::poa::Buffers* b, co
         GWAMD_LDS_LAUNCH(4, 4)
         return hipErrorInvalidConfiguration;
 #undef GWAMD_LDS_LAUNCH
+#undef GWAMD_LDS_LAUNCH_W
     }
     const int lds_bytes = (d->max_seq_len > d->band_width + kBandPad ? d->max_seq_len : d->band_width + kBandPad) + 32;
     const size_t lds    = size_t((lds_bytes + 15) & ~15);

@@ -154,16 +154,51 @@ def test_banded_wide_msa_int32(bw, spoa, monkeypatch):
         assert (st[i], msa[i]) == (r.status, r.msa), (bw, spoa, i)
 
 
-def test_full_int32_long_reads():
+@pytest.mark.parametrize("variant", ["lds", "v1"])
+def test_full_int32_long_reads(variant, monkeypatch):
     # full alignment with 32-bit scores (4 kb reads: use32bitScore,
-    # cudapoa_limits.hpp:28-53): the global-memory kernel
+    # cudapoa_limits.hpp:28-53): the LDS kernel's 32-bit pass
+    # (nw_forward_lds_w, 16 columns per lane on 8 waves) and the global-memory
+    # kernel on the same windows
+    if variant == "v1":
+        monkeypatch.setenv("GWAMD_POA_KERNEL", "v1")
+    else:
+        monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
     wins = synth.poa_windows(27, 3, 4000, 6, 150, 150, 150)
     b = run_gpu(wins, 4400, 6, mem=8 << 30)
-    assert b.get_types()[0] == 32 and b.kernel_variant() == 1
+    assert b.get_types()[0] == 32 and b.kernel_variant() == (1 if variant == "v1" else 2)
     cons, cov, st = b.get_consensus()
     for i, w in enumerate(wins):
         r = run_oracle(w, 4400, 6, score_bits=32)
         assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), i
+
+
+# 32-bit scores on the LDS kernel at every (columns per lane, waves) shape the
+# plan uses; windows whose reads are longer than one sweep (NW * 64 * CPL
+# columns), hit span and sweep boundaries, or are empty / one base, plus a
+# 40-read window (many predecessors; rows read from beyond the ring go
+# through the HBM spill rows), consensus and MSA
+@pytest.mark.parametrize("shape", ["8,1", "8,2", "8,4", "8,8", "16,8"])
+@pytest.mark.parametrize("out", ["consensus", "msa"])
+def test_full_int32_lds_shapes(shape, out, monkeypatch):
+    monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    monkeypatch.setenv("GWAMD_DIAG", "1")
+    monkeypatch.setenv("GWAMD_POA_LDS_SHAPE", shape)
+    max_seq = 2200
+    wins = synth.poa_windows(811, 3, 1500, 10, 60, 60, 60)
+    wins += synth.poa_windows(821, 2, 500, 40, 25, 25, 25)
+    wins.append([b"ACGT" * 256, b"ACGT" * 256 + b"A", b"", b"ACGTTGCA" * 64, b"ACGTTGCA" * 64 + b"G",
+                 b"ACGT" * 128, b"C" * 2100, b"ACGTTGCA" * 257])
+    msa = out == "msa"
+    b = run_gpu(wins, max_seq, 40, output_type=out)
+    assert b.get_types()[0] == 32 and b.kernel_variant() == 2
+    got = b.get_msa() if msa else b.get_consensus()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, max_seq, 40, msa=msa, score_bits=32)
+        if msa:
+            assert (got[1][i], got[0][i]) == (r.status, r.msa), (shape, i)
+        else:
+            assert (got[2][i], got[0][i], got[1][i]) == (r.status, r.consensus, r.coverage), (shape, i)
 
 
 def test_msa_parity_synthetic():
@@ -666,3 +701,28 @@ def test_marked_rows_multi_source_fwd2(fwd, monkeypatch):
         assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), (fwd, i)
         multi += sum(1 for ins in r.graph["in"] if not ins) >= 2
     assert multi >= 10
+
+
+@pytest.mark.parametrize("spoa", [False, True])
+def test_full_int32_persistent_grid(spoa, monkeypatch):
+    # the 32-bit LDS kernel on a persistent grid of 3 slots (workgroups reuse
+    # their slot's scratch across windows, heaviest first), two generates,
+    # SPOA_ACCURATE on and off, final graphs against the oracle
+    monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    monkeypatch.setenv("GWAMD_DIAG", "1")
+    monkeypatch.setenv("GWAMD_POA_SLOTS", "3")
+    wins = synth.poa_windows(841, 4, 900, 8, 40, 40, 40)
+    wins += synth.poa_windows(851, 4, 200, 6, 10, 10, 10)
+    b = run_gpu(wins, 1600, 8, spoa_accurate=spoa)
+    slots, _ = b.get_grid()
+    assert b.get_types()[0] == 32 and b.kernel_variant() == 2 and slots < len(wins)
+    for rep in range(2):
+        if rep:
+            b.generate_poa()
+        cons, cov, st = b.get_consensus()
+        graphs, gst = b.get_graphs()
+        for i, w in enumerate(wins):
+            r = run_oracle(w, 1600, 8, score_bits=32, want_graph=True, spoa_accurate=spoa)
+            assert (st[i], cons[i], cov[i]) == (r.status, r.consensus, r.coverage), (rep, i)
+            expect = {(src, v): wt for v, ins in enumerate(r.graph["in"]) for (src, wt) in ins}
+            assert {(u, v): graphs[i].weight(u, v) for (u, v) in graphs[i].edges} == expect, (rep, i)

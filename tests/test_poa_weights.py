@@ -148,6 +148,16 @@ def test_weighted_windows_config_b_shape():
     _check(b, wins, wts, 1100, 32, False, 256, "consensus", "B")
 
 
+def test_weighted_windows_int32_lds():
+    # 32-bit scores (max_sequence_size 1,600 >= 1,490, use32bitScore) on the
+    # LDS kernel's 32-bit pass, weights on every read, consensus and graphs
+    wins = synth.poa_windows(1951, 6, 1200, 12, 60, 60, 60)
+    wts = _weights_for(wins, 9, lo=0, hi=60, none_every=4)
+    b = _run(wins, wts, 1600, 12, False, 256, "consensus")
+    assert b.kernel_variant() == 2 and b.get_types()[0] == 32
+    _check(b, wins, wts, 1600, 12, False, 256, "consensus", "lds32")
+
+
 def test_negative_weights_raise():
     # cudapoa_batch.cuh:524-528: throw_on_negative -> std::invalid_argument
     b = CudaPoaBatch(4, 128, MEM, alignment_band_width=128)
