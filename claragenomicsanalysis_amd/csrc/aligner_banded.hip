@@ -691,9 +691,28 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
         auto refill = [&](int jcol) {
             const int64_t hi = min<int64_t>(total, int64_t(nwb) * (jcol + 1));
             const int64_t lo = max<int64_t>(0, hi - TLE);
+            const int nr     = int(hi - lo);
             wave_sync();
-            for (int64_t e = lane; e < hi - lo; e += kWave)
-                lds_put(reg + e, glb_get(E + (lo + e)));
+            // 8 entries per lane in flight before the first LDS store waits
+            // (a loop of single loads waited one HBM latency per 64 entries)
+            for (int e0 = 0; e0 < nr; e0 += 8 * kWave)
+            {
+                BandEntry v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                {
+                    const int e = e0 + u * kWave + lane;
+                    if (e < nr)
+                        v[u] = glb_get(E + (lo + e));
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                {
+                    const int e = e0 + u * kWave + lane;
+                    if (e < nr)
+                        lds_put(reg + e, v[u]);
+                }
+            }
             wave_sync();
             tb = lo;
             te = hi;
@@ -810,7 +829,7 @@ __global__ void __launch_bounds__(kWave) ukkonen_kernel(Args a)
     GWAMD_LDS uint8_t* base = (GWAMD_LDS uint8_t*)(lds);
     GWAMD_LDS uint8_t* sA   = base + a.lds_target_off; // along i (the shorter sequence)
     GWAMD_LDS uint8_t* sB   = base + a.lds_seq2_off;   // along j
-    const int TE            = (a.tile_bytes / 4) * 2;  // tile elements (int16), even
+    const int TE8           = ((a.tile_bytes / 2) - 8) & ~7; // tile range (int16 elements); + 7 for alignment
     GWAMD_LDS int16_t* tile = (GWAMD_LDS int16_t*)(base + a.lds_tile_off);
     int16_t* S              = reinterpret_cast<int16_t*>(a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes));
     const int p             = a.ukkonen_p;
@@ -926,18 +945,38 @@ __global__ void __launch_bounds__(kWave) ukkonen_kernel(Args a)
         const int64_t total = int64_t(bw) * cols;
         int64_t tb = -1, te = -1;
         auto refill = [&](int lcol) {
-            // flat range ending with column lcol, aligned to dwords
+            // flat range ending with column lcol, in 16-byte pieces (8
+            // elements) from an aligned start, 8 pieces per lane in flight
+            // before the first LDS store waits (a loop of single dword loads
+            // waited one HBM latency per 64 dwords, the bulk of a long pair's
+            // backtrace)
             const int64_t hi = min<int64_t>(total, int64_t(bw) * (lcol + 1));
-            const int64_t lo = max<int64_t>(0, hi - TE) & ~int64_t(1);
-            const int64_t nd = (hi - lo + 1) / 2;
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(S + lo);
-            GWAMD_LDS uint32_t* dst = (GWAMD_LDS uint32_t*)tile;
+            const int64_t lo = max<int64_t>(0, hi - TE8) & ~int64_t(7);
+            const int np16   = int((hi - lo + 7) / 8);
+            const be_u32x4* src = reinterpret_cast<const be_u32x4*>(S + lo);
+            GWAMD_LDS be_u32x4* dst = (GWAMD_LDS be_u32x4*)tile;
             wave_sync();
-            for (int64_t e = lane; e < nd; e += kWave)
-                dst[e] = src[e];
+            for (int e0 = 0; e0 < np16; e0 += 8 * kWave)
+            {
+                be_u32x4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                {
+                    const int e = e0 + u * kWave + lane;
+                    if (e < np16)
+                        v[u] = src[e];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                {
+                    const int e = e0 + u * kWave + lane;
+                    if (e < np16)
+                        dst[e] = v[u];
+                }
+            }
             wave_sync();
             tb = lo;
-            te = min<int64_t>(lo + 2 * nd, total);
+            te = min<int64_t>(lo + 8 * int64_t(np16), total);
         };
         auto val = [&](int i, int j) -> int {
             const int k = (j - i + p) / 2;

@@ -170,6 +170,9 @@ public:
     void set_alignment_type(AlignmentType t) { type_ = t; }
     void set_status(StatusType s) { status_ = s; }
     void set_alignment(std::vector<AlignmentState>&& a) { alignment_ = std::move(a); }
+    // the result storage, refilled in place by sync_alignments (an aligner
+    // that aligns its batch again reuses the vectors' capacity)
+    std::vector<AlignmentState>& alignment_storage() { return alignment_; }
 
     std::string convert_to_cigar() const override
     {
@@ -305,11 +308,34 @@ public:
         h_paths_.reserve(size_t(max_result_) * max_n_ + 16, stream_);
         h_plen_.reserve(size_t(max_n_) * 4, stream_);
         GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
+        // second stream and the events of the pipelined align_all()
+        for (hipStream_t* st : {&stream2_, &s_in_, &s_out_})
+            GWAMD_HIP_CHECK(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+        for (hipEvent_t* e : {&ev_fork_, &ev_join_})
+            GWAMD_HIP_CHECK(hipEventCreate(e));
+        for (int k = 0; k < kMaxStages; k++)
+            for (hipEvent_t* e : {&ev_d_[k], &ev_h_[k], &ev_k_[2 * k], &ev_k_[2 * k + 1]})
+                GWAMD_HIP_CHECK(hipEventCreateWithFlags(e, e == &ev_k_[2 * k] || e == &ev_k_[2 * k + 1]
+                                                               ? hipEventDefault
+                                                               : hipEventDisableTiming));
     }
 
     ~AlignerGlobalHip() override
     {
         (void)hipSetDevice(device_id_);
+        for (hipStream_t st : {stream2_, s_in_, s_out_})
+            if (st)
+            {
+                (void)hipStreamSynchronize(st);
+                (void)hipStreamDestroy(st);
+            }
+        for (hipEvent_t e : {ev_fork_, ev_join_})
+            if (e)
+                (void)hipEventDestroy(e);
+        for (int k = 0; k < kMaxStages; k++)
+            for (hipEvent_t e : {ev_d_[k], ev_h_[k], ev_k_[2 * k], ev_k_[2 * k + 1]})
+                if (e)
+                    (void)hipEventDestroy(e);
         for (void* p : {static_cast<void*>(d_seqs_), static_cast<void*>(d_lens_), static_cast<void*>(d_paths_),
                         static_cast<void*>(d_plen_), static_cast<void*>(d_ws_), static_cast<void*>(d_stats_)})
             if (p)
@@ -351,48 +377,152 @@ public:
         return StatusType::success;
     }
 
+    // aligner_global.cpp:131-159 (H2D, kernel, D2H on the aligner's stream).
+    // Batches of many grids' worth of pairs run as a pipeline of stages: the
+    // pairs are cut into K consecutive chunks; all uploads go back to back on
+    // a copy-in stream, chunk k's kernel runs on half of the workspace slots
+    // (k % 2, one compute stream per half) once its upload is in, and its
+    // download follows on a copy-out stream, so copies overlap the kernels
+    // and sync_alignments fills each chunk's results on the host while later
+    // chunks are still aligning.  Results are the same pair by pair; the
+    // aligner's stream waits for every stage.
     StatusType align_all() override
     {
         if (alignments_.empty())
             return StatusType::success;
-        upload();
-        launch();
-        download();
+        ScopedDevice dev(device_id_);
+        const int32_t n = int32_t(alignments_.size());
+        stages_         = pipeline_stages(n);
+        if (stages_ <= 1)
+        {
+            stages_ = 1;
+            chunk0_[0] = 0, chunk0_[1] = n;
+            upload();
+            GWAMD_HIP_CHECK(hipEventRecord(ev_k_[0], stream_));
+            launch();
+            GWAMD_HIP_CHECK(hipEventRecord(ev_k_[1], stream_));
+            download();
+            GWAMD_HIP_CHECK(hipEventRecord(ev_d_[0], stream_));
+            return StatusType::success;
+        }
+        GWAMD_HIP_CHECK(hipEventRecord(ev_fork_, stream_));
+        for (hipStream_t st : {s_in_, stream2_, s_out_})
+            GWAMD_HIP_CHECK(hipStreamWaitEvent(st, ev_fork_, 0));
+        const int32_t half_slots = slots_ / 2;
+        for (int k = 0; k < stages_; k++)
+        {
+            const int32_t i0 = int32_t(int64_t(n) * k / stages_);
+            const int32_t c  = int32_t(int64_t(n) * (k + 1) / stages_) - i0;
+            chunk0_[k]       = i0;
+            chunk0_[k + 1]   = i0 + c;
+            GWAMD_HIP_CHECK(hipMemcpyAsync(d_lens_ + 2 * size_t(i0), h_lens_.as<int32_t>() + 2 * size_t(i0),
+                                           2 * size_t(c) * 4, hipMemcpyHostToDevice, s_in_));
+            GWAMD_HIP_CHECK(hipMemcpyAsync(d_seqs_ + 2 * size_t(i0) * stride_,
+                                           h_seqs_.as<char>() + 2 * size_t(i0) * stride_, 2 * size_t(c) * stride_,
+                                           hipMemcpyHostToDevice, s_in_));
+            GWAMD_HIP_CHECK(hipEventRecord(ev_h_[k], s_in_));
+        }
+        for (int k = 0; k < stages_; k++)
+        {
+            hipStream_t st   = (k & 1) ? stream2_ : stream_;
+            const int32_t i0 = chunk0_[k], c = chunk0_[k + 1] - chunk0_[k];
+            GWAMD_HIP_CHECK(hipStreamWaitEvent(st, ev_h_[k], 0));
+            GWAMD_HIP_CHECK(hipEventRecord(ev_k_[2 * k], st));
+            launch_range(i0, c, (k & 1) * half_slots, (k & 1) ? slots_ - half_slots : half_slots, st);
+            GWAMD_HIP_CHECK(hipEventRecord(ev_k_[2 * k + 1], st));
+            GWAMD_HIP_CHECK(hipStreamWaitEvent(s_out_, ev_k_[2 * k + 1], 0));
+            GWAMD_HIP_CHECK(hipMemcpyAsync(h_paths_.as<int8_t>() + size_t(i0) * max_result_,
+                                           d_paths_ + size_t(i0) * max_result_, size_t(c) * max_result_,
+                                           hipMemcpyDeviceToHost, s_out_));
+            GWAMD_HIP_CHECK(hipMemcpyAsync(h_plen_.as<int32_t>() + i0, d_plen_ + i0, size_t(c) * 4,
+                                           hipMemcpyDeviceToHost, s_out_));
+            GWAMD_HIP_CHECK(hipEventRecord(ev_d_[k], s_out_));
+        }
+        GWAMD_HIP_CHECK(hipEventRecord(ev_join_, s_out_)); // after every kernel and download
+        GWAMD_HIP_CHECK(hipStreamWaitEvent(stream_, ev_join_, 0));
         return StatusType::success;
+    }
+
+    // Kernel time of the last align_all(): the union of its launches'
+    // intervals (HIP events on their streams), ms.
+    double last_kernel_ms()
+    {
+        ScopedDevice dev(device_id_);
+        if (stages_ == 0)
+            return 0.0;
+        std::vector<std::pair<double, double>> iv;
+        for (int k = 0; k < stages_; k++)
+        {
+            GWAMD_HIP_CHECK(hipEventSynchronize(ev_k_[2 * k + 1]));
+            float a = 0.f, b = 0.f;
+            GWAMD_HIP_CHECK(hipEventElapsedTime(&a, ev_k_[0], ev_k_[2 * k]));
+            GWAMD_HIP_CHECK(hipEventElapsedTime(&b, ev_k_[0], ev_k_[2 * k + 1]));
+            iv.emplace_back(double(a), double(b));
+        }
+        std::sort(iv.begin(), iv.end());
+        double total = 0.0, lo = iv[0].first, hi = iv[0].second;
+        for (size_t k = 1; k < iv.size(); k++)
+        {
+            if (iv[k].first > hi)
+            {
+                total += hi - lo;
+                lo = iv[k].first;
+            }
+            hi = std::max(hi, iv[k].second);
+        }
+        return total + (hi - lo);
     }
 
     StatusType sync_alignments() override
     {
         // aligner_global.cpp:161-189: paths come out end -> start
         ScopedDevice dev(device_id_);
-        GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
         const int32_t n = int32_t(alignments_.size());
         auto fill       = [&](int32_t i0, int32_t i1) {
             for (int32_t i = i0; i < i1; i++)
             {
                 const int32_t len = h_plen_.as<int32_t>()[i];
                 const int8_t* p   = h_paths_.as<int8_t>() + size_t(i) * max_result_;
-                std::vector<AlignmentState> st(size_t(std::max(len, 0)));
+                auto* a           = static_cast<AlignmentImpl*>(alignments_[size_t(i)].get());
+                std::vector<AlignmentState>& st = a->alignment_storage();
+                st.resize(size_t(std::max(len, 0)));
                 for (int32_t k = 0; k < len; k++)
                     st[size_t(len - 1 - k)] = static_cast<AlignmentState>(p[k]);
-                auto* a = static_cast<AlignmentImpl*>(alignments_[size_t(i)].get());
-                a->set_alignment(std::move(st));
                 a->set_status(StatusType::success);
             }
         };
         // the alignments are independent: large batches are filled by a few
         // host threads (each alignment object is touched by one thread)
-        const int32_t nth = n < 4096 ? 1 : int32_t(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
-        if (nth <= 1)
-            fill(0, n);
-        else
-        {
+        auto fill_range = [&](int32_t b0, int32_t b1) {
+            const int32_t m   = b1 - b0;
+            const int32_t nth = m < 4096 ? 1 : int32_t(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+            if (nth <= 1)
+            {
+                fill(b0, b1);
+                return;
+            }
             std::vector<std::thread> th;
-            const int32_t per = (n + nth - 1) / nth;
+            const int32_t per = (m + nth - 1) / nth;
             for (int32_t t = 0; t < nth; t++)
-                th.emplace_back(fill, std::min(n, t * per), std::min(n, (t + 1) * per));
+                th.emplace_back(fill, b0 + std::min(m, t * per), b0 + std::min(m, (t + 1) * per));
             for (auto& t : th)
                 t.join();
+        };
+        if (stages_ > 1 && chunk0_[stages_] == n)
+        {
+            // each stage's paths reach the host while later stages are still
+            // aligning: fill them as they arrive
+            for (int k = 0; k < stages_; k++)
+            {
+                GWAMD_HIP_CHECK(hipEventSynchronize(ev_d_[k]));
+                fill_range(chunk0_[k], chunk0_[k + 1]);
+            }
+            GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
+        }
+        else
+        {
+            GWAMD_HIP_CHECK(hipStreamSynchronize(stream_));
+            fill_range(0, n);
         }
         return StatusType::success;
     }
@@ -415,8 +545,19 @@ public:
     }
     void launch()
     {
+        launch_range(0, int32_t(alignments_.size()), 0, slots_, stream_);
+    }
+    // Pairs [i0, i0 + count) on workspace slots [slot0, slot0 + nslots).
+    void launch_range(int32_t i0, int32_t count, int32_t slot0, int32_t nslots, hipStream_t s)
+    {
         ScopedDevice dev(device_id_);
         gwamd::aln::Args a = args();
+        a.seqs     = d_seqs_ + 2 * size_t(i0) * stride_;
+        a.lens     = d_lens_ + 2 * size_t(i0);
+        a.paths    = d_paths_ + size_t(i0) * max_result_;
+        a.path_len = d_plen_ + i0;
+        a.n        = count;
+        a.ws       = d_ws_ + size_t(slot0) * size_t(slot_bytes_);
         if (algo_ == GWAMD_ALIGNER_UKKONEN)
         {
             // the widest band of this batch decides the Ukkonen kernel (plan_banded)
@@ -429,11 +570,30 @@ public:
                 a.tile_bytes   = gwamd::aln::kUkTileRows * gwamd::aln::kUkTileCols * 2;
             }
         }
-        const int grid     = std::min<int>(int(alignments_.size()), slots_);
+        const int grid     = std::min<int>(count, nslots);
         if (algo_ == GWAMD_ALIGNER_MYERS_BANDED || algo_ == GWAMD_ALIGNER_UKKONEN)
-            GWAMD_HIP_CHECK(gwamd_internal_banded_launch(&a, algo_, grid, stream_));
+            GWAMD_HIP_CHECK(gwamd_internal_banded_launch(&a, algo_, grid, s));
         else
-            GWAMD_HIP_CHECK(gwamd_internal_align_launch(&a, algo_, grid, stream_));
+            GWAMD_HIP_CHECK(gwamd_internal_align_launch(&a, algo_, grid, s));
+    }
+    // pipeline stages of align_all(): as many (up to kMaxStages) as keep
+    // each stage's half of the slots busy four times over; 1 = one stage
+    // (GWAMD_ALIGNER_PIPELINE=k forces k stages, 1..kMaxStages, diagnostic)
+    int pipeline_stages(int32_t n) const
+    {
+        if (const char* e = gwamd::host::diag_env("GWAMD_ALIGNER_PIPELINE"))
+        {
+            const int k = std::atoi(e);
+            if (k < 0 || k > kMaxStages)
+                throw std::invalid_argument("GWAMD_ALIGNER_PIPELINE must be 0..8 stages");
+            return slots_ < 2 ? 1 : std::max(1, std::min(k, n));
+        }
+        if (slots_ < 2)
+            return 1;
+        const int64_t per = int64_t(4) * (slots_ / 2); // pairs per stage
+        // (config D, 100k pairs on 3,328 slots: 1 / 2 / 4 / 8 stages measured
+        // 365 / 348 / 320 / 309 ms per step, gpurun_out/r5g)
+        return int(std::max<int64_t>(1, std::min<int64_t>(kMaxStages, n / per)));
     }
     void download()
     {
@@ -743,6 +903,18 @@ private:
     int32_t lds_seq2_off_ = 0, lds_tile_off_ = 0, tile_bytes_ = 0, band_waves_ = 1;
     int32_t lds_edge_off_ = 0, uk_narrow_tile_off_ = 0, uk_narrow_lds_ = 0, uk_wide_lds_ = 0;
     int32_t max_diff_ = 0; // largest |query - target| of the batch
+    // pipelined align_all(): the second compute stream, the copy-in and
+    // copy-out streams, fork / join events, per stage the upload-done and
+    // download-done events and the kernel's start / stop events; stages_ of
+    // the last align_all() (0: none yet) and their first pairs
+    static constexpr int kMaxStages = 8;
+    hipStream_t stream2_ = nullptr, s_in_ = nullptr, s_out_ = nullptr;
+    hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+    hipEvent_t ev_d_[kMaxStages]     = {};
+    hipEvent_t ev_h_[kMaxStages]     = {};
+    hipEvent_t ev_k_[2 * kMaxStages] = {};
+    int stages_                      = 0;
+    int32_t chunk0_[kMaxStages + 1]  = {};
     int32_t slots_ = 1;
     int64_t slot_bytes_ = 0, device_bytes_ = 0;
     char* d_seqs_     = nullptr;
@@ -1011,6 +1183,19 @@ int32_t gwamd_aligner_get_config(const gwamd_aligner* a, int32_t* grid, int64_t*
     *grid         = a->impl->grid();
     *device_bytes = a->impl->device_bytes();
     return 0;
+}
+
+int32_t gwamd_aligner_last_kernel_ms(gwamd_aligner* a, double* ms)
+{
+    if (!a || !ms)
+    {
+        gwamd::host::last_error() = "gwamd_aligner_last_kernel_ms: null argument";
+        return GWAMD_E_INVALID_ARGUMENT;
+    }
+    return guarded_aln([&] {
+        *ms = a->impl->last_kernel_ms();
+        return int32_t(0);
+    });
 }
 
 int32_t gwamd_aligner_get_stats(gwamd_aligner* a, int64_t* hbm_state_sweeps, int64_t* ukkonen_wide_pairs,

@@ -50,6 +50,8 @@ def _declare(L):
     L.gwamd_aligner_max_lengths.argtypes = [i32, P(i32), P(i32)]
     L.gwamd_aligner_pair_fits.restype = i32
     L.gwamd_aligner_pair_fits.argtypes = [i32, i32, i32]
+    L.gwamd_aligner_last_kernel_ms.restype = i32
+    L.gwamd_aligner_last_kernel_ms.argtypes = [vp, P(C.c_double)]
     L.gwamd_aligner_get_stats.restype = i32
     L.gwamd_aligner_get_stats.argtypes = [vp, P(i64), P(i64), P(i64)]
     del i8
@@ -226,6 +228,13 @@ class CudaAlignerBatch:
         paths = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int8)), shape=(max(n, 1) * stride.value,))
         lens = np.ctypeslib.as_array(C.cast(ln, C.POINTER(C.c_int32)), shape=(max(n, 1),))
         return paths[:n * stride.value].reshape(n, stride.value).copy(), lens[:n].copy()
+
+    def last_kernel_ms(self):
+        """Kernel time of the last align_all() (ms, union of its launches;
+        gwamd_aligner_last_kernel_ms)."""
+        v = C.c_double()
+        _check(self._lib.gwamd_aligner_last_kernel_ms(self._handle, C.byref(v)))
+        return v.value
 
     def stats(self):
         """Path counters accumulated over this aligner's launches

@@ -24,6 +24,7 @@
  *   gwamd_aligner_max_lengths     (none: this implementation's length limits)
  *   gwamd_aligner_pair_fits       (none: whether a (query, target) limit pair is accepted)
  *   gwamd_aligner_get_stats       (none: path counters for the parity tests)
+ *   gwamd_aligner_last_kernel_ms  (none: kernel time of the last align_all, bench.py)
  *
  * Extra entry points (bench.py): split align_all into upload / launch /
  * download and read the raw device paths.
@@ -124,6 +125,12 @@ int32_t gwamd_aligner_max_lengths(int32_t algorithm, int32_t* max_query, int32_t
  * Q * T <= 9e10) nor for Ukkonen (band rows).  1 fits, 0 does not, or
  * GWAMD_E_INVALID_ARGUMENT. */
 int32_t gwamd_aligner_pair_fits(int32_t algorithm, int32_t max_query_length, int32_t max_target_length);
+
+/* Kernel time of the last gwamd_aligner_align_all (ms; waits for it): the
+ * union of its launches' intervals, measured with HIP events on the streams
+ * they ran on (large batches run as two pipelined halves on two streams).
+ * NULL arguments: GWAMD_E_INVALID_ARGUMENT. */
+int32_t gwamd_aligner_last_kernel_ms(gwamd_aligner* aligner, double* ms);
 
 /* Path counters of this aligner, accumulated over its launches:
  * *hbm_state_sweeps = banded Myers band sweeps whose 32-word chunk state went

@@ -240,3 +240,32 @@ def test_caching_budget_caps_the_workspace():
         assert a.cigar == oracle.cigar(oracle.align(q, t, oracle.ALIGN_HM, 5000))
     with pytest.raises(RuntimeError):
         CudaAlignerBatch(5000, 5000, 64, max_device_memory_allocator_caching_size=1 << 20)
+
+
+@pytest.mark.parametrize("algo", ["hirschberg_myers", "myers", "myers_banded", "ukkonen"])
+def test_pipelined_align_all_matches_oracle(algo, monkeypatch):
+    # align_all() on a batch of many grids' worth of pairs runs as a pipeline
+    # of chunks (copy-in / copy-out streams, two compute streams with half the
+    # workspace slots each; GWAMD_ALIGNER_GRID=1: one workgroup per CU, so
+    # 1,500 pairs are enough); with 3 and 8 stages (uneven chunks, stages
+    # sharing a slot half) every pair equals the oracle and the one-stage run
+    # (GWAMD_ALIGNER_PIPELINE=1), and the kernel time is reported
+    monkeypatch.setenv("GWAMD_DIAG", "1")
+    monkeypatch.setenv("GWAMD_ALIGNER_GRID", "1")
+    qs, ts = synth.pairs(77, 1500, 300, 330, 10, 10, 10)
+    pairs = list(zip(qs, ts))
+    res = {}
+    for mode in ("1", "3", "8"):
+        monkeypatch.setenv("GWAMD_ALIGNER_PIPELINE", mode)
+        b = CudaAlignerBatch(max(len(q) for q in qs), max(len(t) for t in ts), len(pairs), algorithm=algo)
+        for q, t in pairs:
+            assert b.add_alignment(q, t) == 0
+        grid, _ = b.config()
+        assert len(pairs) >= 4 * grid
+        b.align_all()
+        b.sync_alignments()
+        assert b.last_kernel_ms() > 0
+        res[mode] = [states(a) for a in b.get_alignments()]
+    assert res["3"] == res["1"] and res["8"] == res["1"]
+    want, _ = oracle.align_batch(pairs, dict(ALGOS)[algo], max(len(q) for q in qs))
+    assert res["1"] == want
