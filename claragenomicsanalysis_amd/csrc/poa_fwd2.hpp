@@ -119,7 +119,10 @@ __device__ __forceinline__ void fwd2_rows(WinGraph<SizeT> g, const RowProg& P, i
     const uint32_t gap2 = pk_bcast(gap);
     const uint32_t one2 = opaque_u32(0x00010001u);
     const uint32_t two2 = opaque_u32(0x00020002u);
-    const int mask      = P.ring_mask;
+    // wave-uniform (an SGPR): P arrives through a flat pointer, and a value
+    // first used inside the row loop made the compiler wait for vmcnt(0) --
+    // every outstanding code / spill store -- at the top of every row
+    const int mask      = uniform(P.ring_mask);
     GWAMD_LDS int16_t* bnd               = (GWAMD_LDS int16_t*)(shb + kShBnd) + wave * (mask + 1);
     GWAMD_LDS uint32_t* chan             = (GWAMD_LDS uint32_t*)(shb + kShChan);
     volatile GWAMD_LDS uint32_t* chan_in  = chan + (wave - 1) * kChanRows; // wave > 0
@@ -216,7 +219,9 @@ __device__ __forceinline__ void fwd2_rows(WinGraph<SizeT> g, const RowProg& P, i
                     if (((r - 1) & (kWave - 1)) == 0)
                     {
                         const int x = r + lane;
-                        hbm_c       = x <= V ? int(carry_hbm[x]) : 0;
+                        uint32_t hc = x <= V ? uint32_t(int(carry_hbm[x])) : 0u;
+                        settle_vm1(hc); // wait here, once per 64 rows, not at every row's readlane
+                        hbm_c = int(hc);
                     }
                     cin = int(int16_t(__builtin_amdgcn_readlane(hbm_c, (r - 1) & (kWave - 1))));
                 }
@@ -458,8 +463,22 @@ __device__ __forceinline__ void fwd2_rows(WinGraph<SizeT> g, const RowProg& P, i
                 rows_general(std::false_type{}, pv_c, np); // np >= 2, every predecessor in the ring
             else
             {
-                int n        = np;
-                const int pv = row_preds<SizeT>(P, g, r, rec, lane, n); // sources: n = 1, row 0
+                // predecessor rows (sources: n = 1, row 0); lists through the
+                // typed LDS pointer (P's own is flat: its loads count in
+                // vmcnt, so a wait for them also waits for every code store)
+                int n  = np;
+                int pv = 0;
+                if (np == int(kRecEscape))
+                    pv = row_preds<SizeT>(P, g, r, rec, lane, n);
+                else
+                {
+                    if (np >= 2)
+                        pv = lane < np ? int(pxl[(rec >> 16) + lane]) : 0;
+                    else if (np == 1)
+                        pv = r - int(rec >> 16);
+                    if (np == 0)
+                        n = 1;
+                }
                 const uint32_t ub = rec & 0x7fu;
                 if (!((ub & 0xc0u) == 0x40u && ((0x10008aull >> (ub & 0x3fu)) & 1u)))
                 {

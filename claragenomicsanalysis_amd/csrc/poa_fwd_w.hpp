@@ -83,7 +83,10 @@ __device__ int nw_forward_lds_w(WinGraph<SizeT> g, const RowProg& P, int V, cons
     const int gap       = sc.gap;
     const int s_eq      = sc.match - gap;
     const int s_ne      = sc.mismatch - gap;
-    const int mask      = P.ring_mask;
+    // wave-uniform (an SGPR): P arrives through a flat pointer, and a value
+    // first used inside the row loop made the compiler wait for vmcnt(0) --
+    // every outstanding code / spill store -- at the top of every row
+    const int mask      = uniform(P.ring_mask);
     volatile GWAMD_LDS int* prog_v = (volatile GWAMD_LDS int*)(shb + kShProgW);
     GWAMD_LDS int32_t* bnd         = (GWAMD_LDS int32_t*)(shb + kShBndW) + wave * kMaxRingW;
     GWAMD_LDS uint64_t* chan       = (GWAMD_LDS uint64_t*)(shb + kShChanW);
@@ -262,7 +265,9 @@ __device__ int nw_forward_lds_w(WinGraph<SizeT> g, const RowProg& P, int V, cons
                     if (((r - 1) & (kWave - 1)) == 0)
                     {
                         const int x = r + lane;
-                        hbm_c       = x <= V ? carry_hbm[x] : 0;
+                        uint32_t hc = x <= V ? uint32_t(carry_hbm[x]) : 0u;
+                        settle_vm1(hc); // wait here, once per 64 rows, not at every row's readlane
+                        hbm_c = int(hc);
                     }
                     cin = __builtin_amdgcn_readlane(hbm_c, (r - 1) & (kWave - 1));
                 }

@@ -547,7 +547,10 @@ __device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, con
     const uint32_t gap2 = pk_bcast(gap);
     const uint32_t one2 = opaque_u32(0x00010001u);
     const uint32_t two2 = opaque_u32(0x00020002u);
-    const int mask      = P.ring_mask;
+    // wave-uniform (an SGPR): P arrives through a flat pointer, and a value
+    // first used inside the row loop made the compiler wait for vmcnt(0) --
+    // every outstanding code / spill store -- at the top of every row
+    const int mask      = uniform(P.ring_mask);
     GWAMD_LDS int* prog          = (GWAMD_LDS int*)(shb + kShProg);
     GWAMD_LDS int16_t* bnd       = (GWAMD_LDS int16_t*)(shb + kShBnd) + wave * (mask + 1);
     GWAMD_LDS uint32_t* chan     = (GWAMD_LDS uint32_t*)(shb + kShChan);
@@ -790,7 +793,9 @@ __device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, con
                     if (((r - 1) & (kWave - 1)) == 0)
                     {
                         const int x = r + lane;
-                        hbm_c       = x <= V ? int(carry_hbm[x]) : 0;
+                        uint32_t hc = x <= V ? uint32_t(int(carry_hbm[x])) : 0u;
+                        settle_vm1(hc); // wait here, once per 64 rows, not at every row's readlane
+                        hbm_c = int(hc);
                     }
                     cin = int(int16_t(__builtin_amdgcn_readlane(hbm_c, (r - 1) & (kWave - 1))));
                 }
