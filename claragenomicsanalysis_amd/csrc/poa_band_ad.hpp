@@ -228,12 +228,7 @@ __device__ __forceinline__ int ad_block(const AdCtx<ScoreT>& C, WinGraph<SizeT> 
 #pragma unroll
     for (int s = 0; s < NS; s++)
         lv[s] = int(sp[s][0]);
-#ifdef GWAMD_AD_PREFETCH2 // timing experiment only (distance-2 rows may read stale values)
-    int lw[NS];
-#pragma unroll
-    for (int s = 0; s < NS; s++)
-        lw[s] = int(sp[s][1]);
-#endif
+    uint32_t rbn = rp[0]; // read byte of the next step
     int cur      = minv; // emission of the previous step (column c-1)
     int sv       = minv; // emission at column L
     // fast step state: max_s F_s(c-1) and its first slot as a diagonal code
@@ -254,11 +249,6 @@ __device__ __forceinline__ int ad_block(const AdCtx<ScoreT>& C, WinGraph<SizeT> 
                 ad_wait(sh, blk - 1, uint32_t(t0 + kAdSync - 1 + delta));
             ad_publish(sh, blk, uint32_t(t0), lane);
         }
-        // the group's read bytes (a constant buffer) in one go
-        uint32_t rbg[kAdSync];
-#pragma unroll
-        for (int u = 0; u < kAdSync; u++)
-            rbg[u] = rp[t0 + u];
 #pragma unroll
         for (int u = 0; u < kAdSync; u++)
         {
@@ -268,20 +258,15 @@ __device__ __forceinline__ int ad_block(const AdCtx<ScoreT>& C, WinGraph<SizeT> 
 #pragma unroll
         for (int s = 0; s < NS; s++)
             cv[s] = lv[s];
-        const uint32_t rb = rbg[u];
-        // next step's LDS values (written at least one step ago, see header)
-#ifdef GWAMD_AD_PREFETCH2
-#pragma unroll
-        for (int s = 0; s < NS; s++)
-        {
-            lv[s] = lw[s];
-            lw[s] = int(sp[s][t + 2]);
-        }
-#else
+        const uint32_t rb = rbn;
+        // next step's LDS values (ring values written at least one step ago,
+        // see header; the read byte) issued first, so their latency overlaps
+        // this step's arithmetic instead of stalling the next step
 #pragma unroll
         for (int s = 0; s < NS; s++)
             lv[s] = int(sp[s][t + 1]);
-#endif
+        rbn = rp[t + 1];
+        ad_compiler_fence();
         const int dv  = ad_dpp_shr1(cur);
         const int sig = (int(rb) == base) ? vmatch : vmism;
         const int hl  = wadd(cur, gap);
@@ -364,9 +349,7 @@ __device__ __forceinline__ int ad_block(const AdCtx<ScoreT>& C, WinGraph<SizeT> 
         else
             e = cell ? H : minv; // idx 0 is minv: every row of a fast block has band start > 0
         *(row ? wp + t : dw) = ScoreT(e);
-#ifndef GWAMD_AD_NO_CODE_STORE // timing experiment only (wrong results): the pass without its code stores
         codes[cell ? uint32_t(coff + t) : uint32_t(lane)] = uint8_t(code);
-#endif
         if (any_store)
             *reinterpret_cast<ScoreT*>(spillb + (row && store ? soff + uint32_t(sizeof(ScoreT) * t)
                                                                : uint32_t(sizeof(ScoreT) * lane))) = ScoreT(e);
