@@ -820,6 +820,121 @@ __device__ __forceinline__ int dpp_from_upper(int v) // lane i <- lane i+1 (wave
     return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false);
 }
 
+// One column of the anti-diagonal sweep for NCK live 64-row chunks; PAR is
+// the column's parity class (0: (l - p) even, 1: odd). Lane k of chunk c is
+// band row k = c * 64 + lane; its cell is (i, j) = (h - k, k + l - h) with
+// h = (p + l) / 2 (ukkonen_gpu.cu:96-133).
+template <int NCK, int PAR>
+__device__ __forceinline__ void uk_column(const GWAMD_LDS uint8_t* sA, const GWAMD_LDS uint8_t* sB,
+                                          int16_t* Sl, int l, int p, int bw, int lane,
+                                          const int (&lo_lim)[2][NCK], const int (&hi_lim)[2][NCK],
+                                          int (&V1)[NCK], int (&V2)[NCK])
+{
+    constexpr int M = kUkMax;
+    const int h     = (p + l) >> 1;
+    int V0[NCK];
+#pragma unroll
+    for (int c = 0; c < NCK; c++)
+    {
+        const int k = c * kWave + lane;
+        const int i = h - k;
+        const int j = l - i;
+        // lo_lim = lmin + 1 (or INT_MAX for rows past kmax / bw), hi_lim = lmax
+        const bool cmp = l >= lo_lim[PAR][c] && l < hi_lim[PAR][c];
+        int lo         = dpp_from_lower(V1[c]);
+        int hi         = dpp_from_upper(V1[c]);
+        if (c > 0)
+        {
+            const int x = __builtin_amdgcn_readlane(V1[c > 0 ? c - 1 : 0], kWave - 1);
+            if (lane == 0)
+                lo = x;
+        }
+        if (c + 1 < NCK)
+        {
+            const int x = __builtin_amdgcn_readlane(V1[c + 1 < NCK ? c + 1 : c], 0);
+            if (lane == kWave - 1)
+                hi = x;
+        }
+        const int ii  = cmp ? i - 1 : 0;
+        const int jj  = cmp ? j - 1 : 0;
+        const int ca  = sA[ii];
+        const int cb  = sB[jj];
+        const int dgv = l < 2 ? M : V2[c] + (ca == cb ? 0 : 1);
+        int left, above;
+        if (PAR == 0)
+        {
+            left  = k - 1 < 0 ? M : lo + 1;
+            above = V1[c] + 1;
+        }
+        else
+        {
+            left  = V1[c] + 1;
+            above = k + 1 >= bw ? M : hi + 1;
+        }
+        const int init = i == 0 ? j : (j == 0 ? i : M);
+        const int v    = cmp ? min(dgv, min(left, above)) : init;
+        V0[c]          = int(int16_t(v));
+        if (c + 1 < NCK || k < bw)
+            Sl[k] = int16_t(v);
+    }
+#pragma unroll
+    for (int c = 0; c < NCK; c++)
+    {
+        V2[c] = V1[c];
+        V1[c] = V0[c];
+    }
+}
+
+// The whole sweep (ukkonen_init_score_matrix + compute_score_matrix_{even,odd})
+// specialised on the number of live chunks: the per-row diagonal limits of
+// both parities are computed once, and columns run in (even, odd) pairs so
+// the parity is a compile-time constant in each body.
+template <int NCK>
+__device__ void uk_sweep(const GWAMD_LDS uint8_t* sA, const GWAMD_LDS uint8_t* sB, int16_t* S, int m, int n,
+                         int p, int bw, int lane)
+{
+    constexpr int M     = kUkMax;
+    const int cols      = n + m;
+    const int kmax_odd  = (n - m + 2 * p - 1) / 2 + 1;
+    const int kmax_even = (n - m + 2 * p) / 2 + 1;
+    int lo_lim[2][NCK], hi_lim[2][NCK];
+#pragma unroll
+    for (int c = 0; c < NCK; c++)
+    {
+        const int k = c * kWave + lane;
+#pragma unroll
+        for (int par = 0; par < 2; par++)
+        {
+            const int d    = par ? 2 * k + 1 : 2 * k; // diagonal + p
+            const int lmin = d >= p ? d - p : p - d;
+            const int lmax = d <= p ? 2 * (m - p + d) + lmin : 2 * min(m, n - d + p) + lmin;
+            const bool ok  = k < (par ? kmax_odd : kmax_even) && k < bw;
+            lo_lim[par][c] = ok ? lmin + 1 : 0x7fffffff;
+            hi_lim[par][c] = lmax;
+        }
+    }
+    int V1[NCK], V2[NCK];
+#pragma unroll
+    for (int c = 0; c < NCK; c++)
+    {
+        V1[c] = M;
+        V2[c] = M;
+    }
+    int l = 0;
+    if (cols > 0 && ((l - p) & 1) != 0)
+    {
+        uk_column<NCK, 1>(sA, sB, S, l, p, bw, lane, lo_lim, hi_lim, V1, V2);
+        l++;
+    }
+    for (; l + 1 < cols; l += 2)
+    {
+        uk_column<NCK, 0>(sA, sB, S + size_t(bw) * l, l, p, bw, lane, lo_lim, hi_lim, V1, V2);
+        uk_column<NCK, 1>(sA, sB, S + size_t(bw) * (l + 1), l + 1, p, bw, lane, lo_lim, hi_lim, V1, V2);
+    }
+    if (l < cols)
+        uk_column<NCK, 0>(sA, sB, S + size_t(bw) * l, l, p, bw, lane, lo_lim, hi_lim, V1, V2);
+}
+
 } // namespace
 
 __global__ void __launch_bounds__(kWave) ukkonen_kernel(Args a)
@@ -858,80 +973,22 @@ __global__ void __launch_bounds__(kWave) ukkonen_kernel(Args a)
         for (int k = lane; k < n - 1; k += kWave)
             sB[k] = uint8_t(B[k]);
         wave_sync();
-        const int bw        = (1 + n - m + 2 * p + 1) / 2;
-        const int cols      = n + m;
-        const int kmax_odd  = (n - m + 2 * p - 1) / 2 + 1;
-        const int kmax_even = (n - m + 2 * p) / 2 + 1;
-        const int nck       = uni((bw + kWave - 1) / kWave);
+        const int bw   = (1 + n - m + 2 * p + 1) / 2;
+        const int cols = n + m;
+        const int nck  = uni((bw + kWave - 1) / kWave);
 
         // anti-diagonal sweep (ukkonen_init_score_matrix + compute_score_matrix_{even,odd})
-        int V1[kUkChunks], V2[kUkChunks], V0[kUkChunks];
-#pragma unroll
-        for (int c = 0; c < kUkChunks; c++)
+        static_assert(kUkChunks == 8, "uk_sweep dispatch covers 1..8 chunks");
+        switch (nck)
         {
-            V1[c] = M;
-            V2[c] = M;
-        }
-        for (int l = 0; l < cols; l++)
-        {
-            const bool even = ((l - p) & 1) == 0;
-            const int kmax  = even ? kmax_even : kmax_odd;
-#pragma unroll
-            for (int c = 0; c < kUkChunks; c++)
-            {
-                if (c < nck)
-                {
-                    const int k    = c * kWave + lane;
-                    const int j    = k - (p + l) / 2 + l;
-                    const int i    = l - j;
-                    const int d    = even ? 2 * k : 2 * k + 1; // diagonal + p
-                    const int lmin = d >= p ? d - p : p - d;
-                    const int lmax = d <= p ? 2 * (m - p + d) + lmin : 2 * min(m, n - d + p) + lmin;
-                    const bool cmp = k < kmax && k < bw && l >= lmin + 1 && l < lmax;
-                    // k - 1 and k + 1 of column l - 1
-                    int lo = dpp_from_lower(V1[c]);
-                    int hi = dpp_from_upper(V1[c]);
-                    if (c > 0)
-                    {
-                        const int x = __builtin_amdgcn_readlane(V1[c > 0 ? c - 1 : 0], kWave - 1);
-                        if (lane == 0)
-                            lo = x;
-                    }
-                    if (c + 1 < kUkChunks && c + 1 < nck)
-                    {
-                        const int x = __builtin_amdgcn_readlane(V1[c + 1 < kUkChunks ? c + 1 : c], 0);
-                        if (lane == kWave - 1)
-                            hi = x;
-                    }
-                    const int ii  = cmp ? i - 1 : 0;
-                    const int jj  = cmp ? j - 1 : 0;
-                    const int ca  = sA[ii];
-                    const int cb  = sB[jj];
-                    const int dgv = l < 2 ? M : V2[c] + (ca == cb ? 0 : 1);
-                    int left, above;
-                    if (even)
-                    {
-                        left  = k - 1 < 0 ? M : lo + 1;
-                        above = V1[c] + 1;
-                    }
-                    else
-                    {
-                        left  = V1[c] + 1;
-                        above = k + 1 >= bw ? M : hi + 1;
-                    }
-                    const int init = i == 0 ? j : (j == 0 ? i : M);
-                    const int v    = cmp ? min(dgv, min(left, above)) : init;
-                    V0[c]          = int(int16_t(v));
-                    if (k < bw)
-                        S[size_t(k) + size_t(bw) * l] = int16_t(v);
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < kUkChunks; c++)
-            {
-                V2[c] = V1[c];
-                V1[c] = V0[c];
-            }
+        case 1: uk_sweep<1>(sA, sB, S, m, n, p, bw, lane); break;
+        case 2: uk_sweep<2>(sA, sB, S, m, n, p, bw, lane); break;
+        case 3: uk_sweep<3>(sA, sB, S, m, n, p, bw, lane); break;
+        case 4: uk_sweep<4>(sA, sB, S, m, n, p, bw, lane); break;
+        case 5: uk_sweep<5>(sA, sB, S, m, n, p, bw, lane); break;
+        case 6: uk_sweep<6>(sA, sB, S, m, n, p, bw, lane); break;
+        case 7: uk_sweep<7>(sA, sB, S, m, n, p, bw, lane); break;
+        default: uk_sweep<8>(sA, sB, S, m, n, p, bw, lane); break;
         }
         __threadfence_block();
         wave_sync();

@@ -1019,10 +1019,14 @@ __device__ __forceinline__ bool topsort_racon_lds_impl(WinGraph<SizeT> g, int n,
                 }
                 else
                 {
-                    ic = uniform(int(g.in_cnt[id]));
-                    ac = (m & 4) ? uniform(int(g.aln_cnt[id])) : 0;
-                    bl = lane < ic ? int(g.in_e[id * kMaxEdges + lane]) : 0;
-                    al = lane < ac ? int(g.aln[id * kMaxAlignments + lane]) : 0;
+                    // the lists are read in full (every slot of the node's
+                    // rows is in bounds) in the same round trip as the counts
+                    const int blr = lane < kMaxEdges ? int(g.in_e[id * kMaxEdges + lane]) : 0;
+                    const int alr = lane < kMaxAlignments ? int(g.aln[id * kMaxAlignments + lane]) : 0;
+                    ic            = uniform(int(g.in_cnt[id]));
+                    ac            = (m & 4) ? uniform(int(g.aln_cnt[id])) : 0;
+                    bl            = lane < ic ? blr : 0;
+                    al            = lane < ac ? alr : 0;
                 }
                 const int mb      = lane < ic ? int(marks[bl]) : 2;
                 const int ma      = lane < ac ? int(marks[al]) : 2;
