@@ -271,12 +271,21 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
     GWAMD_LDS uint32_t* patL = (GWAMD_LDS uint32_t*)(base + a.lds_pat_off);
     GWAMD_LDS BandEntry* reg = (GWAMD_LDS BandEntry*)(base + a.lds_tile_off); // chunk state / tile
     const int TLE            = a.tile_bytes / int(sizeof(BandEntry));
-    // global-typed: flat stores would hold every LDS wait of the sweep behind them
-    GWAMD_GLB BandEntry* E   = (GWAMD_GLB BandEntry*)(a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes));
     const int pw_stride      = a.pat_words;
+    // band doubling run ahead (Args::spec_phase): launch 1 takes (pair,
+    // sweep) items, launch 2 one pair per workgroup (slot = pair)
+    const int K              = a.spec_sweeps;
+    const int n_items        = a.spec_phase == 1 ? a.n * K : a.n;
 
-    for (int idx = blockIdx.x; idx < a.n; idx += gridDim.x)
+    for (int item = blockIdx.x; item < n_items; item += gridDim.x)
     {
+        const int idx = a.spec_phase == 1 ? item / K : item;
+        const int ks  = a.spec_phase == 1 ? item - idx * K : 0; // launch 1: this item's sweep
+        // global-typed: flat stores would hold every LDS wait of the sweep behind them
+        GWAMD_GLB BandEntry* E =
+            (GWAMD_GLB BandEntry*)(a.ws + size_t(a.spec_phase == 1 ? idx : int(blockIdx.x)) * size_t(a.ws_slot_bytes));
+        // launch 1 stores the band matrix of its last sweep only
+        const bool st_on = a.spec_phase != 1 || ks == K - 1;
         const char* q  = a.seqs + size_t(2 * idx) * a.stride;
         const char* tg = a.seqs + size_t(2 * idx + 1) * a.stride;
         const int Q    = uni(a.lens[2 * idx]);
@@ -284,6 +293,8 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
         PathWriter pw{a.paths + size_t(idx) * a.max_path_length, a.max_path_length};
         if (Q == 0 || T == 0)
         {
+            if (a.spec_phase == 1)
+                continue;
             // the reference asserts non-empty sequences; the only path
             if (wv == 0)
             {
@@ -310,6 +321,7 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
             const uint32_t w = uniu(tcod[(t - 1) >> 4]);
             return int((w >> (2 * ((t - 1) & 15))) & 3u);
         };
+        int kk = 0; // sweep number of this est
         while (true)
         {
             int p = min(min(T, Q), (est - dlen) / 2);
@@ -334,35 +346,79 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
             // band), Q - bw (bottom stripe)
             auto col_off = [&](int t) { return t < db ? 0 : (t < de ? t - db + 1 : Q - bw); };
             int ed       = 0;
-            // all NWV waves: several chunks with their state in LDS, 2 * NWV
-            // columns in flight; column g of a group runs chunk c at step
-            // c + 2g (it needs chunks c and c+1 of column g-1 and its own
-            // chunk c-1), one LDS barrier per step
+            if (a.spec_phase == 1 && kk < ks)
+            {
+                // launch 1: on to this item's sweep, unless the doubling
+                // loop would have stopped at the full band already
+                if (bw >= Q)
+                {
+                    if (threadIdx.x == 0)
+                        a.spec_ed[item] = kSpecUnknown;
+                    break;
+                }
+                est *= 2;
+                ++kk;
+                continue;
+            }
+            if (a.spec_phase == 1 && nwb > TLE && !st_on)
+            {
+                // a sweep with its chunk state in HBM needs its stores (the
+                // host does not run ahead such batches)
+                if (threadIdx.x == 0)
+                    a.spec_ed[item] = kSpecUnknown;
+                break;
+            }
+            if (a.spec_phase == 2 && kk < K)
+            {
+                const int ek = a.spec_ed[idx * K + kk];
+                if (ek != kSpecUnknown)
+                {
+                    if (!(ek <= est || bw == Q))
+                    {
+                        est *= 2; // launch 1's distance rejects this band
+                        ++kk;
+                        continue;
+                    }
+                    if (kk == K - 1)
+                        break; // accepted, and its band matrix is in this pair's slot
+                }
+            }
+            // all NWV waves: several chunks with their state in LDS; half
+            // wave g runs columns g + 1, g + 1 + G, ... (G = 2 * NWV), column
+            // g + 1 + G q starting at step 2 g + q P and its chunk c at the
+            // step after chunk c-1 (it needs chunks c and c+1 of the previous
+            // column, which started at least 2 steps earlier, and its own
+            // chunk c-1); P = max(2 G, nch), so the columns follow each
+            // other without draining the pipeline between groups of G
+            // columns; one LDS barrier per step
             auto sweep_multi = [&]() -> int {
                 lds_barrier(); // this pair's target and patterns (wave 0), previous backtrace done
                 for (int w = int(threadIdx.x); w < nwb; w += kWave * NWV)
                 {
                     const BandEntry e0{~0u, 0u, min((w + 1) * kWordBits, bw), 0};
                     lds_put(reg + w, e0);
-                    glb_put(E + (w), e0);
+                    if (st_on)
+                        glb_put(E + (w), e0);
                 }
                 lds_barrier();
                 constexpr int G = 2 * NWV;
                 const int g     = 2 * wv + (lane >> 5);
                 const int hl    = lane & 31;
-                const int nst   = nch + 2 * (G - 1);
-                for (int t0 = 1; t0 <= T; t0 += G)
+                const int P     = max(2 * G, nch);
+                // the last column's last chunk
+                const int nst   = 2 * ((T - 1) % G) + ((T - 1) / G) * P + nch;
+                int carry       = 1; // +1 into the band's top row
+                int c           = -2 * g; // chunk of the half wave's column at this step
+                int tt          = 1 + g;  // the half wave's column
+                for (int st = 0; st < nst; st++)
                 {
-                    const int tt    = t0 + g; // this half wave's column
                     const bool hcol = tt <= T;
                     const int tc    = min(tt, T);
                     const int code  = int((tcod[(tc - 1) >> 4] >> (2 * ((tc - 1) & 15))) & 3u);
                     const int off   = col_off(tc);
                     const bool diag = tc >= db && tc < de;
-                    int carry       = 1; // +1 into the band's top row
-                    for (int st = 0; st < nst; st++)
+                    carry           = c == 0 ? 1 : carry;
                     {
-                        const int c        = st - 2 * g;
                         const bool cin     = hcol && c >= 0 && c < nch;
                         const int w        = c * kChunkWords + hl;
                         const bool valid   = cin && w < nwb;
@@ -406,9 +462,16 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
                         {
                             const BandEntry o{pv, mv, sc, 0};
                             lds_put(reg + w, o);
-                            glb_put(E + (size_t(tt) * nwb + w), o);
+                            if (st_on)
+                                glb_put(E + (size_t(tt) * nwb + w), o);
                         }
                         lds_barrier();
+                    }
+                    // next step: the next chunk, or the half wave's next column
+                    if (++c == P)
+                    {
+                        c = 0;
+                        tt += G;
                     }
                 }
                 __syncthreads(); // every wave's band-matrix stores before wave 0's backtrace
@@ -429,7 +492,7 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
                 const uint32_t cdb = crb << 1;
                 uint32_t pv = ~0u, mv = 0u;
                 int sc      = min((lane + 1) * kWordBits, bw);
-                if (act_l)
+                if (act_l && st_on)
                     glb_put(E + (lane), BandEntry{pv, mv, sc, 0});
                 uint32_t eqn = band_pattern(patL, pw_stride, nwq, col_off(1), lane, code_of(1));
                 for (int t = 1; t <= T; t++)
@@ -462,7 +525,7 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
                         mv              = m2;
                         sc += right + down;
                     }
-                    if (act_l)
+                    if (act_l && st_on)
                         glb_put(E + (size_t(t) * nwb + lane), BandEntry{pv, mv, sc, 0});
                 }
                 ed = uni(__builtin_amdgcn_readlane(sc, lastw));
@@ -482,7 +545,8 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
                     const BandEntry e0{~0u, 0u, min((w + 1) * kWordBits, bw), 0};
                     if constexpr (lds_state)
                         lds_put(reg + w, e0);
-                    glb_put(E + (w), e0);
+                    if (st_on || !lds_state)
+                        glb_put(E + (w), e0);
                 }
                 __threadfence_block();
                 wave_sync();
@@ -553,7 +617,8 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
                             {
                                 const BandEntry o{pv, mv, sc, 0};
                                 lds_put(reg + w, o);
-                                glb_put(E + (size_t(tt) * nwb + w), o);
+                                if (st_on)
+                                    glb_put(E + (size_t(tt) * nwb + w), o);
                             }
                         }
                     }
@@ -630,7 +695,8 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
                             const BandEntry o{pv, mv, sc, 0};
                             if constexpr (lds_state)
                                 lds_put(reg + w, o);
-                            glb_put(E + (size_t(t) * nwb + w), o);
+                            if (st_on || !lds_state)
+                                glb_put(E + (size_t(t) * nwb + w), o);
                         }
                     }
                     if constexpr (!lds_state)
@@ -668,9 +734,22 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
                     __syncthreads();
                 }
             }
+            if (a.spec_phase == 1)
+            {
+                if (threadIdx.x == 0)
+                    a.spec_ed[item] = ed;
+                break;
+            }
             if (ed <= est || bw == Q)
                 break;
             est *= 2;
+            ++kk;
+        }
+        if (a.spec_phase == 1)
+        {
+            // the next item's target and patterns (wave 0) wait for every wave
+            __syncthreads();
+            continue;
         }
         if (wv != 0)
             continue; // the backtrace is wave 0's
@@ -717,11 +796,46 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
             tb = lo;
             te = hi;
         };
+        // bands too wide for two whole columns in the tile (multi-wave
+        // kernels: long queries): a 64-word x LT-column window of the band
+        // around the walk instead (lane r loads word w0 + r of each column,
+        // one coalesced 1 KiB load per column), refilled when the walk leaves
+        // it; words outside [0, nwb) (the flat index map aliases word nwb onto
+        // the next column) read HBM.  The one-wave kernel (short pairs, many
+        // resident) reads such steps from HBM: the window's registers would
+        // cost it resident waves
+        const int LT = NWV > 1 ? TLE / kWave : 0;
+        int w0 = INT_MIN / 2, j0 = INT_MIN / 2;
+        auto refill_win = [&](int wc, int jc) {
+            w0 = wc - kWave / 2;
+            j0 = jc - LT + 1;
+            const int w     = w0 + lane;
+            const bool w_ok = w >= 0 && w < nwb;
+            wave_sync();
+            for (int c0 = 0; c0 < LT; c0 += 8)
+            {
+                BandEntry v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                {
+                    const int col = j0 + c0 + u;
+                    if (w_ok && c0 + u < LT && col >= 0 && col <= T)
+                        v[u] = glb_get(E + (int64_t(w) + int64_t(nwb) * col));
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (c0 + u < LT)
+                        lds_put(reg + ((c0 + u) * kWave + lane), v[u]);
+            }
+            wave_sync();
+        };
         const uint32_t lem = (bw % kWordBits) != 0 ? (1u << (bw % kWordBits)) - 1u : ~0u;
         const int bl       = min(lane, 2);
         int i = bw, j = T;
         if (use_tile)
             refill(j);
+        else if (LT >= 2)
+            refill_win(i / kWordBits, j);
         // start from the band's last word: the reference reads word
         // band_width / 32 (:393), one past the band when band_width % 32 == 0
         int s = uni(glb_get(E + (int64_t((bw - 1) / kWordBits) + int64_t(nwb) * j)).sc);
@@ -730,6 +844,14 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
             const int phase = j >= de ? 3 : (j >= db ? 2 : 1);
             if (use_tile && int64_t(nwb) * (j - 1) < tb)
                 refill(j);
+            else if (!use_tile && LT >= 2)
+            {
+                // lanes 0..2 read words (i - 2) / 32 .. (i + 1) / 32 of
+                // columns j - 1 and j
+                const int wc = i / kWordBits;
+                if (wc - 1 < w0 || wc + 1 >= w0 + kWave || j - 1 < j0 || j > j0 + LT - 1)
+                    refill_win(wc, j);
+            }
             // lane 0: above, lane 1: diagonal, lane 2: left
             int gi, gj, spv;
             bool special;
@@ -759,8 +881,9 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
             const int64_t o = int64_t(wi) + int64_t(nwb) * gj;
             const bool inr  = o >= 0 && o < total;
             BandEntry e{0u, 0u, 0, 0};
-            if (o >= tb && o < te)
-                e = lds_get(reg + (o - tb));
+            const unsigned ww = unsigned(wi - w0), cc = unsigned(gj - j0);
+            if (use_tile ? (o >= tb && o < te) : (inr && ww < unsigned(kWave) && cc < unsigned(LT) && wi < nwb))
+                e = use_tile ? lds_get(reg + (o - tb)) : lds_get(reg + (cc * kWave + ww));
             else if (inr)
                 e = glb_get(E + (o));
             uint32_t mask = shl_ptx(~1u, bi);

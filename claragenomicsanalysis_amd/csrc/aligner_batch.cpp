@@ -301,6 +301,8 @@ public:
         dalloc(reinterpret_cast<void**>(&d_paths_), size_t(max_result_) * max_n_ + 16);
         dalloc(reinterpret_cast<void**>(&d_plen_), size_t(max_n_) * 4);
         dalloc(reinterpret_cast<void**>(&d_stats_), 32);
+        if (algo_ == GWAMD_ALIGNER_MYERS_BANDED)
+            dalloc(reinterpret_cast<void**>(&d_spec_ed_), size_t(max_n_) * kMaxSpecSweeps * 4, false);
         // workspace: every slot entry is written before it is read
         dalloc(reinterpret_cast<void**>(&d_ws_), size_t(slots_) * size_t(slot_bytes_), false);
         h_seqs_.reserve(size_t(2) * stride_ * max_n_ + 16, stream_);
@@ -337,7 +339,8 @@ public:
                 if (e)
                     (void)hipEventDestroy(e);
         for (void* p : {static_cast<void*>(d_seqs_), static_cast<void*>(d_lens_), static_cast<void*>(d_paths_),
-                        static_cast<void*>(d_plen_), static_cast<void*>(d_ws_), static_cast<void*>(d_stats_)})
+                        static_cast<void*>(d_plen_), static_cast<void*>(d_ws_), static_cast<void*>(d_stats_),
+                        static_cast<void*>(d_spec_ed_)})
             if (p)
                 (void)hipFree(p);
     }
@@ -571,10 +574,41 @@ public:
             }
         }
         const int grid     = std::min<int>(count, nslots);
-        if (algo_ == GWAMD_ALIGNER_MYERS_BANDED || algo_ == GWAMD_ALIGNER_UKKONEN)
+        const int ks       = spec_sweeps(count, nslots);
+        if (ks > 0)
+        {
+            // band doubling run ahead: every (pair, sweep) on its own
+            // workgroup, then one workgroup per pair on its own slot
+            a.spec_sweeps = ks;
+            a.spec_phase  = 1;
+            GWAMD_HIP_CHECK(gwamd_internal_banded_launch(&a, algo_, std::min(count * ks, resident_), s));
+            a.spec_phase = 2;
+            GWAMD_HIP_CHECK(gwamd_internal_banded_launch(&a, algo_, count, s));
+        }
+        else if (algo_ == GWAMD_ALIGNER_MYERS_BANDED || algo_ == GWAMD_ALIGNER_UKKONEN)
             GWAMD_HIP_CHECK(gwamd_internal_banded_launch(&a, algo_, grid, s));
         else
             GWAMD_HIP_CHECK(gwamd_internal_align_launch(&a, algo_, grid, s));
+    }
+    // banded Myers: sweeps of the band doubling run ahead on their own
+    // workgroups when a launch's pairs leave most of the GPU idle (few long
+    // pairs: every pair on its own slot, all (pair, sweep) items resident) and
+    // every band's chunk state fits LDS; 0 = the plain loop.
+    // GWAMD_BAND_SPEC=k forces k (0..kMaxSpecSweeps, diagnostic)
+    int spec_sweeps(int32_t count, int32_t nslots) const
+    {
+        if (algo_ != GWAMD_ALIGNER_MYERS_BANDED || count <= 0)
+            return 0;
+        int k = band_waves_ > 1 ? kDefaultSpecSweeps : 0;
+        if (const char* e = gwamd::host::diag_env("GWAMD_BAND_SPEC"))
+        {
+            k = std::atoi(e);
+            if (k < 0 || k > kMaxSpecSweeps)
+                throw std::invalid_argument("GWAMD_BAND_SPEC must be 0..8 sweeps");
+        }
+        const bool fits = count <= nslots && int64_t(count) * k <= resident_ && 2 * count <= cus_ &&
+                          pat_words_ <= tile_bytes_ / 16;
+        return fits ? k : 0;
     }
     // pipeline stages of align_all(): as many (up to kMaxStages) as keep
     // each stage's half of the slots busy four times over; 1 = one stage
@@ -657,7 +691,14 @@ private:
     {
         using namespace gwamd::aln;
         const int pat_words = (max_q_ + kWordBits - 1) / kWordBits;
-        const int64_t ws_cap = int64_t(64) << 30; // resident workspace slots within 64 GiB of the 288 GB HBM
+        // resident workspace slots within 64 GiB of the 288 GB HBM, or up to
+        // 96 GiB (3/4 of the free memory at most): 32 pairs of 65,536 bp need
+        // 32 band-matrix slots of 2.15 GB, and one slot fewer than pairs
+        // doubles the kernel
+        size_t free_b = 0, total_b = 0;
+        GWAMD_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+        const int64_t ws_cap =
+            std::max<int64_t>(int64_t(64) << 30, std::min<int64_t>(int64_t(96) << 30, int64_t(free_b / 4 * 3)));
         if (algo_ == GWAMD_ALIGNER_MYERS_BANDED)
         {
             // target as 2-bit letter codes, letter-major query patterns, and a
@@ -752,8 +793,10 @@ private:
             per_cu = std::max(per_cu, wide);
         }
         GWAMD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
-        slots_ = std::max(1, per_cu * cus);
-        slots_ = int32_t(std::max<int64_t>(1, std::min<int64_t>(slots_, ws_cap / slot_bytes_)));
+        slots_    = std::max(1, per_cu * cus);
+        resident_ = slots_;
+        cus_      = cus;
+        slots_    = int32_t(std::max<int64_t>(1, std::min<int64_t>(slots_, ws_cap / slot_bytes_)));
         apply_grid_override();
         slots_ = std::min(slots_, max_n_);
     }
@@ -880,6 +923,9 @@ private:
         a.ukkonen_p        = gwamd::aln::kUkkonenP;
         a.uk_threads       = 0; // launch(): the batch's widest band may need ukkonen_wide_kernel
         a.band_waves       = band_waves_;
+        a.spec_phase       = 0;
+        a.spec_sweeps      = 0;
+        a.spec_ed          = d_spec_ed_;
         a.lds_edge_off     = lds_edge_off_;
         a.stats            = d_stats_;
         return a;
@@ -908,6 +954,8 @@ private:
     // download-done events and the kernel's start / stop events; stages_ of
     // the last align_all() (0: none yet) and their first pairs
     static constexpr int kMaxStages = 8;
+    static constexpr int kMaxSpecSweeps     = 8; // banded Myers sweeps run ahead, at most
+    static constexpr int kDefaultSpecSweeps = 5; // est x 1 .. x 16
     hipStream_t stream2_ = nullptr, s_in_ = nullptr, s_out_ = nullptr;
     hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
     hipEvent_t ev_d_[kMaxStages]     = {};
@@ -923,6 +971,8 @@ private:
     int32_t* d_plen_  = nullptr;
     uint8_t* d_ws_    = nullptr;
     unsigned long long* d_stats_ = nullptr;
+    int32_t* d_spec_ed_          = nullptr; // banded Myers: distances of the sweeps run ahead
+    int32_t resident_ = 1, cus_ = 1;        // workgroups resident at once, CUs
     PinnedBuf h_seqs_, h_lens_, h_paths_, h_plen_;
     std::vector<std::shared_ptr<Alignment>> alignments_;
 };

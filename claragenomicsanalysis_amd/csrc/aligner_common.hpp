@@ -28,6 +28,7 @@ constexpr int kUkWideChunks = 4;  // wider bands: rows per thread of a workgroup
 constexpr int kUkTileRows  = 64;  //   backtrace tile: band rows x
 constexpr int kUkTileCols  = 128; //   anti-diagonal columns (int16, 16 KiB)
 constexpr int kUkkonenP    = 100; // aligner_global_ukkonen.cpp:29
+constexpr int32_t kSpecUnknown = -2147483647 - 1; // spec_ed: sweep not run ahead
 constexpr int16_t kUkMax   = 32766; // numeric_limits<int16_t>::max() - 1 (ukkonen_gpu.cu:75)
 
 // AlignmentState (cudaaligner.hpp:46-52)
@@ -79,6 +80,15 @@ struct Args
     int32_t uk_threads;      // Ukkonen: > 0 runs ukkonen_wide_kernel with this many threads per pair
     int32_t lds_edge_off;    //   its 64-row-group edge values (2 x 2 x kUkWideChunks*16 int)
     int32_t band_waves;      // banded Myers: waves per pair (1, 4, 8 or 16; myers_banded_kernel<NWV>)
+    // banded Myers band doubling run ahead (few long pairs): launch 1
+    // (spec_phase 1) runs sweeps 0..spec_sweeps-1 of every pair on their own
+    // workgroups (distance only; the last one also stores its band matrix in
+    // the pair's slot) into spec_ed[pair * spec_sweeps + k]; launch 2
+    // (spec_phase 2) skips the sweeps those distances reject and the stored
+    // last one; spec_phase 0: the plain loop
+    int32_t spec_phase;
+    int32_t spec_sweeps;
+    int32_t* spec_ed;
     // path counters, accumulated over the aligner's launches (gwamd_aligner_get_stats):
     // [0] banded Myers sweeps whose chunk state went through HBM, [1] pairs
     // aligned by ukkonen_wide_kernel, [2] the most band rows one thread of

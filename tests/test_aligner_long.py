@@ -130,6 +130,34 @@ def test_myers_banded_two_column_sweep(waves, monkeypatch):
         assert g == oracle.align(q, tt, oracle.ALIGN_MYERS_BANDED, mq), (len(q), len(tt))
 
 
+@pytest.mark.parametrize("spec", ["0", "1", "2", "3", "8"])
+@pytest.mark.parametrize("waves", ["4", "8"])
+def test_myers_banded_run_ahead_sweeps(spec, waves, monkeypatch):
+    # band doubling run ahead (few long pairs): launch 1 runs sweeps
+    # 0..spec-1 of every pair on their own workgroups (distance only, the last
+    # one with its band matrix), launch 2 skips the rejected ones and the
+    # stored one and carries on doubling past them. Pairs needing 1 to 5
+    # sweeps, and one whose band reaches the whole query early
+    monkeypatch.setenv("GWAMD_BAND_SPEC", spec)
+    monkeypatch.setenv("GWAMD_BAND_WAVES", waves)
+    rng = random.Random(47)
+    t = rand_seq(rng, 12000)
+    pairs = [(mutate(rng, t, 0.02), t), (mutate(rng, t, 0.12), t[:11500]), (mutate(rng, t, 0.3), t),
+             (mutate(rng, t[:9001], 0.2), t[:9001]), (rand_seq(rng, 11000), t[:11001]),
+             (mutate(rng, t[:2500], 0.1), t[:2400])]
+    got, mq = gpu_states(pairs, "myers_banded")
+    for (q, tt), g in zip(pairs, got):
+        assert g == oracle.align(q, tt, oracle.ALIGN_MYERS_BANDED, mq), (spec, len(q), len(tt))
+
+
+def test_band_spec_checked(monkeypatch):
+    monkeypatch.setenv("GWAMD_BAND_SPEC", "9")
+    b = CudaAlignerBatch(12000, 12000, 1, algorithm="myers_banded")
+    assert b.add_alignment("ACGT" * 3000, "ACGT" * 3000) == 0
+    with pytest.raises(ValueError):
+        b.align_all()
+
+
 def test_band_tile_bytes_checked(monkeypatch):
     monkeypatch.setenv("GWAMD_BAND_TILE_BYTES", "4k")
     with pytest.raises(ValueError):
