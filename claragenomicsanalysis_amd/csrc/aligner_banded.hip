@@ -1170,17 +1170,32 @@ __global__ void __launch_bounds__(kWave) ukkonen_kernel(Args a)
         int i = m - 1, j = n - 1;
         refill(i + j);
         int s = uni(val(i, j));
-        // lane 0: above (i-1, j), lane 1: diagonal (i-1, j-1), lane 2: left (i, j-1)
-        const int di = lane == 2 ? 0 : 1;
-        const int dj = lane == 0 ? 0 : 1;
+        // neighbours above (i-1, j), diagonal (i-1, j-1) and left (i, j-1).
+        // When the tile holds >= 16 columns, lane 8a + b reads cell (i0 - a,
+        // j0 - b) of an 8 x 8 window at (i0, j0) and the walk takes its
+        // neighbours from registers until it is 7 rows or columns away (each
+        // step moves a, b or both by one): one LDS round trip per ~7 steps.
+        // Otherwise lanes 0..2 read the three neighbours at every step
+        const bool win = TE8 >= 16 * bw;
+        const int wa   = win ? lane >> 3 : (lane == 2 ? 0 : 1);
+        const int wb   = win ? lane & 7 : (lane == 0 ? 0 : 1);
+        int i0 = i, j0 = j, wv = 0;
+        bool reload = true;
         while (i > 0 && j > 0)
         {
-            if (int64_t(bw) * (i + j - 2) < tb)
-                refill(i + j);
-            const int v     = val(i - di, j - dj);
-            const int above = uni(__builtin_amdgcn_readlane(v, 0));
-            const int dg    = uni(__builtin_amdgcn_readlane(v, 1));
-            const int left  = uni(__builtin_amdgcn_readlane(v, 2));
+            if (reload || i0 - i > 6 || j0 - j > 6)
+            {
+                if (int64_t(bw) * max(i + j - (win ? 14 : 2), 0) < tb)
+                    refill(i + j);
+                i0     = i;
+                j0     = j;
+                wv     = val(i0 - wa, j0 - wb);
+                reload = !win;
+            }
+            const int o     = win ? 8 * (i0 - i) + (j0 - j) : 0; // window lane of (i, j)
+            const int above = uni(__builtin_amdgcn_readlane(wv, win ? o + 8 : 0));
+            const int dg    = uni(__builtin_amdgcn_readlane(wv, win ? o + 9 : 1));
+            const int left  = uni(__builtin_amdgcn_readlane(wv, win ? o + 1 : 2));
             int8_t r;
             if (left + 1 == s)
             {
