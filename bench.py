@@ -91,7 +91,12 @@ CONFIGS = {
     # 32-bit scores (4 kb reads, 16 per window: use32bitScore,
     # cudapoa_limits.hpp:28-53; the LDS kernel's 32-bit pass)
     "B_banded_384": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=True, bw=384, windows=1024),
-    "B_banded_1024": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=True, bw=1024, windows=1024),
+    # (bw 1,024 runs four windows per CU, so the persistent grid's per-slot
+    # scratch for 1,024 slots needs more than 12.5 MB per window; the
+    # reference's benchmark gives its batch 90 % of the free memory,
+    # single_batch.hpp:43-50)
+    "B_banded_1024": dict(backbone=1000, reads=32, err=50, max_seq=1100, banded=True, bw=1024, windows=1024,
+                          mem_per_window=24e6),
     "F_int32_4k": dict(backbone=4000, reads=16, err=200, max_seq=4400, banded=False, bw=256, windows=128,
                        mem_per_window=300e6),
 }

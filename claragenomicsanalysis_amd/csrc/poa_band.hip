@@ -37,13 +37,11 @@ namespace gwamd
 namespace poa
 {
 
-constexpr int kBandRing  = 16; // LDS ring rows (power of two)
 #ifndef GWAMD_BAND_ADD_AU
 #define GWAMD_BAND_ADD_AU 4
 #endif
 // read positions per lane and pass of the add (one wave per SIMD: registers to spare)
 constexpr int kBandAddAU = GWAMD_BAND_ADD_AU;
-constexpr int kBandTile  = 64; // traceback tile rows
 constexpr uint32_t kNpEsc = 63;
 
 // rec_a: base (8) | np (6; 63 = escape: read the graph) | sink (1) | spill (1) | band_start/4 (16)
@@ -367,6 +365,7 @@ __device__ __forceinline__ void band_fetch(int p, int d, int r, const int (&Hp)[
                                            GWAMD_LDS ScoreT* ring, const ScoreT* spill, int rowsz, int gap, int minv,
                                            int lane, int (&F)[CPL + 1])
 {
+    constexpr int kBandRing = band_ring_rows(CPL);
     if (p == 0)
     {
 #pragma unroll
@@ -484,6 +483,7 @@ __device__ __forceinline__ int band_forward(WinGraph<SizeT> g, BandAux X, int V,
                             const Band& B, const Scores sc, GWAMD_LDS ScoreT* ring, GWAMD_LDS uint32_t* stage,
                             ScoreT* spill, int rowsz, int lane, BandProf& bp)
 {
+    constexpr int kBandRing = band_ring_rows(CPL);
     X = as_global(X);
     g = as_global(g);
     const uint64_t f_t0 = BandProf::now();
@@ -990,6 +990,7 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
                               GWAMD_LDS uint8_t* tile, SizeT* ag, SizeT* ar, int aln_cap,
                               int lane, BandProf& bp, bool rank, int tbmode)
 {
+    constexpr int kBandTile = band_tile_rows(CPL);
     X = as_global(X);
     spill = glb(spill);
     ag    = glb(ag);
@@ -1005,7 +1006,7 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
     int prev_i = 0, prev_j = 0;
     int ti0 = INT_MIN / 2;
     uint32_t ta = 0, tb = 0, tcw = 0; // row records of the tile rows, lane k: row ti0 + k
-    static_assert(kBandTile == kWave, "tile records are held one per lane");
+    static_assert(kBandTile <= kWave, "tile records are held one per lane (lanes past the tile: unused)");
     // per-row move-decode info of the tile rows, after the code tile
     GWAMD_LDS v4i_t* rowinfo = reinterpret_cast<GWAMD_LDS v4i_t*>(tile + kBandTile * bw);
     int n = 0, loops = 0;
@@ -1030,12 +1031,12 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
         // 4*CPL 16-B pieces per lane, all loads of a chunk issued before its
         // first store waits (band widths past 512: chunks of 16 pieces, so the
         // staging stays within 64 VGPRs)
-        constexpr int kPer    = 4 * CPL;
+        constexpr int kPer    = kBandTile * CPL / 16;
         constexpr int kPerRow = 4 * CPL; // 16-B pieces per code row
         constexpr int kCh     = kPer > 32 ? (kPer % 16 == 0 ? 16 : 8) : kPer;
         static_assert(kPer % kCh == 0, "whole chunks");
         {
-            const int rr = min(ti0 + lane, V); // kBandTile == kWave: one record per lane
+            const int rr = min(ti0 + lane, V); // one record per lane (rows past the tile: unused)
             ta           = X.reca[rr];
             tb           = X.recb[rr];
             tcw          = X.recc[rr];
@@ -1089,7 +1090,7 @@ __device__ __forceinline__ int band_traceback(WinGraph<SizeT> g, BandAux X, int 
     auto decode_cell = [&](int t) -> uint32_t {
         const int r      = G.row(t);
         const int c      = G.col(t);
-        const int k      = min(max(r - ti0, 0), kWave - 1);
+        const int k      = min(max(r - ti0, 0), kBandTile - 1);
         const v4i_t info = rowinfo[k];
         const uint32_t x = uint32_t(info.x);
         const int bs     = int(x & 0x3fffffffu);
@@ -1330,6 +1331,7 @@ __device__ __forceinline__ void band_window_ptrs(const Buffers& b, const Dims& d
 template <typename ScoreT, typename SizeT, bool MSA, int CPL>
 __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Buffers b, Dims d, Scores sc)
 {
+    constexpr int kBandRing = band_ring_rows(CPL);
     extern __shared__ __align__(16) uint8_t lds[];
     __shared__ int sh_status;
     __shared__ int sh_len;

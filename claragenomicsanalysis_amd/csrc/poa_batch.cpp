@@ -785,8 +785,9 @@ private:
         const int64_t ms  = dims_.max_seq_len, mn = dims_.max_nodes;
         const int64_t read_b  = a16(gwamd::poa::kReadGuard + ms + bw + 48);
         const int64_t sh_b    = 64;
-        const int64_t ring_b  = a16(int64_t(16) * rowsz * sbytes) + 4 * 256 * 4 + 1024 * 4; // + record staging
-        const int64_t tile_b  = a16(int64_t(64) * bw + 64 * 16 + 512 + gwamd::poa::kTbRankBytes); // codes +
+        const int ring_rows   = gwamd::poa::band_ring_rows(cpl), tile_rows = gwamd::poa::band_tile_rows(cpl);
+        const int64_t ring_b  = a16(int64_t(ring_rows) * rowsz * sbytes) + 4 * 256 * 4 + 1024 * 4; // + record staging
+        const int64_t tile_b  = a16(int64_t(tile_rows) * bw + 64 * 16 + 512 + gwamd::poa::kTbRankBytes); // codes +
                                                                       // per-row decode info + walk tables
         const int64_t flags_b = 2 * a16(mn + 2); // row program: spill and far flags
         const int64_t add_b   = 7 * a16(ms + 16) + a16(2 * (mn + ms + 16)); // + the edge-slot bytes
@@ -829,7 +830,7 @@ private:
         dims_.lds_waves      = 1;
         dims_.lds_bytes      = int32_t(total);
         dims_.lds_ring_off   = int32_t(read_b);
-        dims_.lds_ring_rows  = 16;
+        dims_.lds_ring_rows  = ring_rows;
         dims_.lds_work_bytes = int32_t(work);
         dims_.lds_sh_off     = int32_t(read_b + work);
         dims_.score_stride   = rowsz; // spill rows: band row at position idx + cpl - 1

@@ -22,6 +22,13 @@ constexpr int kCellsPerLane  = 8;  // full-mode DP: 8 consecutive columns per la
 constexpr int kChunk         = kWave * kCellsPerLane; // 512 columns per wave pass
 constexpr int kAdRing        = 128; // LDS ring rows of the banded anti-diagonal pass (poa_band_ad.hpp)
 constexpr int kAdSpillDist   = kAdRing - kWave + 1; // successor distance that needs a spill row there
+// banded kernel (poa_band.hip): LDS ring rows (power of two) and traceback
+// tile rows per cells-per-lane value.  Band widths past 512 take a 32-row
+// tile and, at 1,024, an 8-row ring, so four windows share a CU (one wave per
+// SIMD) instead of two; the host plan (plan_band_kernel) sizes the LDS image
+// from the same two functions
+constexpr int band_ring_rows(int cpl) { return cpl >= 16 ? 8 : 16; }
+constexpr int band_tile_rows(int cpl) { return cpl >= 10 ? 32 : 64; }
 constexpr int kReadGuard     = 64;  // banded kernel: LDS bytes in front of the staged read
 constexpr int kAdMaxWaves    = 4;   // waves of a banded workgroup running the anti-diagonal pass
 constexpr int kColShift      = 7;  // column j of a full-mode score row lives at index j + 7,
