@@ -224,7 +224,8 @@ def load_traffic(kind, key, n):
         return None, None
     if tf.get("windows", tf.get("pairs")) != n:
         return None, None
-    return tf.get("hbm_bytes_per_launch"), tf.get("source")
+    # aligner batches run several launches per align_all(): bytes per step
+    return tf.get("hbm_bytes_per_step", tf.get("hbm_bytes_per_launch")), tf.get("source")
 
 
 def load_sq(key):

@@ -16,7 +16,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(src, name, config="B", windows=1024, kernel="poa_window_kernel"):
+def main(src, name, config="B", windows=1024, kernel="poa_window_kernel", steps=None):
     dst = os.path.join(ROOT, "profiles", name)
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "trace_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
@@ -54,12 +54,21 @@ def main(src, name, config="B", windows=1024, kernel="poa_window_kernel"):
         json.dump({"config": config, "windows": windows, "hbm_bytes_per_launch": hbm, "source": "profiles/" + name},
                   open(os.path.join(ROOT, "profiles", "traffic_poa_%s.json" % config), "w"), indent=1)
     else:
-        json.dump({"config": config, "pairs": windows, "hbm_bytes_per_launch": hbm, "source": "profiles/" + name},
-                  open(os.path.join(ROOT, "profiles", "traffic_aligner_%s.json" % config), "w"), indent=1)
+        t = {"config": config, "pairs": windows, "hbm_bytes_per_launch": hbm, "source": "profiles/" + name}
+        if steps:
+            # align_all() of a large batch runs several launches per step
+            # (pipeline stages on two streams): bytes per step = every
+            # dispatch of the profiled run / the steps it ran (warmup included)
+            t["dispatches_per_step"] = len(vals["FETCH_SIZE"]) / steps
+            t["hbm_bytes_per_step"] = int((2 * sum(vals["FETCH_SIZE"]) + sum(vals["WRITE_SIZE"])) * 1024 / steps)
+            t["kernel_ns_sum_per_step"] = (float(poa[0]["TotalDurationNs"]) / steps) if poa else None
+            summ.update({k: t[k] for k in ("dispatches_per_step", "hbm_bytes_per_step", "kernel_ns_sum_per_step")})
+            json.dump(summ, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+        json.dump(t, open(os.path.join(ROOT, "profiles", "traffic_aligner_%s.json" % config), "w"), indent=1)
     print(json.dumps(summ, indent=1))
 
 
 if __name__ == "__main__":
     a = sys.argv[1:]
     main(a[0], a[1], a[2] if len(a) > 2 else "B", int(a[3]) if len(a) > 3 else 1024,
-         a[4] if len(a) > 4 else "poa_window_kernel")
+         a[4] if len(a) > 4 else "poa_window_kernel", int(a[5]) if len(a) > 5 else None)
