@@ -479,7 +479,7 @@ __device__ __forceinline__ void fwd2_rows(WinGraph<SizeT> g, const RowProg& P, i
                     if (np == 0)
                         n = 1;
                 }
-                const uint32_t ub = rec & 0x7fu;
+                const uint32_t ub = uint32_t(row_base<SizeT>(g, rec, r));
                 if (!((ub & 0xc0u) == 0x40u && ((0x10008aull >> (ub & 0x3fu)) & 1u)))
                 {
                     const GWAMD_LDS uint32_t* rw = reinterpret_cast<const GWAMD_LDS uint32_t*>(read + ja);

@@ -161,7 +161,7 @@ __device__ int nw_forward_lds_w(WinGraph<SizeT> g, const RowProg& P, int V, cons
             const uint32_t rec = rec_c;
             const int np       = np_c;
             const int pv       = pv_c;
-            const int base     = int(rec & 0x7f); // bit 7: the 16-bit pass's general-path flag
+            const int base     = row_base<SizeT>(g, rec, r); // bit 7: the 16-bit pass's general-path flag
             const bool spill_r = (rec >> 15) & 1;
             GWAMD_LDS int32_t* row = ring + (r & mask) * ring_stride;
             const bool anyfar  = __builtin_amdgcn_ballot_w64(lane < np && pv != 0 && r - pv > mask) != 0;

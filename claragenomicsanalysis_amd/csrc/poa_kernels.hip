@@ -235,6 +235,17 @@ __device__ __forceinline__ int prog_np(WinGraph<SizeT> g, int r, uint32_t rec)
 // ring_rows or more rows later; that is marked from the successor's side
 // (row s, predecessor row p: s - p >= ring_rows) into byte flags in `flags`
 // (V + 2 bytes of free LDS), so no out-edge lists are read.
+// The base of forward-pass row r from its record (build_row_program): bits
+// 0-6, or the graph's own byte when they hold 0x7f, which stands for 0x7f and
+// for every byte >= 0x80 (the reference compares whole bytes, and bit 7 of
+// the record is the general-path flag)
+template <typename SizeT>
+__device__ __forceinline__ int row_base(WinGraph<SizeT> g, uint32_t rec, int r)
+{
+    const int b = int(rec & 0x7fu);
+    return b == 0x7f ? uniform(int(g.base[g.sorted[r - 1]])) : b;
+}
+
 template <typename SizeT>
 __device__ void build_row_program(WinGraph<SizeT> g, int V, uint32_t* rec, uint16_t* xl, int xl_cap,
                                   int ring_rows, int lane, GWAMD_LDS uint8_t* flags)
@@ -280,11 +291,14 @@ __device__ void build_row_program(WinGraph<SizeT> g, int V, uint32_t* rec, uint1
             const int excl   = wave_excl_sum(n >= 2 ? n : 0, lane, total);
             if (valid)
             {
-                uint32_t v = uint32_t(base[u]) | (uint32_t(oc[u] == 0 ? 1 : 0) << 14);
-                // bit 7 (bases are ASCII): the forward pass must take its
-                // general path (nw_forward_lds_v2): a source, a predecessor
-                // beyond the ring, an escaped list or a base other than ACGT
+                // bits 0-6: the base, 0x7f standing for 0x7f and for every
+                // byte >= 0x80 (the forward passes read such rows' base back
+                // from the graph, row_base); bit 7: the forward pass must take
+                // its general path (nw_forward_lds_v2): a source, a
+                // predecessor beyond the ring, an escaped list or a base
+                // other than ACGT
                 const uint32_t ub = uint32_t(base[u]);
+                uint32_t v        = (ub >= 0x7fu ? 0x7fu : ub) | (uint32_t(oc[u] == 0 ? 1 : 0) << 14);
                 bool slow = n == 0 || !((ub & 0xc0u) == 0x40u && ((0x10008aull >> (ub & 0x3fu)) & 1u));
                 if (n == 1)
                 {
@@ -630,7 +644,7 @@ __device__ int nw_forward_lds_pk(WinGraph<SizeT> g, const RowProg& P, int V, con
             const uint32_t rec = rec_c;
             const int np       = np_c;
             const int pv       = pv_c;
-            const int base     = int(rec & 0x7f); // bit 7: general-path flag (build_row_program)
+            const int base     = row_base<SizeT>(g, rec, r); // bit 7: general-path flag (build_row_program)
             const bool spill_r = (rec >> 15) & 1;
             int16_t* row       = ring + (r & mask) * ring_stride;
             const bool anyfar  = __builtin_amdgcn_ballot_w64(lane < np && pv != 0 && r - pv > mask) != 0;

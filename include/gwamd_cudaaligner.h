@@ -128,7 +128,9 @@ int32_t gwamd_aligner_pair_fits(int32_t algorithm, int32_t max_query_length, int
 
 /* Kernel time of the last gwamd_aligner_align_all (ms; waits for it): the
  * union of its launches' intervals, measured with HIP events on the streams
- * they ran on (large batches run as two pipelined halves on two streams).
+ * they ran on (large batches run as up to 8 pipelined stages whose kernels
+ * alternate between two streams; banded Myers batches of a few long pairs run
+ * their band doubling ahead in a first launch).
  * NULL arguments: GWAMD_E_INVALID_ARGUMENT. */
 int32_t gwamd_aligner_last_kernel_ms(gwamd_aligner* aligner, double* ms);
 

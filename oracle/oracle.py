@@ -120,14 +120,15 @@ def poa_window(reads, weights=None, gap=-8, mismatch=-6, match=8, banded=False, 
     finally:
         lib().oracle_set_spoa_accurate(0)
     n = int(clen[0])
-    consensus = bytes(cons[:n]).decode() if st == 0 and not msa else ""
+    # latin-1: lossless for any byte (windows may hold non-ASCII bases); ASCII as before
+    consensus = bytes(cons[:n]).decode("latin-1") if st == 0 and not msa else ""
     coverage = cov[:n].tolist() if st == 0 and not msa else []
     rows = None
     if msa and st == 0:
         rows = []
         for s in range(len(reads)):
             row = bytes(msa_buf[s * max_consensus:(s + 1) * max_consensus])
-            rows.append(row.split(b"\0", 1)[0].decode())
+            rows.append(row.split(b"\0", 1)[0].decode("latin-1"))
     graph = None
     if want_graph:
         nn = int(fnodes[0])

@@ -703,6 +703,46 @@ def test_marked_rows_multi_source_fwd2(fwd, monkeypatch):
     assert multi >= 10
 
 
+@pytest.mark.parametrize("shape", ["fwd2", "v1", "int32"])
+def test_non_ascii_bases_compared_whole(shape, monkeypatch):
+    # The LDS kernel's row records keep 7 bits of the base (bit 7 is the
+    # general-path flag); 0x7f stands for 0x7f and every byte >= 0x80, and
+    # the forward passes read those rows' base back from the graph, because
+    # the reference compares whole bytes (0xc1 is not 'A').  Reads carry such
+    # bytes; the graphs (edges and weights: the alignments decide them) must
+    # equal the oracle's on the 16-bit row-program pass, the round-3 pass and
+    # the 32-bit pass.
+    monkeypatch.delenv("GWAMD_POA_KERNEL", raising=False)
+    monkeypatch.delenv("GWAMD_POA_FWD", raising=False)
+    if shape == "v1":
+        monkeypatch.setenv("GWAMD_POA_FWD", "v1")
+    import random
+    rng = random.Random(9)
+    odd = [0xc1, 0xc3, 0xc7, 0xd4, 0x7f, 0xe1, 0x81]
+    wins = []
+    for k in range(8):
+        bb = bytearray(rng.choice(b"ACGT") for _ in range(250 + 30 * k))
+        for _ in range(len(bb) // 12):
+            bb[rng.randrange(len(bb))] = rng.choice(odd)
+        reads = [bytes(bb)]
+        for j in range(9):
+            r = bytearray(bb[rng.randrange(0, 10):len(bb) - rng.randrange(0, 10)])
+            for _ in range(10):
+                r[rng.randrange(len(r))] = rng.choice(odd if j % 2 else b"ACGT")
+            reads.append(bytes(r))
+        wins.append(reads)
+    max_seq = 1600 if shape == "int32" else 600
+    b = run_gpu(wins, max_seq, 10)
+    sbits = b.get_types()[0]
+    assert b.kernel_variant() == 2 and sbits == (32 if shape == "int32" else 16)
+    graphs, _ = b.get_graphs()
+    for i, w in enumerate(wins):
+        r = run_oracle(w, max_seq, 10, score_bits=sbits, want_graph=True)
+        g = graphs[i]
+        expect = {(src, v): wt for v, ins in enumerate(r.graph["in"]) for (src, wt) in ins}
+        assert {(u, v): g.weight(u, v) for (u, v) in g.edges} == expect, (shape, i)
+
+
 @pytest.mark.parametrize("spoa", [False, True])
 def test_full_int32_persistent_grid(spoa, monkeypatch):
     # the 32-bit LDS kernel on a persistent grid of 3 slots (workgroups reuse
