@@ -1171,54 +1171,95 @@ __global__ void __launch_bounds__(kWave) ukkonen_kernel(Args a)
         refill(i + j);
         int s = uni(val(i, j));
         // neighbours above (i-1, j), diagonal (i-1, j-1) and left (i, j-1).
-        // When the tile holds >= 16 columns, lane 8a + b reads cell (i0 - a,
-        // j0 - b) of an 8 x 8 window at (i0, j0) and the walk takes its
-        // neighbours from registers until it is 7 rows or columns away (each
-        // step moves a, b or both by one): one LDS round trip per ~7 steps.
-        // Otherwise lanes 0..2 read the three neighbours at every step
-        const bool win = TE8 >= 16 * bw;
-        const int wa   = win ? lane >> 3 : (lane == 2 ? 0 : 1);
-        const int wb   = win ? lane & 7 : (lane == 0 ? 0 : 1);
-        int i0 = i, j0 = j, wv = 0;
-        bool reload = true;
-        while (i > 0 && j > 0)
+        // The move out of a cell depends on that cell alone (its value is the
+        // walk's running score), so when the tile holds >= 16 columns lane
+        // 8a + b takes cell (i0 - a, j0 - b) of an 8 x 8 window at the walk's
+        // position (i0, j0) and decides that cell's move from its neighbours
+        // (three ds_bpermute reads); the walk then only follows next-lane
+        // links (one v_readlane per step) until it reaches the window's last
+        // row or column, i = 0 or j = 0, and the visited lanes store their
+        // moves at their rank on the path (a + b grows by 1 or 2 per step, so
+        // the rank is the number of visited cells with a smaller a + b).
+        // Otherwise lanes 0..2 read the three neighbours at every step.
+        if (TE8 >= 16 * bw)
         {
-            if (reload || i0 - i > 6 || j0 - j > 6)
+            const int wa = lane >> 3, wb = lane & 7;
+            while (i > 0 && j > 0)
             {
-                if (int64_t(bw) * max(i + j - (win ? 14 : 2), 0) < tb)
+                if (int64_t(bw) * max(i + j - 14, 0) < tb)
                     refill(i + j);
-                i0     = i;
-                j0     = j;
-                wv     = val(i0 - wa, j0 - wb);
-                reload = !win;
+                const int i0 = i, j0 = j;
+                const int wv = val(i0 - wa, j0 - wb);
+                const int up = __builtin_amdgcn_ds_bpermute(4 * (lane + 8), wv);
+                const int dg = __builtin_amdgcn_ds_bpermute(4 * (lane + 9), wv);
+                const int lf = __builtin_amdgcn_ds_bpermute(4 * (lane + 1), wv);
+                const bool mv_ins = lf + 1 == wv;
+                const bool mv_del = !mv_ins && up + 1 == wv;
+                const int r       = mv_ins ? int(ins) : (mv_del ? int(del) : (dg == wv ? int(kMatch) : int(kMismatch)));
+                const bool term   = wa == 7 || wb == 7 || i0 - wa <= 0 || j0 - wb <= 0;
+                const int nxt     = term ? lane : lane + (mv_ins ? 1 : (mv_del ? 8 : 9));
+                uint64_t visited  = 0;
+                uint32_t sums     = 0;
+                int o = 0, steps = 0;
+                while (true)
+                {
+                    const int nx = uni(__builtin_amdgcn_readlane(nxt, o));
+                    if (nx == o)
+                        break;
+                    visited |= 1ull << o;
+                    sums |= 1u << ((o >> 3) + (o & 7));
+                    ++steps;
+                    o = nx;
+                }
+                if ((visited >> lane) & 1ull)
+                {
+                    const int at = pw.pos + __builtin_popcount(sums & ((1u << (wa + wb)) - 1u));
+                    if (at < pw.cap)
+                        pw.path[at] = int8_t(r);
+                }
+                pw.pos += steps;
+                i = i0 - (o >> 3);
+                j = j0 - (o & 7);
             }
-            const int o     = win ? 8 * (i0 - i) + (j0 - j) : 0; // window lane of (i, j)
-            const int above = uni(__builtin_amdgcn_readlane(wv, win ? o + 8 : 0));
-            const int dg    = uni(__builtin_amdgcn_readlane(wv, win ? o + 9 : 1));
-            const int left  = uni(__builtin_amdgcn_readlane(wv, win ? o + 1 : 2));
-            int8_t r;
-            if (left + 1 == s)
-            {
-                r = ins;
-                s = left;
-                --j;
-            }
-            else if (above + 1 == s)
-            {
-                r = del;
-                s = above;
-                --i;
-            }
-            else
-            {
-                r = dg == s ? kMatch : kMismatch;
-                s = dg;
-                --i;
-                --j;
-            }
-            pw.put(r, lane);
+            pw.overflow = pw.overflow || pw.pos > pw.cap;
         }
-        pw.finish(lane);
+        else
+        {
+            // lane 0: above (i-1, j), lane 1: diagonal (i-1, j-1), lane 2: left (i, j-1)
+            const int di = lane == 2 ? 0 : 1;
+            const int dj = lane == 0 ? 0 : 1;
+            while (i > 0 && j > 0)
+            {
+                if (int64_t(bw) * (i + j - 2) < tb)
+                    refill(i + j);
+                const int v     = val(i - di, j - dj);
+                const int above = uni(__builtin_amdgcn_readlane(v, 0));
+                const int dg    = uni(__builtin_amdgcn_readlane(v, 1));
+                const int left  = uni(__builtin_amdgcn_readlane(v, 2));
+                int8_t r;
+                if (left + 1 == s)
+                {
+                    r = ins;
+                    s = left;
+                    --j;
+                }
+                else if (above + 1 == s)
+                {
+                    r = del;
+                    s = above;
+                    --i;
+                }
+                else
+                {
+                    r = dg == s ? kMatch : kMismatch;
+                    s = dg;
+                    --i;
+                    --j;
+                }
+                pw.put(r, lane);
+            }
+            pw.finish(lane);
+        }
         pw.fill(del, i, lane);
         pw.fill(ins, j, lane);
         if (lane == 0)
