@@ -3,7 +3,7 @@
 # and a link walk (parity, benches)
 cd "$(dirname "$0")/.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-OUT=gpurun_out/r5y
+OUT=gpurun_out/${TAG:-r5y}
 mkdir -p $OUT
 echo "[$(date +%T)] pytest ukkonen"
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
