@@ -1067,7 +1067,13 @@ __global__ void __launch_bounds__(kWave) ukkonen_kernel(Args a)
     GWAMD_LDS uint8_t* base = (GWAMD_LDS uint8_t*)(lds);
     GWAMD_LDS uint8_t* sA   = base + a.lds_target_off; // along i (the shorter sequence)
     GWAMD_LDS uint8_t* sB   = base + a.lds_seq2_off;   // along j
-    const int TE8           = ((a.tile_bytes / 2) - 8) & ~7; // tile range (int16 elements); + 7 for alignment
+    // tiles of 16 KiB and more (long pairs, one workgroup per CU) are filled
+    // by direct-to-LDS loads (global_load_lds_dwordx4: every piece in flight
+    // at once, no staging registers), whose last 64-lane chunk may write up
+    // to 1 KiB past the range: those tiles keep 1 KiB spare
+    const bool tdirect      = a.tile_bytes >= 16384;
+    const int TE8           = tdirect ? ((a.tile_bytes - 1024) / 2) & ~511
+                                      : ((a.tile_bytes / 2) - 8) & ~7; // tile range (int16 elements); + 7 for alignment
     GWAMD_LDS int16_t* tile = (GWAMD_LDS int16_t*)(base + a.lds_tile_off);
     int16_t* S              = reinterpret_cast<int16_t*>(a.ws + size_t(blockIdx.x) * size_t(a.ws_slot_bytes));
     const int p             = a.ukkonen_p;
@@ -1136,6 +1142,16 @@ __global__ void __launch_bounds__(kWave) ukkonen_kernel(Args a)
             const be_u32x4* src = reinterpret_cast<const be_u32x4*>(S + lo);
             GWAMD_LDS be_u32x4* dst = (GWAMD_LDS be_u32x4*)tile;
             wave_sync();
+            if (tdirect)
+            {
+                // lane r of chunk e0 writes piece e0 + r (lanes past the range
+                // reload its last piece into the spare kilobyte)
+                for (int e0 = 0; e0 < np16; e0 += kWave)
+                    __builtin_amdgcn_global_load_lds(src + min(e0 + lane, np16 - 1), (GWAMD_LDS void*)(dst + e0), 16, 0,
+                                                     0);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            else
             for (int e0 = 0; e0 < np16; e0 += 8 * kWave)
             {
                 be_u32x4 v[8];

@@ -761,8 +761,14 @@ private:
             const int64_t seqs  = lds_seq2_off_ + a16(stride_ + 16);
             uk_narrow_tile_off_ = int32_t(seqs);
             // ukkonen_kernel's backtrace tile (the narrow kernel's only use of
-            // it; any size is correct, reads outside it go to HBM)
+            // it; any size is correct, reads outside it go to HBM).  8 KiB keeps
+            // 8 workgroups per CU for short pairs; pairs of 32 kb and more
+            // (few per batch, one workgroup per CU already) take what the CU's
+            // LDS has left, up to 48 KiB, so the walk refills every ~100
+            // columns instead of every ~22 (one HBM latency each)
             int32_t uk_tile     = 8192;
+            if (stride_ >= 32768)
+                uk_tile = int32_t(std::max<int64_t>(8192, std::min<int64_t>(49152, (163840 - 64 - seqs) & ~int64_t(511))));
             if (const char* tb = gwamd::host::diag_env("GWAMD_UK_TILE_BYTES"))
             {
                 char* end    = nullptr;

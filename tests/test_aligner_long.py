@@ -216,3 +216,26 @@ def test_ukkonen_narrow_batch_keeps_single_wave_kernel():
     assert st["ukkonen_wide_pairs"] == 0
     for (q, tt), g in zip(pairs, got):
         assert g == oracle.align(q, tt, oracle.ALIGN_UKKONEN, mq)
+
+
+@pytest.mark.parametrize("tile", [None, "16384", "24576"])
+def test_ukkonen_long_pairs_large_tile(tile, monkeypatch):
+    # pairs of 32 kb and more take a backtrace tile of what the CU's LDS has
+    # left (up to 48 KiB) filled by direct-to-LDS loads, and the walk decides
+    # each 8 x 8 window's moves in parallel: narrow-band pairs of 3-40 kb
+    # (single-wave kernel) against the oracle, with the default and two
+    # forced tile sizes
+    if tile:
+        monkeypatch.setenv("GWAMD_UK_TILE_BYTES", tile)
+    else:
+        monkeypatch.delenv("GWAMD_UK_TILE_BYTES", raising=False)
+    rng = random.Random(17)
+    t = rand_seq(rng, 40000)
+    pairs = [(mutate(rng, t, 0.04)[:39950], t), (t[:39800], t), (mutate(rng, t[:3000], 0.1), t[:3100]),
+             (mutate(rng, t[:25000], 0.08), t[:25020]), (rand_seq(rng, 33000)[:32990], t[:33000])]
+    pairs = [(q, tt) for q, tt in pairs if abs(len(q) - len(tt)) <= 500]
+    st = {}
+    got, mq = gpu_states(pairs, "ukkonen", 40000, 40000, stats=st)
+    assert st["ukkonen_wide_pairs"] == 0
+    for (q, tt), g in zip(pairs, got):
+        assert g == oracle.align(q, tt, oracle.ALIGN_UKKONEN, mq), (len(q), len(tt))
