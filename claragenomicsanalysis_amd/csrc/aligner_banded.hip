@@ -763,11 +763,20 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
 
         // backtrace (myers_backtrace_banded, :377-494): the three neighbour
         // scores of a step are evaluated by lanes 0..2 (get_myers_score,
-        // :173-185) from an LDS tile of the band columns j-1..j
-        const int64_t total = int64_t(nwb) * (T + 1);
-        const bool use_tile = 2 * nwb <= TLE;
-        int64_t tb = 0, te = 0; // tile holds flat entries [tb, te)
-        auto refill = [&](int jcol) {
+        // :173-185) from an LDS tile of the band.  One-wave kernel (short
+        // pairs, many resident): whole columns j-1..j and below, a flat range
+        // of contiguous entries (coalesced refills), or HBM when two columns
+        // do not fit.  Multi-wave kernels (long pairs, few resident): KW words
+        // x KC columns around the walk (a step reads words (i - 2) / 32 ..
+        // i / 32 of columns j - 1 and j, and the word index changes once every
+        // 32 rows, so a few words over many columns last ~KC steps), refilled
+        // when the walk leaves it.  Words outside [0, nwb) (the flat index
+        // map aliases word nwb onto the next column) read HBM
+        constexpr bool kRect = NWV > 1;
+        const int64_t total  = int64_t(nwb) * (T + 1);
+        const bool use_tile  = !kRect && 2 * nwb <= TLE;
+        int64_t tb = 0, te = 0; // flat tile: entries [tb, te)
+        auto refill_flat = [&](int jcol) {
             const int64_t hi = min<int64_t>(total, int64_t(nwb) * (jcol + 1));
             const int64_t lo = max<int64_t>(0, hi - TLE);
             const int nr     = int(hi - lo);
@@ -796,36 +805,35 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
             tb = lo;
             te = hi;
         };
-        // bands too wide for two whole columns in the tile (multi-wave
-        // kernels: long queries): a 64-word x LT-column window of the band
-        // around the walk instead (lane r loads word w0 + r of each column,
-        // one coalesced 1 KiB load per column), refilled when the walk leaves
-        // it; words outside [0, nwb) (the flat index map aliases word nwb onto
-        // the next column) read HBM.  The one-wave kernel (short pairs, many
-        // resident) reads such steps from HBM: the window's registers would
-        // cost it resident waves
-        const int LT = NWV > 1 ? TLE / kWave : 0;
-        int w0 = INT_MIN / 2, j0 = INT_MIN / 2;
-        auto refill_win = [&](int wc, int jc) {
-            w0 = wc - kWave / 2;
-            j0 = jc - LT + 1;
-            const int w     = w0 + lane;
-            const bool w_ok = w >= 0 && w < nwb;
+        const int kwb = TLE >= 1024 ? 4 : 2; // rectangular tile: KW = 16 or 4 words
+        const int KW  = 1 << kwb;
+        const int KC  = TLE >> kwb;
+        int w0 = INT_MIN / 2, c0 = INT_MIN / 2;
+        auto refill = [&](int wc, int jc) {
+            w0          = wc - 1;
+            c0          = jc - KC + 1;
+            const int n = KW * KC;
             wave_sync();
-            for (int c0 = 0; c0 < LT; c0 += 8)
+            // 8 entries per lane in flight before the first LDS store waits
+            for (int e0 = 0; e0 < n; e0 += 8 * kWave)
             {
                 BandEntry v[8];
 #pragma unroll
                 for (int u = 0; u < 8; u++)
                 {
-                    const int col = j0 + c0 + u;
-                    if (w_ok && c0 + u < LT && col >= 0 && col <= T)
+                    const int e   = e0 + u * kWave + lane;
+                    const int w   = w0 + (e & (KW - 1));
+                    const int col = c0 + (e >> kwb);
+                    if (e < n && w >= 0 && w < nwb && col >= 0 && col <= T)
                         v[u] = glb_get(E + (int64_t(w) + int64_t(nwb) * col));
                 }
 #pragma unroll
                 for (int u = 0; u < 8; u++)
-                    if (c0 + u < LT)
-                        lds_put(reg + ((c0 + u) * kWave + lane), v[u]);
+                {
+                    const int e = e0 + u * kWave + lane;
+                    if (e < n)
+                        lds_put(reg + e, v[u]);
+                }
             }
             wave_sync();
         };
@@ -833,25 +841,21 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
         const int bl       = min(lane, 2);
         int i = bw, j = T;
         if (use_tile)
-            refill(j);
-        else if (LT >= 2)
-            refill_win(i / kWordBits, j);
+            refill_flat(j);
         // start from the band's last word: the reference reads word
         // band_width / 32 (:393), one past the band when band_width % 32 == 0
         int s = uni(glb_get(E + (int64_t((bw - 1) / kWordBits) + int64_t(nwb) * j)).sc);
         while (j > 0 && (i > 0 || j >= db))
         {
             const int phase = j >= de ? 3 : (j >= db ? 2 : 1);
-            if (use_tile && int64_t(nwb) * (j - 1) < tb)
-                refill(j);
-            else if (!use_tile && LT >= 2)
+            if constexpr (kRect)
             {
-                // lanes 0..2 read words (i - 2) / 32 .. (i + 1) / 32 of
-                // columns j - 1 and j
-                const int wc = i / kWordBits;
-                if (wc - 1 < w0 || wc + 1 >= w0 + kWave || j - 1 < j0 || j > j0 + LT - 1)
-                    refill_win(wc, j);
+                const int wc = (i - 1) / kWordBits;
+                if ((i - 2) / kWordBits < w0 || i / kWordBits >= w0 + KW || j - 1 < c0 || j > c0 + KC - 1)
+                    refill(wc, j);
             }
+            else if (use_tile && int64_t(nwb) * (j - 1) < tb)
+                refill_flat(j);
             // lane 0: above, lane 1: diagonal, lane 2: left
             int gi, gj, spv;
             bool special;
@@ -881,9 +885,9 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
             const int64_t o = int64_t(wi) + int64_t(nwb) * gj;
             const bool inr  = o >= 0 && o < total;
             BandEntry e{0u, 0u, 0, 0};
-            const unsigned ww = unsigned(wi - w0), cc = unsigned(gj - j0);
-            if (use_tile ? (o >= tb && o < te) : (inr && ww < unsigned(kWave) && cc < unsigned(LT) && wi < nwb))
-                e = use_tile ? lds_get(reg + (o - tb)) : lds_get(reg + (cc * kWave + ww));
+            const unsigned ww = unsigned(wi - w0), cc = unsigned(gj - c0);
+            if (kRect ? (inr && wi < nwb && ww < unsigned(KW) && cc < unsigned(KC)) : (o >= tb && o < te))
+                e = kRect ? lds_get(reg + ((cc << kwb) + ww)) : lds_get(reg + (o - tb));
             else if (inr)
                 e = glb_get(E + (o));
             uint32_t mask = shl_ptx(~1u, bi);
