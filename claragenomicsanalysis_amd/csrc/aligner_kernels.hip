@@ -1091,11 +1091,12 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
         pr[4] += uint64_t(T) * uint64_t((nw + kWave - 1) / kWave);
 #endif
         GWAMD_PROF_T0(t_bt);
-        // backtrace (myers_backtrace, myers_gpu.cu:181-245).  The walk reads
-        // words (i-2)/32, (i-1)/32 of columns j-1, j; a tile of kTbW words x
-        // kTbC columns ending at the current cell is staged in LDS with one
-        // round of lane-parallel loads and refilled when the walk leaves it
-        // (about every 64 steps), so a step costs LDS reads, not HBM latency.
+        // backtrace (myers_backtrace, myers_gpu.cu:181-245).  The walk's
+        // windows read words (i-9)/32 .. (i-1)/32 of columns j-8 .. j; a tile
+        // of kTbW words x kTbC columns ending at the current cell is staged in
+        // LDS with one round of lane-parallel loads and refilled when a window
+        // leaves it (about every 55 steps), so a step costs LDS reads, not HBM
+        // latency.
         const uint32_t last_mask = (Q % kWordBits) != 0 ? (1u << (Q % kWordBits)) - 1u : ~0u;
         GWAMD_LDS uint32_t* tpv  = (GWAMD_LDS uint32_t*)(base + a.lds_scratch_off);
         GWAMD_LDS uint32_t* tmv  = tpv + kTbW * kTbC;
@@ -1120,56 +1121,62 @@ __global__ void __launch_bounds__(kWave) myers_kernel(Args a)
             }
             wave_sync();
         };
-        auto gms = [&](int i, int j) -> int {
-            const int wi     = (i - 1) / kWordBits;
-            const int bi     = (i - 1) % kWordBits;
-            uint32_t mask    = (~1u) << bi;
-            if (wi == nw - 1)
-                mask &= last_mask;
-            const int e      = (j - tc0) * kTbW + (wi - tw0);
-            const uint32_t p = uniu(tpv[e]);
-            const uint32_t n = uniu(tmv[e]);
-            return uni(tsc[e]) - __builtin_popcount(mask & p) + __builtin_popcount(mask & n);
-        };
         int i = Q, j = T, pos = 0;
-        int s = Q > 0 ? uni(wsc[size_t(T) * nwp + (nw - 1)]) : 0;
-        int pbuf = 0; // 64 path states, one per lane, stored together
-        if (i > 0 && j > 0)
-            refill(i, j);
-        while (i > 0 && j > 0)
+        // the walk in 8 x 8 windows (as ukkonen_kernel): lane 8a + b takes
+        // cell (i0 - a, j0 - b), computes its value from the tile (row 0 is
+        // j) and, from its three neighbours (ds_bpermute), its move, which
+        // depends on the cell alone (its value is the walk's running score);
+        // the walk follows next-lane links until the window's last row or
+        // column, i = 0 or j = 0, and the visited lanes store their moves at
+        // their rank (a + b grows by 1 or 2 per step)
         {
-            if (j - 1 < tc0 || (i > 1 && (i - 2) / kWordBits < tw0))
+            const int wa = lane >> 3, wb = lane & 7;
+            if (i > 0 && j > 0)
                 refill(i, j);
-            const int above = i == 1 ? j : gms(i - 1, j);
-            const int diag  = i == 1 ? j - 1 : gms(i - 1, j - 1);
-            const int left  = gms(i, j - 1);
-            int8_t r;
-            if (left + 1 == s)
+            while (i > 0 && j > 0)
             {
-                r = kInsertion;
-                s = left;
-                --j;
+                if ((max(i - 9, 1) - 1) / kWordBits < tw0 || max(j - 8, 0) < tc0)
+                    refill(i, j);
+                const int ci = i - wa, cj = j - wb;
+                int v        = cj;
+                if (ci > 0)
+                {
+                    const int wi  = (ci - 1) / kWordBits;
+                    const int bi  = (ci - 1) % kWordBits;
+                    uint32_t mask = (~1u) << bi;
+                    if (wi == nw - 1)
+                        mask &= last_mask;
+                    const int e = min(max((cj - tc0) * kTbW + (wi - tw0), 0), kTbW * kTbC - 1);
+                    v           = tsc[e] - __builtin_popcount(mask & tpv[e]) + __builtin_popcount(mask & tmv[e]);
+                }
+                const int up      = __builtin_amdgcn_ds_bpermute(4 * (lane + 8), v);
+                const int dg      = __builtin_amdgcn_ds_bpermute(4 * (lane + 9), v);
+                const int lf      = __builtin_amdgcn_ds_bpermute(4 * (lane + 1), v);
+                const bool mv_ins = lf + 1 == v;
+                const bool mv_del = !mv_ins && up + 1 == v;
+                const int r       = mv_ins ? int(kInsertion) : (mv_del ? int(kDeletion) : (dg == v ? int(kMatch) : int(kMismatch)));
+                const bool term   = wa == 7 || wb == 7 || ci <= 0 || cj <= 0;
+                const int nxt     = term ? lane : lane + (mv_ins ? 1 : (mv_del ? 8 : 9));
+                uint64_t visited  = 0;
+                uint32_t sums     = 0;
+                int o = 0, steps = 0;
+                while (true)
+                {
+                    const int nx = uni(__builtin_amdgcn_readlane(nxt, o));
+                    if (nx == o)
+                        break;
+                    visited |= 1ull << o;
+                    sums |= 1u << ((o >> 3) + (o & 7));
+                    ++steps;
+                    o = nx;
+                }
+                if ((visited >> lane) & 1ull)
+                    path[pos + __builtin_popcount(sums & ((1u << (wa + wb)) - 1u))] = int8_t(r);
+                pos += steps;
+                i -= o >> 3;
+                j -= o & 7;
             }
-            else if (above + 1 == s)
-            {
-                r = kDeletion;
-                s = above;
-                --i;
-            }
-            else
-            {
-                r = diag == s ? kMatch : kMismatch;
-                s = diag;
-                --i;
-                --j;
-            }
-            pbuf = lane == (pos & (kWave - 1)) ? int(r) : pbuf;
-            if ((pos & (kWave - 1)) == kWave - 1)
-                path[pos - (kWave - 1) + lane] = int8_t(pbuf);
-            ++pos;
         }
-        if (lane < (pos & (kWave - 1)))
-            path[(pos & ~(kWave - 1)) + lane] = int8_t(pbuf);
         for (int k = lane; k < i; k += kWave)
             path[pos + k] = kDeletion;
         pos += i;
