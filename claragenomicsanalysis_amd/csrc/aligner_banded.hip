@@ -258,9 +258,12 @@ __device__ __forceinline__ void lds_barrier()
 
 // NWV waves per pair: wave 0 does everything; waves 1..NWV-1 join the sweeps of
 // bands of several chunks whose state fits LDS (2 * NWV target columns in
-// flight, see sweep_multi)
+// flight, see sweep_multi).  Compiled for 5 waves per SIMD (96 VGPRs, a few
+// bytes of scratch): with the window backtrace the one-wave kernel needs 100,
+// and 4 resident waves per SIMD instead of 5 cost D_banded 830k -> 751k
+// alignments/s
 template <int NWV>
-__global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
+__global__ void __launch_bounds__(kWave * NWV) __attribute__((amdgpu_waves_per_eu(5))) myers_banded_kernel(Args a)
 {
     extern __shared__ __align__(16) uint8_t lds[];
     __shared__ int ed_slot;
@@ -845,17 +848,93 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
         // start from the band's last word: the reference reads word
         // band_width / 32 (:393), one past the band when band_width % 32 == 0
         int s = uni(glb_get(E + (int64_t((bw - 1) / kWordBits) + int64_t(nwb) * j)).sc);
+        // score of band cell (gi, gj) (get_myers_score, :173-185) on this
+        // lane, without the callers' boundary cases: 0 outside the flat range
+        auto band_val = [&](int gi, int gj) -> int {
+            const int wi    = (gi - 1) / kWordBits;
+            const int bi    = (gi - 1) % kWordBits;
+            const int64_t o = int64_t(wi) + int64_t(nwb) * gj;
+            const bool inr  = o >= 0 && o < total;
+            BandEntry e{0u, 0u, 0, 0};
+            const unsigned ww = unsigned(wi - w0), cc = unsigned(gj - c0);
+            if (kRect ? (inr && wi < nwb && ww < unsigned(KW) && cc < unsigned(KC)) : (o >= tb && o < te))
+                e = kRect ? lds_get(reg + ((cc << kwb) + ww)) : lds_get(reg + (o - tb));
+            else if (inr)
+                e = glb_get(E + (o));
+            uint32_t mask = shl_ptx(~1u, bi);
+            if (wi == nwb - 1)
+                mask &= lem;
+            const int v = e.sc - __builtin_popcount(mask & e.pv) + __builtin_popcount(mask & e.mv);
+            return inr ? v : 0;
+        };
+        // Window walk.  A step's move depends on its cell (i, j) and the
+        // running score s; for cells with i >= 1 s is the cell's own score
+        // whichever neighbour the walk arrived from (the boundary cases of
+        // :173-185 only apply to rows <= 0), so lane 8(a + 4) + b takes cell
+        // (i0 + a, j0 - b), a in [-4, 3], computes its score, its three
+        // neighbours' (ds_bpermute, with the per-role boundary cases) and its
+        // move, and the walk follows next-lane links (one v_readlane per step,
+        // the step's rank kept in its lane) until a cell at the window's edge, a row
+        // <= 0 or the end of the loop; the visited lanes store their moves at
+        // their ranks.  Rows <= 0 take the per-step code below with the
+        // running score.  Tiles must hold the window (10 rows, 9 columns).
+        const bool win = kRect || (use_tile && TLE >= 10 * nwb);
+        const int wr = lane >> 3, wcl = lane & 7;
         while (j > 0 && (i > 0 || j >= db))
         {
-            const int phase = j >= de ? 3 : (j >= db ? 2 : 1);
             if constexpr (kRect)
             {
-                const int wc = (i - 1) / kWordBits;
-                if ((i - 2) / kWordBits < w0 || i / kWordBits >= w0 + KW || j - 1 < c0 || j > c0 + KC - 1)
-                    refill(wc, j);
+                if ((i - 6) / kWordBits < w0 || (i + 3) / kWordBits >= w0 + KW || j - 8 < c0 || j > c0 + KC - 1)
+                    refill((i - 1) / kWordBits, j);
             }
-            else if (use_tile && int64_t(nwb) * (j - 1) < tb)
+            else if (use_tile && int64_t(nwb) * max(j - (win ? 8 : 1), 0) < tb)
                 refill_flat(j);
+            if (win && i >= 1)
+            {
+                const int i0 = i, j0 = j;
+                const int r  = i0 + wr - 4, c = j0 - wcl;
+                const int ph = c >= de ? 3 : (c >= db ? 2 : 1);
+                const int v  = band_val(r, c);
+                const int la = lane - 8;                        // (r - 1, c)
+                const int ld = ph == 2 ? lane + 1 : lane - 7;   // (r, c - 1) / (r - 1, c - 1)
+                const int ll = ph == 2 ? lane + 9 : lane + 1;   // (r + 1, c - 1) / (r, c - 1)
+                const int va = __builtin_amdgcn_ds_bpermute(4 * (la & 63), v);
+                const int vd = __builtin_amdgcn_ds_bpermute(4 * (ld & 63), v);
+                const int vl = __builtin_amdgcn_ds_bpermute(4 * (ll & 63), v);
+                const int above = r <= 1 ? c : va;
+                const int dg    = (ph == 2 ? r <= 0 : r <= 1) ? c - 1 : vd;
+                const int left  = vl;
+                const bool mins = left + 1 == v;
+                const bool mdel = !mins && above + 1 == v;
+                const int mr    = mins ? int(kInsertion) : (mdel ? int(kDeletion) : (dg == v ? int(kMatch) : int(kMismatch)));
+                const int chosen = mins ? left : (mdel ? above : dg);
+                const bool term  = wr == 0 || wr == 7 || wcl == 7 || r <= 0 || !(c > 0 && (r > 0 || c >= db));
+                const int nxt    = term ? lane : (mins ? ll : (mdel ? la : ld));
+                uint64_t visited = 0;
+                int rank = 0, o = 32, last = 32, steps = 0;
+                while (true)
+                {
+                    const int nx = uni(__builtin_amdgcn_readlane(nxt, o));
+                    if (nx == o)
+                        break;
+                    rank = lane == o ? steps : rank;
+                    visited |= 1ull << o;
+                    last = o;
+                    ++steps;
+                    o = nx;
+                }
+                if (((visited >> lane) & 1ull) && pw.pos + rank < pw.cap)
+                    pw.path[pw.pos + rank] = int8_t(mr);
+                pw.pos += steps;
+                if (steps > 0)
+                {
+                    s = uni(__builtin_amdgcn_readlane(chosen, last));
+                    i = i0 + (o >> 3) - 4;
+                    j = j0 - (o & 7);
+                    continue;
+                }
+            }
+            const int phase = j >= de ? 3 : (j >= db ? 2 : 1);
             // lane 0: above, lane 1: diagonal, lane 2: left
             int gi, gj, spv;
             bool special;
@@ -880,21 +959,7 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
                 special = false;
                 spv     = 0;
             }
-            const int wi    = (gi - 1) / kWordBits;
-            const int bi    = (gi - 1) % kWordBits;
-            const int64_t o = int64_t(wi) + int64_t(nwb) * gj;
-            const bool inr  = o >= 0 && o < total;
-            BandEntry e{0u, 0u, 0, 0};
-            const unsigned ww = unsigned(wi - w0), cc = unsigned(gj - c0);
-            if (kRect ? (inr && wi < nwb && ww < unsigned(KW) && cc < unsigned(KC)) : (o >= tb && o < te))
-                e = kRect ? lds_get(reg + ((cc << kwb) + ww)) : lds_get(reg + (o - tb));
-            else if (inr)
-                e = glb_get(E + (o));
-            uint32_t mask = shl_ptx(~1u, bi);
-            if (wi == nwb - 1)
-                mask &= lem;
-            int v = e.sc - __builtin_popcount(mask & e.pv) + __builtin_popcount(mask & e.mv);
-            v     = special ? spv : (inr ? v : 0);
+            const int v     = special ? spv : band_val(gi, gj);
             const int above = uni(__builtin_amdgcn_readlane(v, 0));
             const int dg    = uni(__builtin_amdgcn_readlane(v, 1));
             const int left  = uni(__builtin_amdgcn_readlane(v, 2));
@@ -921,9 +986,11 @@ __global__ void __launch_bounds__(kWave * NWV) myers_banded_kernel(Args a)
                     --i;
                 --j;
             }
-            pw.put(r, lane);
+            if (lane == 0 && pw.pos < pw.cap)
+                pw.path[pw.pos] = r;
+            pw.pos++;
         }
-        pw.finish(lane);
+        pw.overflow = pw.overflow || pw.pos > pw.cap;
         pw.fill(kDeletion, max(i, 0), lane);
         pw.fill(kInsertion, max(j, 0), lane);
         if (lane == 0)
