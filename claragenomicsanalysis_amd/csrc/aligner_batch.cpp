@@ -761,12 +761,15 @@ private:
             const int64_t seqs  = lds_seq2_off_ + a16(stride_ + 16);
             uk_narrow_tile_off_ = int32_t(seqs);
             // ukkonen_kernel's backtrace tile (the narrow kernel's only use of
-            // it; any size is correct, reads outside it go to HBM).  8 KiB keeps
-            // 8 workgroups per CU for short pairs; pairs of 32 kb and more
-            // (few per batch, one workgroup per CU already) take what the CU's
-            // LDS has left, up to 48 KiB, so the walk refills every ~100
-            // columns instead of every ~22 (one HBM latency each)
-            int32_t uk_tile     = 8192;
+            // it; any size is correct, reads outside it go to HBM).  Pairs up
+            // to 8 kb: 5 KiB, 10 workgroups per CU at 5 kb (8 KiB: 8; measured
+            // 653-658k against 611k alignments/s on D_ukkonen, profiles/
+            // r5an_bench); up to 32 kb: 8 KiB, which keeps the window walk
+            // for bands up to 255 rows; pairs of 32 kb and more (few per
+            // batch, one workgroup per CU already) take what the CU's LDS has
+            // left, up to 48 KiB, so the walk refills every ~100 columns
+            // instead of every ~22 (one HBM latency each)
+            int32_t uk_tile     = stride_ <= 8192 ? 5120 : 8192;
             if (stride_ >= 32768)
                 uk_tile = int32_t(std::max<int64_t>(8192, std::min<int64_t>(49152, (163840 - 64 - seqs) & ~int64_t(511))));
             if (const char* tb = gwamd::host::diag_env("GWAMD_UK_TILE_BYTES"))
