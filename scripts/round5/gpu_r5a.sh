@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: new parity tests (weights, marked rows, wide Ukkonen 3-4 rows per
 # thread, aligner stats), then config E with 2 pinned CPUs against unpinned
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5a
 mkdir -p $OUT

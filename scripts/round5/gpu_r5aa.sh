@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: SQ counters of ukkonen_kernel on D_ukkonen_64k, whole kernel and
 # forward sweep alone (no-backtrace build), to split instructions and cycles
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5aa
 mkdir -p $OUT

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5: Ukkonen large-tile long-pair parity
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5ac
 mkdir -p $OUT

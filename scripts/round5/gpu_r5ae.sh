@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5: banded Myers backtrace over a words x columns tile (parity, benches)
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/${TAG:-r5ae}
 mkdir -p $OUT

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5: D_banded backtrace tile size (LDS bytes) sweep
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5ag
 mkdir -p $OUT

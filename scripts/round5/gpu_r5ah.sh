@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5: full Myers phase counters (score matrix / backtrace cycles)
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/${TAG:-r5ah}
 mkdir -p $OUT

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5: full Myers backtrace in 8 x 8 windows (parity, bench, phase counters)
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5ai
 mkdir -p $OUT

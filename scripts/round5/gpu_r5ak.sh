@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: banded Myers backtrace window walk (parity, benches; 4 vs 5 waves
 # per SIMD build)
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/${TAG:-r5ak}
 mkdir -p $OUT

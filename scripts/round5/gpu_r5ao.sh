@@ -1,14 +1,14 @@
 #!/bin/bash
-# round 5: non-ASCII graph bases compared whole on the LDS kernel passes
-cd "$(dirname "$0")/.." || exit 1
+# round 5: Ukkonen default tile by length (parity, benches)
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-OUT=gpurun_out/r5w
+OUT=gpurun_out/r5ao
 mkdir -p $OUT
-echo "[$(date +%T)] pytest poa"
+echo "[$(date +%T)] pytest ukkonen"
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
-  tests/test_poa_gpu.py tests/test_poa_weights.py > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+  tests/test_aligner_gpu.py tests/test_aligner_long.py -k "ukkonen or Ukkonen" > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
 tail -2 $OUT/pytest.log
-for C in B F_int32_4k; do
+for C in D_ukkonen D_ukkonen_wide_16k D_ukkonen_64k; do
   echo "[$(date +%T)] bench $C"
   timeout -k 10 300 python bench.py --config $C --steps 3 --warmup 1 --no-cpu > $OUT/bench_$C.log 2>&1 || { tail -20 $OUT/bench_$C.log; exit 1; }
 done

@@ -2,7 +2,7 @@
 # round 5: band kernel at every band width up to 1,024 (parity + bench lines),
 # then refresh the C / D / E evidence the bench lines cite (kernel stats, HBM
 # passes and SQ counters of the current kernels)
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5b
 mkdir -p $OUT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: the LDS kernel's 32-bit pass (parity at every shape, weights,
 # persistent grid) and the F_int32_4k bench line
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5c
 mkdir -p $OUT

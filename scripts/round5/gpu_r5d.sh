@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: batched backtrace tile refills (banded Myers, Ukkonen): aligner
 # parity, the banded / Ukkonen bench lines, and config D's step breakdown
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5d
 mkdir -p $OUT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: config D with the pipelined align_all (and one-stage for A/B),
 # config C without the anti-diagonal pass's code stores (timing experiment)
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5e
 mkdir -p $OUT

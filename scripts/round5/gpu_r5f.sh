@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5 timing experiment on config C's anti-diagonal pass: ring loads
 # prefetched two steps ahead (exp2), and that without code stores (exp3)
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5f
 mkdir -p $OUT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: K-stage pipelined align_all (copy-in / copy-out streams): aligner
 # parity, then config D and the D_* lines
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5g
 mkdir -p $OUT

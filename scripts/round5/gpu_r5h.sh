@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: the LDS kernel's forward pass without the per-row vmcnt(0) wait
 # (ring mask and list pointer out of the flat RowProg): POA parity, then B, E, F
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5h
 mkdir -p $OUT

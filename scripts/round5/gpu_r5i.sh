@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: anti-diagonal pass with the next step's LDS loads issued at the
 # top of each step: banded parity, then C and B_banded
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5i
 mkdir -p $OUT

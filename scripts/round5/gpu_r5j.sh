@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: where D_ukkonen_64k's time goes (forward sweep alone vs the whole
 # kernel) and its SQ counters
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5j
 mkdir -p $OUT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: Ukkonen sweep specialised per live chunk count (parity + benches),
 # racon DFS list loads (MSA / SPOA_ACCURATE parity + C)
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5k
 mkdir -p $OUT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: Ukkonen backtrace walking 8 x 8 register windows, sweep bytes read
 # one column pair ahead (parity, benches)
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/${TAG:-r5q}
 mkdir -p $OUT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: band kernel past 512 with a 32-row traceback tile (8-row ring at
 # 1,024): four windows per CU (parity, benches)
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/${TAG:-r5s}
 mkdir -p $OUT

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5: config B with 3 and 4 waves per window (LDS kernel shapes)
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5u
 mkdir -p $OUT

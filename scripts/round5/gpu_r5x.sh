@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: Ukkonen forward sweep alone (no backtrace build) against the whole
 # kernel, D_ukkonen and D_ukkonen_64k
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 OUT=gpurun_out/r5x
 mkdir -p $OUT
