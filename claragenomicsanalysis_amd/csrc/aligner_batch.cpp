@@ -573,8 +573,19 @@ public:
                 a.tile_bytes   = gwamd::aln::kUkTileRows * gwamd::aln::kUkTileCols * 2;
             }
         }
+        if (algo_ == GWAMD_ALIGNER_MYERS_BANDED && band_waves_ > 1 && !band_waves_forced_)
+        {
+            // an aligner planned for long queries (8 waves per pair) runs a
+            // launch whose queries are all short with one wave per pair:
+            // their bands fit one 32-word chunk, which only wave 0 sweeps
+            int32_t mq = 0;
+            for (int32_t k = i0; k < i0 + count; k++)
+                mq = std::max(mq, h_lens_.as<int32_t>()[2 * size_t(k)]);
+            if (mq <= kLongBandQuery)
+                a.band_waves = 1;
+        }
         const int grid     = std::min<int>(count, nslots);
-        const int ks       = spec_sweeps(count, nslots);
+        const int ks       = spec_sweeps(count, nslots, a.band_waves);
         if (ks > 0)
         {
             // band doubling run ahead: every (pair, sweep) on its own
@@ -595,11 +606,11 @@ public:
     // pairs: every pair on its own slot, all (pair, sweep) items resident) and
     // every band's chunk state fits LDS; 0 = the plain loop.
     // GWAMD_BAND_SPEC=k forces k (0..kMaxSpecSweeps, diagnostic)
-    int spec_sweeps(int32_t count, int32_t nslots) const
+    int spec_sweeps(int32_t count, int32_t nslots, int32_t waves) const
     {
         if (algo_ != GWAMD_ALIGNER_MYERS_BANDED || count <= 0)
             return 0;
-        int k = band_waves_ > 1 ? kDefaultSpecSweeps : 0;
+        int k = waves > 1 ? kDefaultSpecSweeps : 0;
         if (const char* e = gwamd::host::diag_env("GWAMD_BAND_SPEC"))
         {
             k = std::atoi(e);
@@ -733,13 +744,14 @@ private:
             // long queries (bands of many 32-word chunks) run 8 waves per pair,
             // 16 target columns in flight; short ones keep one wave per pair
             // and their occupancy
-            band_waves_ = max_q_ > 8192 ? 8 : 1;
+            band_waves_ = max_q_ > kLongBandQuery ? 8 : 1;
             if (const char* bwv = gwamd::host::diag_env("GWAMD_BAND_WAVES"))
             {
                 const std::string v(bwv);
                 if (v != "1" && v != "4" && v != "8" && v != "16")
                     throw std::invalid_argument("GWAMD_BAND_WAVES must be 1, 4, 8 or 16");
-                band_waves_ = std::stoi(v);
+                band_waves_        = std::stoi(v);
+                band_waves_forced_ = true;
             }
             lds_bytes_       = lds_tile_off_ + tile_bytes_;
             // band entries (pv, mv, score, pad) of the widest band (the whole query)
@@ -963,6 +975,8 @@ private:
     // download-done events and the kernel's start / stop events; stages_ of
     // the last align_all() (0: none yet) and their first pairs
     static constexpr int kMaxStages = 8;
+    static constexpr int kLongBandQuery     = 8192; // banded Myers: longer queries run 8 waves per pair
+    bool band_waves_forced_                 = false; // GWAMD_BAND_WAVES (diagnostic)
     static constexpr int kMaxSpecSweeps     = 8; // banded Myers sweeps run ahead, at most
     static constexpr int kDefaultSpecSweeps = 5; // est x 1 .. x 16
     hipStream_t stream2_ = nullptr, s_in_ = nullptr, s_out_ = nullptr;

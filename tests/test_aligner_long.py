@@ -239,3 +239,16 @@ def test_ukkonen_long_pairs_large_tile(tile, monkeypatch):
     assert st["ukkonen_wide_pairs"] == 0
     for (q, tt), g in zip(pairs, got):
         assert g == oracle.align(q, tt, oracle.ALIGN_UKKONEN, mq), (len(q), len(tt))
+
+
+def test_myers_banded_short_launch_on_long_aligner(monkeypatch):
+    # an aligner planned for long queries (8 waves per pair) whose batch holds
+    # only queries up to 8,192 bases runs that launch with one wave per pair
+    # (ADVICE: band waves per launch); same paths as the oracle
+    monkeypatch.delenv("GWAMD_BAND_WAVES", raising=False)
+    rng = random.Random(53)
+    t = rand_seq(rng, 8000)
+    pairs = [(mutate(rng, t, 0.1), t), (mutate(rng, t[:5000], 0.2), t[:5000]), (mutate(rng, t[:300], 0.05), t[:320])]
+    got, mq = gpu_states(pairs, "myers_banded", 12000, 12000)
+    for (q, tt), g in zip(pairs, got):
+        assert g == oracle.align(q, tt, oracle.ALIGN_MYERS_BANDED, mq), (len(q), len(tt))
