@@ -1266,6 +1266,13 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
                 return qinfo[uint32_t(qq) & qmask];
             return info[int(queue[qq])];
         };
+        // all queued words (kMode 1): entry q + 1 <= n is always in bounds, so
+        // it is read without testing whether it is queued yet
+        auto next_info = [&](int qq, int tl) -> uint32_t {
+            if (kMode == 1)
+                return qinfo[qq];
+            return qq < tl ? pop_info(qq, tl) : 0u;
+        };
         int tail       = uniform(k);
         int q          = 0;
         uint32_t vinfo = tail > 0 ? uint32_t(uniform(int(info[int(queue[0])]))) : 0u;
@@ -1282,7 +1289,7 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
             // issued together with this pop's successor read.  Otherwise the
             // next node is the first one this pop releases.
             const bool have_next = q + 1 < tail;
-            uint32_t nxt         = have_next ? pop_info(q + 1, tail) : 0u;
+            uint32_t nxt         = next_info(q + 1, tail);
             if (deg <= 1)
             {
                 // no or one successor, without branches: a sink decrements the
@@ -1307,17 +1314,20 @@ __device__ __forceinline__ bool topsort_lds(WinGraph<SizeT> g, int n, GWAMD_LDS 
                 // all successors at once, one per lane: children are distinct,
                 // so the decrements are independent; ready ones are queued in
                 // successor-slot order (cudapoa_topsort.cuh:72-83)
+                // (lanes past the count repeat the last successor: they read
+                // and store the same word as its lane, with the exec mask left
+                // whole)
                 const int off     = int(vinfo & 0xffffu);
                 const bool act    = lane < deg;
-                const int o       = act ? int(edges[off + lane]) : 0;
-                const uint32_t oi = act ? info[o] - (1u << 24) : 0xffffffffu;
-                if (act)
-                    info[o] = oi;
+                const int o       = int(edges[off + min(lane, deg - 1)]);
+                const uint32_t oi = info[o] - (1u << 24);
+                info[o]           = oi;
                 const bool rdy       = act && (oi >> 24) == 0u;
                 const uint64_t ready = __builtin_amdgcn_ballot_w64(rdy);
                 if (ready)
                 {
-                    const int before = __popcll(ready & ((uint64_t(1) << lane) - 1));
+                    const int before = int(__builtin_amdgcn_mbcnt_hi(
+                        uint32_t(ready >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(ready), 0u)));
                     if (rdy)
                     {
                         queue[tail + before] = uint16_t(o);
