@@ -1336,7 +1336,8 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
     __shared__ int sh_status;
     __shared__ int sh_len;
     __shared__ AdShared ad_sh;
-    __shared__ int sh_job[4]; // window, V, L, gradient bits
+    __shared__ int sh_job[5]; // window, V, L, gradient bits, job kind (0 forward pass, 1 topological sort:
+                              // window, node count, hint count, previous node count)
 
     __shared__ int sh_next;
     if (int(blockIdx.x) >= b.num_windows)
@@ -1369,6 +1370,15 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
             BandAux X;
             ScoreT* spill;
             band_window_ptrs<ScoreT, SizeT>(b, d, w, slot, rowsz, g, X, spill);
+            if (sh_job[4] == 1)
+            {
+                // the level-keyed Kahn sort of this read (every wave)
+                topsort_levels<SizeT>(g, sh_job[1], sh_job[3], (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off,
+                                      int(threadIdx.x), int(blockDim.x),
+                                      static_cast<SizeT*>(b.cpred) + slot * size_t(d.max_nodes) * 4, sh_job[2]);
+                __syncthreads(); // pass done
+                continue;
+            }
             Band B;
             B.bw         = d.band_width;
             B.stride     = d.band_width + kBandPad;
@@ -1401,13 +1411,14 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
 
     PhaseTimer ph;
     BandProf bp;
-    uint64_t tsprof[4] = {0, 0, 0, 0}; // topsort sections (GWAMD_TOPSORT_PROFILE builds)
+    uint64_t tsprof[8] = {0, 0, 0, 0, 0, 0, 0, 0}; // topsort sections (GWAMD_TOPSORT_PROFILE builds)
     uint64_t addprof[8] = {0, 0, 0, 0, 0, 0, 0, 0}; // add sections (GWAMD_ADD_PROFILE builds)
     const WindowDesc wd = b.windows[w];
     const int nseq      = wd.num_seqs;
     int status          = kSuccess;
     int64_t cells       = 0;
     int node_count      = 0;
+    int lv_hint         = 0; // nodes whose critical predecessor of the last level sort is in cpred
 
     if (nseq > 0)
     {
@@ -1458,6 +1469,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
                         sh_job[1] = V;
                         sh_job[2] = L;
                         sh_job[3] = __float_as_int(B.gradient);
+                        sh_job[4] = 0;
                     }
                     __syncthreads(); // pass posted
                 }
@@ -1530,7 +1542,37 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
             ph.lap<kPhAdd>();
             rc = uniform(rc); // wave-uniform: the sort below runs scalar control flow
             nc = uniform(nc);
-            if (rc == kSuccess)
+            bool lv_done = false;
+            if (rc == kSuccess && !d.spoa_accurate && !(d.diag & 4))
+            {
+                // level-keyed Kahn sort on every wave of the workgroup
+                // (GWAMD_TOPSORT=fifo, Dims::diag bit 2, keeps the FIFO below)
+                if (nw > 1)
+                {
+                    if (lane == 0)
+                    {
+                        sh_job[0] = w;
+                        sh_job[1] = nc;
+                        sh_job[2] = lv_hint;
+                        sh_job[3] = V;
+                        sh_job[4] = 1;
+                    }
+                    __syncthreads(); // pass posted
+                }
+                lv_done = topsort_levels<SizeT>(g, nc, V, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, int(threadIdx.x),
+                                                int(blockDim.x), cpred, lv_hint,
+#ifdef GWAMD_TOPSORT_PROFILE
+                                                tsprof
+#else
+                                                nullptr
+#endif
+                );
+                if (nw > 1)
+                    __syncthreads(); // pass done
+                lv_done = uniform(lv_done ? 1 : 0) != 0;
+            }
+            lv_hint = lv_done ? nc : 0; // cpred holds c(v) of this sort for the next one
+            if (rc == kSuccess && !lv_done)
             {
                 if (d.spoa_accurate)
                     rc = topsort_racon_wave<SizeT>(g, nc, cscore, cpred, 4 * d.max_nodes, lane,
@@ -1582,10 +1624,13 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
             b.phase[size_t(w) * kPhases + kPhRowProg]  = int64_t(oprof[2]);
 #endif
 #ifdef GWAMD_TOPSORT_PROFILE
-            b.phase[size_t(w) * kPhases + kPhBackbone] = int64_t(tsprof[0] / 1000);
-            b.phase[size_t(w) * kPhases + kPhAdd]      = int64_t(tsprof[1] / 1000);
-            b.phase[size_t(w) * kPhases + kPhOutput]   = int64_t(tsprof[2] / 1000);
-            b.phase[size_t(w) * kPhases + kPhRowProg]  = int64_t(tsprof[3]);
+            // level sort sections (s_memtime cycles / 1000 in every phase slot,
+            // in order: init, reset, in-order pass, anchor rounds, final pass +
+            // checks, counting sort + slots, runs + outputs; the total slot
+            // holds the anchor count)
+            for (int k = 0; k < 7; k++)
+                b.phase[size_t(w) * kPhases + k] = int64_t(tsprof[k] / 1000);
+            b.phase[size_t(w) * kPhases + kPhTotal] = int64_t(tsprof[7] / 1000);
 #endif
 #ifdef GWAMD_BAND_PROFILE
             // counters over the phase slots (read raw: value = phase_ms * 1e5)

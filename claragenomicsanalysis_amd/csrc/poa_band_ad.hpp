@@ -413,8 +413,17 @@ __device__ __forceinline__ void band_ad_init(GWAMD_LDS ScoreT* ring, int rowsz, 
 // predecessors (bitmap in LDS; in-block predecessors are assumed real and the
 // assumption checked: if a lane fails, a fixed point over the block decides)
 // and published before the block's first progress word.
+// The pass is out of line: its register allocation is its own, so the rest of
+// the band kernel (the level sort's call, the serial phases) cannot push its
+// step loop into SGPR spills (config C forward 77.6 -> 65.7 ms per window,
+// round 6, gpurun_out/r6b).  GWAMD_BAND_AD_INLINE builds keep it inline.
+#ifdef GWAMD_BAND_AD_INLINE
+#define GWAMD_BAND_AD_ATTR __forceinline__
+#else
+#define GWAMD_BAND_AD_ATTR __noinline__
+#endif
 template <typename ScoreT, typename SizeT, int CPL>
-__device__ __forceinline__ void band_forward_ad(WinGraph<SizeT> g, BandAux X, int V, GWAMD_LDS const uint8_t* read,
+__device__ GWAMD_BAND_AD_ATTR void band_forward_ad(WinGraph<SizeT> g, BandAux X, int V, GWAMD_LDS const uint8_t* read,
                                                 int L, const Band& B, const Scores sc, GWAMD_LDS ScoreT* ring,
                                                 ScoreT* spill, int rowsz, int score_rows, int lane, int wave, int nw,
                                                 GWAMD_LDS AdShared* sh, BandProf& bp)

@@ -739,12 +739,16 @@ public:
     }
     // Dims::diag: bit 0 forces the Kahn sort's ring of queued words
     // (GWAMD_TOPSORT_RING=1, ring-mode parity tests); bit 1 keeps the LDS
-    // kernel on the round-3 forward pass (GWAMD_POA_FWD=v1, A/B runs)
+    // kernel on the round-3 forward pass (GWAMD_POA_FWD=v1, A/B runs); bit 2
+    // keeps the LDS and banded kernels on the FIFO Kahn sort instead of the
+    // level-keyed one (GWAMD_TOPSORT=fifo, cross-check tests and A/B runs)
     static int diag_bits()
     {
         const char* r = gwamd::host::diag_env("GWAMD_TOPSORT_RING");
         const char* f = gwamd::host::diag_env("GWAMD_POA_FWD");
-        return ((r && std::atoi(r) != 0) ? 1 : 0) | ((f && std::string(f) == "v1") ? 2 : 0);
+        const char* t = gwamd::host::diag_env("GWAMD_TOPSORT");
+        return ((r && std::atoi(r) != 0) ? 1 : 0) | ((f && std::string(f) == "v1") ? 2 : 0) |
+               ((t && std::string(t) == "fifo") ? 4 : 0);
     }
     static int tb_walk_bits()
     {

@@ -1172,9 +1172,13 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
 // pass and the traceback tile loads use every wave; the serial phases (graph
 // update, topological sort, consensus, MSA) run on wave 0 while the other
 // waves wait at the next barrier.  W: 32-bit scores (nw_forward_lds_w, the
-// reference's use32bitScore batches), else 16-bit.
+// reference's use32bitScore batches), else 16-bit.  Two waves per window
+// (config B: four windows per CU, two waves per SIMD) are held to 256
+// registers (HIP's second launch bound is the waves per SIMD), so the
+// allocation of the rest of the kernel cannot push it to one wave per SIMD
+// (half the windows resident).
 template <bool MSA, int CPL, int NW, bool W>
-__global__ void __launch_bounds__(kWave * NW, W ? (NW >= 8 ? 2 : 1) : (NW >= 4 ? 4 : 1))
+__global__ void __launch_bounds__(kWave * NW, W ? (NW >= 8 ? 2 : 1) : (NW >= 4 ? 4 : (NW == 2 ? 2 : 1)))
     poa_window_kernel_lds(Buffers b, Dims d, Scores sc)
 {
     using SizeT  = int16_t;
@@ -1255,6 +1259,7 @@ __global__ void __launch_bounds__(kWave * NW, W ? (NW >= 8 ? 2 : 1) : (NW >= 4 ?
     int status          = kSuccess;
     int64_t cells       = 0;
     int node_count      = 0;
+    int lv_hint         = 0; // nodes whose critical predecessor of the last level sort is in cpred
 
     if (nseq > 0)
     {
@@ -1345,7 +1350,26 @@ __global__ void __launch_bounds__(kWave * NW, W ? (NW >= 8 ? 2 : 1) : (NW >= 4 ?
                     nc = sh_len;
                 }
                 ph.lap<kPhAdd>();
-                if (rc == kSuccess)
+                if (lane == 0)
+                {
+                    sh_status = rc;
+                    sh_len    = nc;
+                }
+            }
+            __syncthreads();
+            int rc       = uniform(sh_status);
+            int nc       = uniform(sh_len);
+            bool lv_done = false;
+            __syncthreads(); // sh_* are rewritten below
+            // level-keyed Kahn sort on every wave of the workgroup
+            // (GWAMD_TOPSORT=fifo, Dims::diag bit 2, keeps the FIFO below)
+            if (rc == kSuccess && !d.spoa_accurate && !(d.diag & 4))
+                lv_done = topsort_levels<SizeT>(g, nc, V, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, tid, kThr, cpred,
+                                                lv_hint);
+            lv_hint = lv_done ? nc : 0; // cpred holds c(v) of this sort for the next one
+            if (wave == 0)
+            {
+                if (rc == kSuccess && !lv_done)
                 {
                     if (d.spoa_accurate)
                         rc = topsort_racon_wave<SizeT>(g, nc, cscore, cpred, 4 * d.max_nodes, lane,
@@ -1420,8 +1444,123 @@ __global__ void __launch_bounds__(kWave * NW, W ? (NW >= 8 ? 2 : 1) : (NW >= 4 ?
     }
 }
 
+// Test hook: the level-keyed Kahn sort (topsort_levels) of one graph by one
+// workgroup, for the known-answer and random-DAG tests against the FIFO sort.
+template <typename SizeT>
+__global__ void __launch_bounds__(1024) topsort_levels_test_kernel(WinGraph<SizeT> g, int n, int n_prev, int scratch,
+                                                                   SizeT* hint, int n_hint, int* ok)
+{
+    extern __shared__ __align__(16) uint8_t lds[];
+    const bool r = topsort_levels<SizeT>(g, n, n_prev, (GWAMD_LDS uint8_t*)(lds), scratch, int(threadIdx.x),
+                                         int(blockDim.x), hint, n_hint);
+    if (threadIdx.x == 0)
+        *ok = r ? 1 : 0;
+}
+
+template <typename SizeT>
+int topsort_levels_test(int n, int n_prev, int n_hint, const uint16_t* in_cnt, const int32_t* in_e,
+                        const uint16_t* out_cnt, const int32_t* out_e, int32_t* hint, const int32_t* order_prev,
+                        int threads, int scratch, int32_t* sorted)
+{
+    const size_t ne = size_t(n) * kMaxEdges;
+    std::vector<SizeT> ie(ne), oe(ne), hi(n, SizeT(0));
+    for (size_t i = 0; i < ne; i++)
+    {
+        ie[i] = SizeT(in_e[i]);
+        oe[i] = SizeT(out_e[i]);
+    }
+    for (int v = 0; hint && v < n; v++)
+        hi[v] = SizeT(hint[v]);
+    uint16_t *d_ic = nullptr, *d_oc = nullptr;
+    SizeT *d_ie = nullptr, *d_oe = nullptr, *d_sorted = nullptr, *d_pos = nullptr, *d_hint = nullptr;
+    int* d_ok   = nullptr;
+    int ok      = 0;
+    auto fin    = [&](int r) {
+        (void)hipFree(d_ic);
+        (void)hipFree(d_oc);
+        (void)hipFree(d_ie);
+        (void)hipFree(d_oe);
+        (void)hipFree(d_sorted);
+        (void)hipFree(d_pos);
+        (void)hipFree(d_hint);
+        (void)hipFree(d_ok);
+        return r;
+    };
+    if (n <= 0 || threads < 64 || threads > 1024 || threads % 64 || scratch < 0 || scratch > 163840 ||
+        (n_hint > 0 && !hint) || n_prev < 0 || n_prev > n || (n_prev > 0 && !order_prev))
+        return -2;
+    // the previous order: a permutation of the first n_prev nodes
+    std::vector<SizeT> so(n, SizeT(0));
+    {
+        std::vector<char> seen(n_prev, 0);
+        for (int q = 0; q < n_prev; q++)
+        {
+            const int v = order_prev[q];
+            if (v < 0 || v >= n_prev || seen[v])
+                return -2;
+            seen[v] = 1;
+            so[q]   = SizeT(v);
+        }
+    }
+    if (hipMalloc(&d_ic, n * 2) || hipMalloc(&d_oc, n * 2) || hipMalloc(&d_ie, ne * sizeof(SizeT)) ||
+        hipMalloc(&d_oe, ne * sizeof(SizeT)) || hipMalloc(&d_sorted, n * sizeof(SizeT)) ||
+        hipMalloc(&d_pos, n * sizeof(SizeT)) || hipMalloc(&d_hint, n * sizeof(SizeT)) ||
+        hipMalloc(&d_ok, sizeof(int)))
+        return fin(-1);
+    if (hipMemcpy(d_ic, in_cnt, n * 2, hipMemcpyHostToDevice) || hipMemcpy(d_oc, out_cnt, n * 2, hipMemcpyHostToDevice) ||
+        hipMemcpy(d_ie, ie.data(), ne * sizeof(SizeT), hipMemcpyHostToDevice) ||
+        hipMemcpy(d_oe, oe.data(), ne * sizeof(SizeT), hipMemcpyHostToDevice) ||
+        hipMemcpy(d_hint, hi.data(), n * sizeof(SizeT), hipMemcpyHostToDevice) ||
+        hipMemcpy(d_sorted, so.data(), n * sizeof(SizeT), hipMemcpyHostToDevice))
+        return fin(-1);
+    WinGraph<SizeT> g{};
+    g.in_cnt    = d_ic;
+    g.out_cnt   = d_oc;
+    g.in_e      = d_ie;
+    g.out_e     = d_oe;
+    g.sorted    = d_sorted;
+    g.pos       = d_pos;
+    g.max_nodes = n;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&topsort_levels_test_kernel<SizeT>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, scratch))
+        return fin(-1);
+    hipLaunchKernelGGL(topsort_levels_test_kernel<SizeT>, dim3(1), dim3(threads), size_t(scratch), 0, g, n, n_prev,
+                       scratch, d_hint, n_hint, d_ok);
+    if (hipGetLastError() || hipDeviceSynchronize() || hipMemcpy(&ok, d_ok, sizeof(int), hipMemcpyDeviceToHost))
+        return fin(-1);
+    std::vector<SizeT> s(n);
+    if (hipMemcpy(s.data(), d_sorted, n * sizeof(SizeT), hipMemcpyDeviceToHost) ||
+        hipMemcpy(hi.data(), d_hint, n * sizeof(SizeT), hipMemcpyDeviceToHost))
+        return fin(-1);
+    for (int q = 0; q < n; q++)
+        sorted[q] = int32_t(s[q]);
+    for (int v = 0; hint && v < n; v++)
+        hint[v] = int32_t(hi[v]);
+    return fin(ok);
+}
+
 } // namespace poa
 } // namespace gwamd
+
+// Test hook (tests/test_poa_topsort.py): topsort_levels of one graph given as
+// the reference's fixed-slot edge arrays (kMaxEdges slots per node), with the
+// previous read's order of the first n_prev nodes (order_prev: a permutation
+// of 0..n_prev-1, may be null when n_prev is 0) and critical-predecessor
+// hints for the first n_hint nodes (hint may be null when n_hint is 0; it
+// receives the final c(v)).  Returns 1 when the level sort produced sorted[],
+// 0 when it declined (the kernels then run the FIFO sort), negative on a HIP
+// error or bad arguments.
+extern "C" int gwamd_internal_topsort_levels(int size_bits, int n, int n_prev, int n_hint, const uint16_t* in_cnt,
+                                             const int32_t* in_e, const uint16_t* out_cnt, const int32_t* out_e,
+                                             int32_t* hint, const int32_t* order_prev, int threads, int scratch,
+                                             int32_t* sorted)
+{
+    if (size_bits == 16)
+        return gwamd::poa::topsort_levels_test<int16_t>(n, n_prev, n_hint, in_cnt, in_e, out_cnt, out_e, hint,
+                                                        order_prev, threads, scratch, sorted);
+    return gwamd::poa::topsort_levels_test<int32_t>(n, n_prev, n_hint, in_cnt, in_e, out_cnt, out_e, hint, order_prev,
+                                                    threads, scratch, sorted);
+}
 
 // ---------------------------------------------------------------------------
 extern "C" hipError_t gwamd_internal_poa_band_launch(const gwamd::poa::Buffers* b, const gwamd::poa::Dims* d,

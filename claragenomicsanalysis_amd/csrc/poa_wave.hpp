@@ -1439,6 +1439,658 @@ __device__ __forceinline__ bool topsort_lds_big(WinGraph<SizeT> g, int n, GWAMD_
 }
 
 // ---------------------------------------------------------------------------
+// Kahn order by levels, on every wave of the workgroup (round 6).
+//
+// The reference's FIFO sort (cudapoa_topsort.cuh:56-85: sources in id order,
+// then each popped node releases its successors in out-slot order) pops the
+// nodes in increasing longest-path level from the sources (a node is released
+// by its last-popped predecessor, which lies one level below it), and within
+// a level in the order of (position of that releasing predecessor, the node's
+// slot in its out-list); level 0 is in id order.  The releasing predecessor
+// ("parent") is the highest-positioned predecessor of the level below.  So:
+//   1. levels D(v) = 1 + max D(pred): every node points to one critical
+//      predecessor c(v) (first guess: the one the previous read's sort found,
+//      kept in `hint`, else the first in-edge), depths along c are found by
+//      pointer jumping (one 32-bit LDS word per node, anc | depth << 16,
+//      updated in place: any word a lane reads is a valid (ancestor, distance)
+//      pair), and nodes with two or more predecessors check D(v) > D(p) for
+//      every p (their in-lists cached in LDS); violators move c(v) to their
+//      deepest predecessor and the jumping is redone (2-4 rounds of this per
+//      read at configs B and C);
+//   2. a counting sort by level (the counts and offsets live in the low halves
+//      of the same words, indexed by level);
+//   3. levels holding one node are placed directly; every run of consecutive
+//      multi-node levels follows a one-node level (whose node is then every
+//      member's parent) or starts at level 0, so each run is ordered by one
+//      lane, level by level, from the previous level's positions.
+// Same order as the FIFO by construction (tests/test_poa_topsort.py: the
+// reference's topsort KATs, random DAGs, whole windows against the FIFO).
+// LDS: 9 bytes per node + 128 (the in-list cache shares the level bucket's
+// 2 bytes per node); returns false (nothing written, the caller runs the FIFO
+// sort) when that does not fit, when n > 65535, when the cached in-lists
+// exceed n entries, or when the checks have not converged after kLvIters (32)
+// rounds.  Must be called by every thread of the workgroup (it holds
+// barriers); n and n_hint must be workgroup-uniform.  hint[v] for v < n_hint:
+// c(v) of the previous sort of this window (edges are never removed, so it is
+// still a predecessor); the final c(v) is written back to hint[0..n).
+constexpr int kLvIters  = 32;
+constexpr int kLvRounds = 40;
+constexpr int kLvU      = 4; // nodes per thread whose HBM loads are issued together
+constexpr int kLvE      = 8; // edge slots loaded with a node's counts
+constexpr int kLvC      = 16; // nodes per chunk of the in-order pass (their loads issued together)
+#ifdef GWAMD_TS_INLINE // diagnostic builds: the sort inlined into its kernels
+#define GWAMD_TS_ATTR __forceinline__
+#else
+#define GWAMD_TS_ATTR __noinline__
+#endif
+template <typename SizeT>
+__device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_prev, GWAMD_LDS uint8_t* scratch,
+                                             int scratch_bytes, int tid, int nthr, SizeT* hint, int n_hint,
+                                             uint64_t* prof = nullptr)
+{
+    // typed global pointers: the function is out of line, where the graph's
+    // pointers would arrive flat, and a flat load counts against the LDS wait
+    // counter too (every LDS wait would wait for the HBM loads in flight)
+    GWAMD_GLB const uint16_t* g_in_cnt  = glb_of(g.in_cnt);
+    GWAMD_GLB const uint16_t* g_out_cnt = glb_of(g.out_cnt);
+    GWAMD_GLB const SizeT* g_in_e       = glb_of(g.in_e);
+    GWAMD_GLB const SizeT* g_out_e      = glb_of(g.out_e);
+    GWAMD_GLB SizeT* g_sorted           = glb_of(g.sorted);
+    GWAMD_GLB SizeT* g_pos              = glb_of(g.pos);
+    GWAMD_GLB SizeT* g_hint             = glb_of(hint);
+    const int N8             = (n + 7) & ~7;
+    const int nmw            = (n + 31) / 32; // anchor mask words
+    const int need           = 128 + 9 * N8 + 4 * ((nmw + 3) & ~3);
+    n_prev                   = min(max(n_prev, 0), n);
+    if (n <= 0 || n > 65535 || need > scratch_bytes)
+        return false;
+#ifdef GWAMD_TOPSORT_PROFILE
+    uint64_t tp = __builtin_amdgcn_s_memtime();
+    auto lap    = [&](int k) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        if (prof && tid == 0)
+            prof[k] += t - tp;
+        tp = t;
+    };
+#else
+    auto lap = [&](int) {};
+#endif
+    GWAMD_LDS int* ctl       = (GWAMD_LDS int*)(scratch);                     // [0..1] flags, [2] fail, [4..] wave sums
+    GWAMD_LDS uint32_t* word = (GWAMD_LDS uint32_t*)(scratch + 128);          // anc | depth << 16; level counters
+    GWAMD_LDS uint16_t* cc   = (GWAMD_LDS uint16_t*)(scratch + 128 + 4 * N8); // critical pred, then key, then pos
+    GWAMD_LDS uint16_t* bkt  = cc + N8;                                       // in-list cache, then level buckets
+    GWAMD_LDS uint8_t* meta  = (GWAMD_LDS uint8_t*)(bkt + N8);                // 0x80 multi-pred | 0x40 multi-parent | ic/slot
+    GWAMD_LDS uint32_t* mask = (GWAMD_LDS uint32_t*)(meta + N8);              // anchor bits
+    const int wave           = tid / kWave;
+    const int lane           = tid & (kWave - 1);
+    const int nwaves         = nthr / kWave;
+    // workgroup exclusive sum of one int per thread (wave sums through ctl[4..])
+    auto wg_excl_sum = [&](int x, int& total) -> int {
+        int wtot     = 0;
+        const int ex = wave_excl_sum(x, lane, wtot);
+        if (lane == 0)
+            ctl[4 + wave] = wtot;
+        __syncthreads();
+        int before = 0;
+        total      = 0;
+        for (int k = 0; k < nwaves; k++)
+        {
+            const int t = ctl[4 + k];
+            before += k < wave ? t : 0;
+            total += t;
+        }
+        __syncthreads();
+        return before + ex;
+    };
+    // 1a. in-degrees (coalesced); the thread's multi-predecessor in-lists are
+    // cached in LDS in its node order, at an offset from a workgroup scan
+    // (every per-node loop below issues the loads of kLvB nodes before their
+    // stores: LDS stores and loads may alias, so one node at a time would
+    // serialise a round trip per node)
+    constexpr int kLvB = 8;
+    int mine = 0;
+    for (int v0 = tid; v0 < n; v0 += kLvB * nthr)
+    {
+        int ic[kLvB];
+#pragma unroll
+        for (int u = 0; u < kLvB; u++)
+            ic[u] = int(g_in_cnt[min(v0 + u * nthr, n - 1)]);
+#pragma unroll
+        for (int u = 0; u < kLvB; u++)
+            if (v0 + u * nthr < n)
+            {
+                meta[v0 + u * nthr] = uint8_t((ic[u] >= 2 ? 0x80 : 0) | ic[u]);
+                mine += ic[u] >= 2 ? ic[u] : 0;
+            }
+    }
+    if (tid == 0)
+    {
+        ctl[0] = 0;
+        ctl[1] = 0;
+        ctl[2] = 0;
+        ctl[3] = 0;
+    }
+    int ctotal          = 0;
+    const int cbase     = wg_excl_sum(mine, ctotal);
+    const bool cache_ok = ctotal <= N8; // uniform: else the checks read the in-lists from HBM
+    // 1b. first guess of c(v) and the in-list cache: kLvU nodes per thread, the
+    // counts (from LDS) and the first kLvE in-edge slots of each issued together
+    {
+        int cur = cbase;
+        for (int v0 = tid; v0 < n; v0 += kLvU * nthr)
+        {
+            int ic[kLvU], hv[kLvU];
+            SizeT ev[kLvU][kLvE];
+#pragma unroll
+            for (int u = 0; u < kLvU; u++)
+            {
+                const int v = min(v0 + u * nthr, n - 1);
+                ic[u]       = meta[v] & 63;
+                hv[u]       = v < n_hint ? int(g_hint[v]) : v;
+#pragma unroll
+                for (int e = 0; e < kLvE; e++)
+                    ev[u][e] = e < ic[u] ? g_in_e[v * kMaxEdges + e] : SizeT(0);
+            }
+#pragma unroll
+            for (int u = 0; u < kLvU; u++)
+            {
+                const int v = v0 + u * nthr;
+                if (v >= n)
+                    break;
+                int c = v;
+                if (ic[u] > 0)
+                    c = hv[u] != v ? hv[u] : int(ev[u][0]);
+                if (ic[u] >= 2 && cache_ok)
+                {
+#pragma unroll
+                    for (int e = 0; e < kLvE; e++)
+                        if (e < ic[u])
+                            bkt[cur + e] = uint16_t(int(ev[u][e]));
+                    for (int e = kLvE; e < ic[u]; e++)
+                        bkt[cur + e] = uint16_t(int(g_in_e[v * kMaxEdges + e]));
+                    cur += ic[u];
+                }
+                cc[v] = uint16_t(c);
+            }
+        }
+    }
+    __syncthreads();
+    lap(0);
+    int r   = 0; // flag generation: slot r & 1 holds r when some thread raised it
+    bool ok = false;
+    int rounds_total = 0;
+    for (int it = 0; it < kLvIters; it++)
+    {
+        // reset: every word (c(v), 1), sources (v, 0); anchor bits cleared
+        for (int v0 = tid; v0 < n; v0 += kLvB * nthr)
+        {
+            uint32_t c[kLvB];
+#pragma unroll
+            for (int u = 0; u < kLvB; u++)
+                c[u] = cc[min(v0 + u * nthr, n - 1)];
+#pragma unroll
+            for (int u = 0; u < kLvB; u++)
+            {
+                const int v = v0 + u * nthr;
+                if (v < n)
+                    word[v] = c[u] | (c[u] != uint32_t(v) ? 1u << 16 : 0u);
+            }
+        }
+        for (int k = tid; k < nmw; k += nthr)
+            mask[k] = 0;
+        __syncthreads();
+        lap(1);
+        // one pass per thread in topological order (a contiguous slice of the
+        // previous read's order, then a slice of this read's new nodes in id
+        // order, which follows the read): a node whose c is the node before it
+        // takes that node's fresh word from a register, any other reads c's
+        // word as it is (every word is a valid (ancestor, distance) pair), so
+        // chains collapse in one pass; every ancestor a word ends on is marked
+        // as an anchor
+        {
+            uint32_t pv = 0xffffffffu, pw = 0, last_mark = 0xffffffffu;
+            auto seq_chunk = [&](const int* vs, int cnt) {
+                int cs[kLvC];
+                uint32_t wc[kLvC];
+#pragma unroll
+                for (int u = 0; u < kLvC; u++)
+                    cs[u] = u < cnt ? int(cc[vs[u]]) : 0;
+#pragma unroll
+                for (int u = 0; u < kLvC; u++)
+                    wc[u] = word[cs[u]];
+#pragma unroll
+                for (int u = 0; u < kLvC; u++)
+                {
+                    if (u >= cnt)
+                        break;
+                    const uint32_t v = uint32_t(vs[u]), c = uint32_t(cs[u]);
+                    if (c == v)
+                        continue; // a source keeps (v, 0)
+                    const uint32_t b = c == pv ? pw : wc[u];
+                    const uint32_t w = (b & 0xffffu) | ((b & 0xffff0000u) + (1u << 16));
+                    word[v]          = w;
+                    const uint32_t a = w & 0xffffu;
+                    if (a != last_mark)
+                    {
+                        __hip_atomic_fetch_or(&mask[a >> 5], 1u << (a & 31), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+                        last_mark = a;
+                    }
+                    pv = v;
+                    pw = w;
+                }
+            };
+            const int ro = (n_prev + nthr - 1) / nthr;
+            const int q0 = min(tid * ro, n_prev), q1 = min(q0 + ro, n_prev);
+            SizeT nx[kLvC];
+#pragma unroll
+            for (int u = 0; u < kLvC; u++)
+                nx[u] = q0 + u < q1 ? g_sorted[q0 + u] : SizeT(0);
+            for (int q = q0; q < q1; q += kLvC)
+            {
+                int vs[kLvC];
+#pragma unroll
+                for (int u = 0; u < kLvC; u++)
+                    vs[u] = int(nx[u]);
+#pragma unroll
+                for (int u = 0; u < kLvC; u++)
+                    nx[u] = q + kLvC + u < q1 ? g_sorted[q + kLvC + u] : SizeT(0);
+                seq_chunk(vs, min(kLvC, q1 - q));
+            }
+            pv = 0xffffffffu;
+            const int rn = (n - n_prev + nthr - 1) / nthr;
+            const int i0 = n_prev + min(tid * rn, n - n_prev), i1 = min(i0 + rn, n);
+            for (int i = i0; i < i1; i += kLvC)
+            {
+                int vs[kLvC];
+#pragma unroll
+                for (int u = 0; u < kLvC; u++)
+                    vs[u] = i + u;
+                seq_chunk(vs, min(kLvC, i1 - i));
+            }
+        }
+        __syncthreads();
+        lap(2);
+        // pointer jumping among the anchors only (an anchor's own word ends on
+        // an anchor or a source)
+        bool conv = false;
+        for (int round = 0; round < kLvRounds; round++)
+        {
+            bool ch = false;
+            for (int k = tid; k < nmw; k += nthr)
+            {
+                uint32_t bits = mask[k];
+                while (bits)
+                {
+                    const int a = k * 32 + __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    const uint32_t wa = word[a];
+                    const uint32_t x  = wa & 0xffffu;
+                    const uint32_t wx = word[x];
+                    if ((wx & 0xffffu) != x)
+                    {
+                        word[a] = (wx & 0xffffu) | ((wa & 0xffff0000u) + (wx & 0xffff0000u));
+                        ch      = true;
+                    }
+                }
+            }
+            r++;
+            rounds_total++;
+            if (ch)
+                ctl[r & 1] = r;
+            __syncthreads();
+            if (uniform(ctl[r & 1]) != r)
+            {
+                conv = true;
+                break;
+            }
+        }
+        lap(3);
+#ifdef GWAMD_TOPSORT_PROFILE
+        {
+            int na = 0;
+            for (int k = tid; k < nmw; k += nthr)
+                na += __popc(mask[k]);
+            __hip_atomic_fetch_add(&ctl[3], na, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+#endif
+        if (!conv)
+            break;
+        // every word one step through its (now final) anchor
+        for (int v0 = tid; v0 < n; v0 += kLvB * nthr)
+        {
+            uint32_t w[kLvB], wa[kLvB];
+#pragma unroll
+            for (int u = 0; u < kLvB; u++)
+                w[u] = word[min(v0 + u * nthr, n - 1)];
+#pragma unroll
+            for (int u = 0; u < kLvB; u++)
+                wa[u] = word[w[u] & 0xffffu];
+#pragma unroll
+            for (int u = 0; u < kLvB; u++)
+            {
+                const int v = v0 + u * nthr;
+                if (v < n && (wa[u] & 0xffffu) != (w[u] & 0xffffu))
+                    word[v] = (wa[u] & 0xffffu) | ((w[u] & 0xffff0000u) + (wa[u] & 0xffff0000u));
+            }
+        }
+        __syncthreads();
+        lap(4);
+        // check D(v) > D(p) on the nodes with several predecessors (cached
+        // lists; kLvV nodes and their first kLvVE entries per batch)
+        constexpr int kLvV  = 4;
+        constexpr int kLvVE = 4;
+        bool viol           = false;
+        int cur             = cbase;
+        for (int v0 = tid; v0 < n; v0 += kLvV * nthr)
+        {
+            int m[kLvV], D[kLvV], off[kLvV], vv[kLvV];
+#pragma unroll
+            for (int u = 0; u < kLvV; u++)
+            {
+                vv[u] = min(v0 + u * nthr, n - 1);
+                m[u]  = v0 + u * nthr < n ? int(meta[vv[u]]) : 0;
+                D[u]  = int(word[vv[u]] >> 16);
+            }
+#pragma unroll
+            for (int u = 0; u < kLvV; u++)
+            {
+                off[u] = cur;
+                cur += m[u] >= 0x80 ? (m[u] & 63) : 0;
+            }
+            int pe[kLvV][kLvVE], dp[kLvV][kLvVE];
+#pragma unroll
+            for (int u = 0; u < kLvV; u++)
+#pragma unroll
+                for (int e = 0; e < kLvVE; e++)
+                {
+                    const bool live = m[u] >= 0x80 && e < (m[u] & 63);
+                    pe[u][e]        = !live ? vv[u]
+                                            : (cache_ok ? int(bkt[off[u] + e]) : int(g_in_e[vv[u] * kMaxEdges + e]));
+                }
+#pragma unroll
+            for (int u = 0; u < kLvV; u++)
+#pragma unroll
+                for (int e = 0; e < kLvVE; e++)
+                    dp[u][e] = int(word[pe[u][e]] >> 16);
+#pragma unroll
+            for (int u = 0; u < kLvV; u++)
+            {
+                if (m[u] < 0x80)
+                    continue;
+                const int ic = m[u] & 63;
+                int best = -1, bd = -1, ncand = 0;
+#pragma unroll
+                for (int e = 0; e < kLvVE; e++)
+                {
+                    if (e < ic)
+                    {
+                        if (dp[u][e] > bd)
+                        {
+                            bd   = dp[u][e];
+                            best = pe[u][e];
+                        }
+                        ncand += dp[u][e] == D[u] - 1 ? 1 : 0;
+                    }
+                }
+                for (int e = kLvVE; e < ic; e++)
+                {
+                    const int p = cache_ok ? int(bkt[off[u] + e]) : int(g_in_e[vv[u] * kMaxEdges + e]);
+                    const int d = int(word[p] >> 16);
+                    if (d > bd)
+                    {
+                        bd   = d;
+                        best = p;
+                    }
+                    ncand += d == D[u] - 1 ? 1 : 0;
+                }
+                if (bd + 1 > D[u])
+                {
+                    cc[vv[u]] = uint16_t(best);
+                    viol      = true;
+                }
+                else
+                    meta[vv[u]] = uint8_t(0x80 | (ncand > 1 ? 0x40 : 0) | ic);
+            }
+        }
+        r++;
+        if (viol)
+            ctl[r & 1] = r;
+        __syncthreads();
+        lap(4);
+        if (uniform(ctl[r & 1]) != r)
+        {
+            ok = true;
+            break;
+        }
+    }
+    lap(4);
+#ifdef GWAMD_TOPSORT_PROFILE
+    if (prof && tid == 0)
+        (void)0; // (slot 7 times the outputs)
+    (void)rounds_total;
+#endif
+    if (!ok)
+        return false;
+    // 2. counting sort by level: counts in the low halves (indexed by level),
+    // exclusive offsets, then the running ends after placing the nodes
+    for (int v0 = tid; v0 < n; v0 += kLvB * nthr)
+    {
+        uint32_t w[kLvB];
+#pragma unroll
+        for (int u = 0; u < kLvB; u++)
+            w[u] = word[min(v0 + u * nthr, n - 1)];
+#pragma unroll
+        for (int u = 0; u < kLvB; u++)
+            if (v0 + u * nthr < n)
+                word[v0 + u * nthr] = w[u] & 0xffff0000u;
+    }
+    __syncthreads();
+    for (int v0 = tid; v0 < n; v0 += kLvB * nthr)
+    {
+        uint32_t l[kLvB];
+#pragma unroll
+        for (int u = 0; u < kLvB; u++)
+            l[u] = word[min(v0 + u * nthr, n - 1)] >> 16;
+#pragma unroll
+        for (int u = 0; u < kLvB; u++)
+            if (v0 + u * nthr < n)
+                __hip_atomic_fetch_add(&word[l[u]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    {
+        const int per = (n + nthr - 1) / nthr;
+        const int l0  = min(tid * per, n), l1 = min(l0 + per, n);
+        int sum       = 0;
+        for (int l = l0; l < l1; l++)
+            sum += int(word[l] & 0xffffu);
+        int total_unused = 0;
+        int run          = wg_excl_sum(sum, total_unused);
+        for (int b0 = l0; b0 < l1; b0 += kLvB)
+        {
+            uint32_t w[kLvB];
+#pragma unroll
+            for (int u = 0; u < kLvB; u++)
+                w[u] = word[min(b0 + u, l1 - 1)];
+#pragma unroll
+            for (int u = 0; u < kLvB; u++)
+                if (b0 + u < l1)
+                {
+                    word[b0 + u] = (w[u] & 0xffff0000u) | uint32_t(run);
+                    run += int(w[u] & 0xffffu);
+                }
+        }
+    }
+    __syncthreads();
+    for (int v0 = tid; v0 < n; v0 += kLvB * nthr)
+    {
+        uint32_t l[kLvB], old[kLvB];
+#pragma unroll
+        for (int u = 0; u < kLvB; u++)
+            l[u] = word[min(v0 + u * nthr, n - 1)] >> 16;
+#pragma unroll
+        for (int u = 0; u < kLvB; u++)
+            old[u] = v0 + u * nthr < n ? __hip_atomic_fetch_add(&word[l[u]], 1u, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_WORKGROUP)
+                                       : 0u;
+#pragma unroll
+        for (int u = 0; u < kLvB; u++)
+            if (v0 + u * nthr < n)
+                bkt[old[u] & 0xffffu] = uint16_t(v0 + u * nthr);
+    }
+    __syncthreads();
+    auto lv_end = [&](int l) -> int { return int(word[l] & 0xffffu); };
+    auto lv_off = [&](int l) -> int { return l > 0 ? int(word[l - 1] & 0xffffu) : 0; };
+    // 3a. c(v) back to the hint array; one-node levels take their position;
+    // members of multi-node levels with one candidate parent (c(v), one level
+    // below) find their slot in its out-list (kLvU nodes' count and first
+    // kLvE out-slots issued together)
+    for (int v0 = tid; v0 < n; v0 += kLvU * nthr)
+    {
+        int par[kLvU], oc[kLvU], lo[kLvU], le[kLvU], lvl[kLvU], mt[kLvU];
+        SizeT ov[kLvU][kLvE];
+        bool want[kLvU];
+#pragma unroll
+        for (int u = 0; u < kLvU; u++)
+        {
+            const int v = min(v0 + u * nthr, n - 1);
+            lvl[u]      = int(word[v] >> 16);
+            par[u]      = cc[v];
+            mt[u]       = meta[v];
+        }
+#pragma unroll
+        for (int u = 0; u < kLvU; u++)
+        {
+            lo[u]   = lv_off(lvl[u]);
+            le[u]   = lv_end(lvl[u]);
+            want[u] = v0 + u * nthr < n && lvl[u] > 0 && le[u] - lo[u] > 1 && (mt[u] & 0x40) == 0;
+            oc[u]   = want[u] ? int(g_out_cnt[par[u]]) : 0;
+#pragma unroll
+            for (int e = 0; e < kLvE; e++)
+                ov[u][e] = want[u] ? g_out_e[par[u] * kMaxEdges + e] : SizeT(0);
+        }
+#pragma unroll
+        for (int u = 0; u < kLvU; u++)
+        {
+            const int v = v0 + u * nthr;
+            if (v >= n)
+                break;
+            g_hint[v] = SizeT(par[u]);
+            if (le[u] - lo[u] == 1)
+                cc[v] = uint16_t(lo[u]);
+            else if (want[u])
+            {
+                int slot = 0;
+#pragma unroll
+                for (int s = 0; s < kLvE; s++)
+                    slot = (s < oc[u] && int(ov[u][s]) == v) ? s : slot;
+                for (int s = kLvE; s < oc[u]; s++)
+                    if (int(g_out_e[par[u] * kMaxEdges + s]) == v)
+                        slot = s;
+                meta[v] = uint8_t((mt[u] & 0xc0) | slot);
+            }
+        }
+    }
+    __syncthreads();
+    lap(5);
+    // 3b. runs of multi-node levels, one lane per run
+    bool fail = false;
+    for (int l = tid; l < n; l += nthr)
+    {
+        int lo = lv_off(l), le = lv_end(l);
+        if (le - lo <= 1 || (l > 0 && lo - lv_off(l - 1) > 1))
+            continue;
+        int plo = l > 0 ? lv_off(l - 1) : 0;
+        for (int ll = l;;)
+        {
+            // keys (rank of the parent in the level below, out-slot), or the
+            // node id at level 0, in place of c(v)
+            for (int i = lo; i < le; i++)
+            {
+                const int v = bkt[i];
+                int key     = v;
+                if (ll > 0)
+                {
+                    int par, slot;
+                    if (meta[v] & 0x40)
+                    {
+                        // several predecessors one level below: the one placed last
+                        const int ic = meta[v] & 63;
+                        par          = -1;
+                        int bp       = -1;
+                        for (int e = 0; e < ic; e++)
+                        {
+                            const int p = int(g_in_e[v * kMaxEdges + e]);
+                            if (int(word[p] >> 16) == ll - 1 && int(cc[p]) > bp)
+                            {
+                                bp  = cc[p];
+                                par = p;
+                            }
+                        }
+                        const int oc = int(g_out_cnt[par]);
+                        slot         = 0;
+                        for (int s = 0; s < oc; s++)
+                            if (int(g_out_e[par * kMaxEdges + s]) == v)
+                                slot = s;
+                    }
+                    else
+                    {
+                        par  = cc[v];
+                        slot = meta[v] & 63;
+                    }
+                    const int pr = int(cc[par]) - plo;
+                    fail         = fail || pr >= 1024;
+                    key          = (pr << 6) | slot;
+                }
+                cc[v] = uint16_t(key);
+            }
+            fail = fail || le - lo > 255;
+            for (int i = lo; i < le; i++)
+            {
+                const int v = bkt[i];
+                const int k = cc[v];
+                int rank    = 0;
+                for (int j = lo; j < le; j++)
+                    rank += int(cc[bkt[j]]) < k ? 1 : 0;
+                meta[v] = uint8_t(rank);
+            }
+            for (int i = lo; i < le; i++)
+            {
+                const int v = bkt[i];
+                cc[v]       = uint16_t(lo + meta[v]);
+            }
+            ll++;
+            if (ll >= n)
+                break;
+            plo = lo;
+            lo  = le;
+            le  = lv_end(ll);
+            if (le - lo <= 1)
+                break;
+        }
+    }
+    if (fail)
+        ctl[2] = 1;
+    __syncthreads();
+    lap(6);
+    if (uniform(ctl[2]) != 0)
+        return false;
+    // 4. outputs
+    for (int v = tid; v < n; v += nthr)
+    {
+        const int p = cc[v];
+        if (p < n)
+        {
+            g_sorted[p] = SizeT(v);
+            g_pos[v]    = SizeT(p);
+        }
+    }
+    __syncthreads();
+    lap(7);
+    return true;
+}
+
+// ---------------------------------------------------------------------------
 // Traceback move window: 128 cells around the walk whose moves are decoded
 // lane-parallel, two per lane (cell t and t + 64).  Two shapes:
 //  * rectangle (slope == 0): 16 rows x 8 columns, cell t = a * 8 + b at row

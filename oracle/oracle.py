@@ -229,7 +229,7 @@ def edges_from_lists(outgoing, n):
     for i, outs in enumerate(outgoing):
         out_cnt[i] = len(outs)
         for j, o in enumerate(outs):
-            in_e[o * MAX_EDGES + in_cnt[o]] = i
+            in_e[o * MAX_EDGES + int(in_cnt[o])] = i
             in_cnt[o] += 1
             out_e[i * MAX_EDGES + j] = o
     return in_cnt, in_e, out_cnt, out_e

@@ -638,6 +638,7 @@ def test_traceback_walk_modes(mode, out, monkeypatch):
 @pytest.mark.parametrize("mode", ["full", "full_msa"])
 def test_topsort_queue_ring(mode, monkeypatch):
     monkeypatch.setenv("GWAMD_TOPSORT_RING", "1")
+    monkeypatch.setenv("GWAMD_TOPSORT", "fifo")  # the FIFO sort (the default is the level sort)
     banded = mode.startswith("banded")
     msa = mode.endswith("msa")
     wins = synth.poa_windows(7, 6, 300, 32, 40, 40, 40)
