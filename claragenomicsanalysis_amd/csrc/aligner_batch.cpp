@@ -243,15 +243,17 @@ private:
 class AlignerGlobalHip : public Aligner
 {
 public:
-    // device_budget: the caller's DefaultDeviceAllocator caching budget in
-    // bytes (-1: all available memory, allocator.hpp:282-298).  The reference
+    // budget: the pool of the caller's DefaultDeviceAllocator (null or a
+    // negative capacity: all available memory, allocator.hpp:282-305), shared
+    // by every aligner made from copies of that allocator.  The reference
     // serves every device buffer of the aligner from that pool; here the
     // fixed buffers (sequences, paths, lengths) come first and the workspace
-    // gets as many persistent-grid slots as the rest of the budget holds; a
-    // budget below the fixed buffers plus one slot throws, as the reference's
-    // pool does when an allocation does not fit.
+    // gets as many persistent-grid slots as what is left of the pool holds;
+    // less than the fixed buffers plus one slot throws, as the reference's
+    // pool does when an allocation does not fit.  The bytes stay reserved
+    // until the aligner is destroyed.
     AlignerGlobalHip(int32_t max_query_length, int32_t max_target_length, int32_t max_alignments, int algorithm,
-                     hipStream_t stream, int32_t device_id, int64_t device_budget = -1)
+                     hipStream_t stream, int32_t device_id, std::shared_ptr<DeviceBudget> budget = nullptr)
         : max_q_(throw_on_negative(max_query_length, "max_query_length must be non-negative."))
         , max_t_(throw_on_negative(max_target_length, "max_target_length must be non-negative."))
         , max_n_(throw_on_negative(max_alignments, "max_alignments must be non-negative."))
@@ -279,16 +281,24 @@ public:
         max_result_ = (max_q_ + max_t_ + 3) / 4 * 4; // calc_max_result_length (aligner_global.cpp:26-31)
         ScopedDevice dev(device_id_);
         plan();
-        if (device_budget >= 0)
+        if (budget && budget->capacity() >= 0)
         {
             const int64_t fixed = int64_t(2) * stride_ * max_n_ + 16 + int64_t(2) * max_n_ * 4 +
-                                  int64_t(max_result_) * max_n_ + 16 + int64_t(max_n_) * 4;
-            const int64_t room  = (device_budget - fixed) / std::max<int64_t>(1, slot_bytes_);
-            if (room < 1)
-                throw std::runtime_error("The aligner needs " + std::to_string(fixed + slot_bytes_) +
-                                         " device bytes, more than max_device_memory_allocator_caching_size (" +
-                                         std::to_string(device_budget) + ").");
-            slots_ = int32_t(std::min<int64_t>(slots_, room));
+                                  int64_t(max_result_) * max_n_ + 16 + int64_t(max_n_) * 4 + 32 +
+                                  (algo_ == GWAMD_ALIGNER_MYERS_BANDED ? int64_t(max_n_) * kMaxSpecSweeps * 4 : 0);
+            const int64_t sb    = std::max<int64_t>(1, slot_bytes_);
+            const int64_t got   = budget->reserve(fixed + sb, fixed + int64_t(slots_) * sb);
+            if (got < 0)
+                throw std::runtime_error("The aligner needs " + std::to_string(fixed + sb) +
+                                         " device bytes, more than its allocator has left (" +
+                                         std::to_string(budget->capacity() - budget->used()) + " of " +
+                                         std::to_string(budget->capacity()) + ").");
+            slots_    = int32_t(std::min<int64_t>(slots_, (got - fixed) / sb));
+            // keep exactly what this aligner uses
+            const int64_t used = fixed + int64_t(slots_) * sb;
+            budget->release(got - used);
+            budget_   = std::move(budget);
+            reserved_ = used;
         }
         auto dalloc = [&](void** p, size_t bytes, bool zero = true) {
             GWAMD_HIP_CHECK(hipMalloc(p, std::max<size_t>(bytes, 16)));
@@ -324,6 +334,8 @@ public:
 
     ~AlignerGlobalHip() override
     {
+        if (budget_)
+            budget_->release(reserved_);
         (void)hipSetDevice(device_id_);
         for (hipStream_t st : {stream2_, s_in_, s_out_})
             if (st)
@@ -401,9 +413,7 @@ public:
             stages_ = 1;
             chunk0_[0] = 0, chunk0_[1] = n;
             upload();
-            GWAMD_HIP_CHECK(hipEventRecord(ev_k_[0], stream_));
-            launch();
-            GWAMD_HIP_CHECK(hipEventRecord(ev_k_[1], stream_));
+            launch(); // records ev_k_[0] / ev_k_[1] around the kernel
             download();
             GWAMD_HIP_CHECK(hipEventRecord(ev_d_[0], stream_));
             return StatusType::success;
@@ -535,20 +545,33 @@ public:
     {
         alignments_.clear();
         max_diff_ = 0;
+        stages_   = 0; // no launch of this batch yet
     }
 
-    // bench / C ABI helpers
+    // bench / C ABI helpers: the split path (upload, launch, download) runs
+    // one stage on stream_, so sync_alignments waits for stream_ before it
+    // fills and last_kernel_ms times that launch (the state of an
+    // earlier pipelined align_all() must not survive into a split launch)
     void upload()
     {
         ScopedDevice dev(device_id_);
         const size_t n = alignments_.size();
+        stages_        = 1;
+        chunk0_[0]     = 0;
+        chunk0_[1]     = int32_t(n);
         GWAMD_HIP_CHECK(hipMemcpyAsync(d_lens_, h_lens_.as<int32_t>(), 2 * n * 4, hipMemcpyHostToDevice, stream_));
         GWAMD_HIP_CHECK(hipMemcpyAsync(d_seqs_, h_seqs_.as<char>(), 2 * n * size_t(stride_), hipMemcpyHostToDevice,
                                        stream_));
     }
     void launch()
     {
+        ScopedDevice dev(device_id_);
+        stages_    = 1;
+        chunk0_[0] = 0;
+        chunk0_[1] = int32_t(alignments_.size());
+        GWAMD_HIP_CHECK(hipEventRecord(ev_k_[0], stream_));
         launch_range(0, int32_t(alignments_.size()), 0, slots_, stream_);
+        GWAMD_HIP_CHECK(hipEventRecord(ev_k_[1], stream_));
     }
     // Pairs [i0, i0 + count) on workspace slots [slot0, slot0 + nslots).
     void launch_range(int32_t i0, int32_t count, int32_t slot0, int32_t nslots, hipStream_t s)
@@ -560,6 +583,10 @@ public:
         a.paths    = d_paths_ + size_t(i0) * max_result_;
         a.path_len = d_plen_ + i0;
         a.n        = count;
+        // run-ahead distances of this stage's pairs: stages on the two compute
+        // streams must not share [0, count * sweeps)
+        if (a.spec_ed)
+            a.spec_ed = a.spec_ed + size_t(i0) * kMaxSpecSweeps;
         a.ws       = d_ws_ + size_t(slot0) * size_t(slot_bytes_);
         if (algo_ == GWAMD_ALIGNER_UKKONEN)
         {
@@ -576,8 +603,10 @@ public:
         if (algo_ == GWAMD_ALIGNER_MYERS_BANDED && band_waves_ > 1 && !band_waves_forced_)
         {
             // an aligner planned for long queries (8 waves per pair) runs a
-            // launch whose queries are all short with one wave per pair:
-            // their bands fit one 32-word chunk, which only wave 0 sweeps
+            // launch whose queries are all short with one wave per pair: the
+            // one-wave kernel is the default plan for such queries (short
+            // bands leave most of 8 waves idle, and one wave per pair keeps
+            // more pairs resident)
             int32_t mq = 0;
             for (int32_t k = i0; k < i0 + count; k++)
                 mq = std::max(mq, h_lens_.as<int32_t>()[2 * size_t(k)]);
@@ -702,14 +731,6 @@ private:
     {
         using namespace gwamd::aln;
         const int pat_words = (max_q_ + kWordBits - 1) / kWordBits;
-        // resident workspace slots within 64 GiB of the 288 GB HBM, or up to
-        // 96 GiB (3/4 of the free memory at most): 32 pairs of 65,536 bp need
-        // 32 band-matrix slots of 2.15 GB, and one slot fewer than pairs
-        // doubles the kernel
-        size_t free_b = 0, total_b = 0;
-        GWAMD_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-        const int64_t ws_cap =
-            std::max<int64_t>(int64_t(64) << 30, std::min<int64_t>(int64_t(96) << 30, int64_t(free_b / 4 * 3)));
         if (algo_ == GWAMD_ALIGNER_MYERS_BANDED)
         {
             // target as 2-bit letter codes, letter-major query patterns, and a
@@ -817,7 +838,22 @@ private:
         slots_    = std::max(1, per_cu * cus);
         resident_ = slots_;
         cus_      = cus;
-        slots_    = int32_t(std::max<int64_t>(1, std::min<int64_t>(slots_, ws_cap / slot_bytes_)));
+        // resident workspace slots within 64 GiB of the 288 GB HBM; only a
+        // batch whose slots need more (32 pairs of 65,536 bp: 32 band-matrix
+        // slots of 2.15 GB, and one slot fewer than pairs doubles the kernel)
+        // may take up to 96 GiB, and at most 3/4 of the free memory, so short-
+        // pair aligners keep a plan that does not depend on what else the
+        // process has allocated
+        int64_t ws_cap        = int64_t(64) << 30;
+        const int64_t want_ws = int64_t(std::min(slots_, max_n_)) * slot_bytes_;
+        if (want_ws > ws_cap)
+        {
+            size_t free_b = 0, total_b = 0;
+            GWAMD_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+            ws_cap = std::max<int64_t>(ws_cap, std::min<int64_t>({int64_t(96) << 30, want_ws,
+                                                                  int64_t(free_b / 4 * 3)}));
+        }
+        slots_ = int32_t(std::max<int64_t>(1, std::min<int64_t>(slots_, ws_cap / slot_bytes_)));
         apply_grid_override();
         slots_ = std::min(slots_, max_n_);
     }
@@ -996,6 +1032,8 @@ private:
     unsigned long long* d_stats_ = nullptr;
     int32_t* d_spec_ed_          = nullptr; // banded Myers: distances of the sweeps run ahead
     int32_t resident_ = 1, cus_ = 1;        // workgroups resident at once, CUs
+    std::shared_ptr<DeviceBudget> budget_;  // the allocator pool this aligner reserved from
+    int64_t reserved_ = 0;
     PinnedBuf h_seqs_, h_lens_, h_paths_, h_plen_;
     std::vector<std::shared_ptr<Alignment>> alignments_;
 };
@@ -1008,7 +1046,7 @@ std::unique_ptr<Aligner> create_aligner(int32_t max_query_length, int32_t max_ta
     if (type == AlignmentType::global_alignment)
         return std::make_unique<AlignerGlobalHip>(max_query_length, max_target_length, max_alignments,
                                                   GWAMD_ALIGNER_HIRSCHBERG_MYERS, stream, device_id,
-                                                  allocator.max_cached_bytes());
+                                                  allocator.budget());
     throw std::runtime_error("Aligner for specified type not implemented yet.");
 }
 
@@ -1077,6 +1115,11 @@ struct gwamd_aligner
     std::unique_ptr<ca::AlignerGlobalHip> impl;
 };
 
+struct gwamd_device_allocator
+{
+    claraparabricks::genomeworks::DefaultDeviceAllocator alloc;
+};
+
 extern "C" {
 
 int32_t gwamd_aligner_create(gwamd_aligner** out, int32_t max_query_length, int32_t max_target_length,
@@ -1094,15 +1137,68 @@ int32_t gwamd_aligner_create(gwamd_aligner** out, int32_t max_query_length, int3
         if (algorithm < GWAMD_ALIGNER_HIRSCHBERG_MYERS || algorithm > GWAMD_ALIGNER_UKKONEN)
             throw std::invalid_argument("unknown aligner algorithm");
         auto h  = std::make_unique<gwamd_aligner>();
-        h->impl = std::make_unique<ca::AlignerGlobalHip>(max_query_length, max_target_length, max_alignments,
-                                                         algorithm, static_cast<hipStream_t>(stream), device_id,
-                                                         max_caching);
+        h->impl = std::make_unique<ca::AlignerGlobalHip>(
+            max_query_length, max_target_length, max_alignments, algorithm, static_cast<hipStream_t>(stream),
+            device_id, max_caching >= 0 ? std::make_shared<claraparabricks::genomeworks::DeviceBudget>(max_caching)
+                                        : nullptr);
         *out    = h.release();
         return int32_t(0);
     });
 }
 
 void gwamd_aligner_destroy(gwamd_aligner* a) { delete a; }
+
+int32_t gwamd_device_allocator_create(gwamd_device_allocator** out, int64_t max_caching_size)
+{
+    return guarded_aln([&] {
+        if (!out)
+            throw std::invalid_argument("out is NULL");
+        if (max_caching_size < -1)
+            throw std::invalid_argument("max_caching_size has to be either -1 (=all available GPU memory) or "
+                                        "greater or equal than 0.");
+        auto h   = std::make_unique<gwamd_device_allocator>();
+        h->alloc = claraparabricks::genomeworks::create_default_device_allocator(max_caching_size);
+        *out     = h.release();
+        return int32_t(0);
+    });
+}
+
+void gwamd_device_allocator_destroy(gwamd_device_allocator* a) { delete a; }
+
+int64_t gwamd_device_allocator_capacity(const gwamd_device_allocator* a)
+{
+    return a ? a->alloc.max_cached_bytes() : -1;
+}
+
+int64_t gwamd_device_allocator_used(const gwamd_device_allocator* a)
+{
+    return a && a->alloc.budget() ? a->alloc.budget()->used() : 0;
+}
+
+int64_t gwamd_device_allocator_default_size(void)
+{
+    return claraparabricks::genomeworks::create_default_device_allocator().max_cached_bytes();
+}
+
+int32_t gwamd_aligner_create_with_allocator(gwamd_aligner** out, int32_t max_query_length, int32_t max_target_length,
+                                            int32_t max_alignments, int32_t alignment_type, int32_t algorithm,
+                                            void* stream, int32_t device_id, gwamd_device_allocator* allocator)
+{
+    return guarded_aln([&] {
+        if (!out || !allocator)
+            throw std::invalid_argument("out or allocator is NULL");
+        if (alignment_type != ca::AlignmentType::global_alignment)
+            throw std::runtime_error("Aligner for specified type not implemented yet.");
+        if (algorithm < GWAMD_ALIGNER_HIRSCHBERG_MYERS || algorithm > GWAMD_ALIGNER_UKKONEN)
+            throw std::invalid_argument("unknown aligner algorithm");
+        auto h  = std::make_unique<gwamd_aligner>();
+        h->impl = std::make_unique<ca::AlignerGlobalHip>(max_query_length, max_target_length, max_alignments,
+                                                         algorithm, static_cast<hipStream_t>(stream), device_id,
+                                                         allocator->alloc.budget());
+        *out    = h.release();
+        return int32_t(0);
+    });
+}
 
 int32_t gwamd_aligner_add_alignment(gwamd_aligner* a, const char* q, int32_t qlen, const char* t, int32_t tlen,
                                     int32_t rc_q, int32_t rc_t)

@@ -54,6 +54,17 @@ def _declare(L):
     L.gwamd_aligner_last_kernel_ms.argtypes = [vp, P(C.c_double)]
     L.gwamd_aligner_get_stats.restype = i32
     L.gwamd_aligner_get_stats.argtypes = [vp, P(i64), P(i64), P(i64)]
+    L.gwamd_device_allocator_create.restype = i32
+    L.gwamd_device_allocator_create.argtypes = [P(vp), i64]
+    L.gwamd_device_allocator_destroy.restype = None
+    L.gwamd_device_allocator_destroy.argtypes = [vp]
+    for name in ("gwamd_device_allocator_capacity", "gwamd_device_allocator_used"):
+        getattr(L, name).restype = i64
+        getattr(L, name).argtypes = [vp]
+    L.gwamd_device_allocator_default_size.restype = i64
+    L.gwamd_device_allocator_default_size.argtypes = []
+    L.gwamd_aligner_create_with_allocator.restype = i32
+    L.gwamd_aligner_create_with_allocator.argtypes = [P(vp), i32, i32, i32, i32, i32, vp, i32, vp]
     del i8
 
 
@@ -126,6 +137,35 @@ def _format(query, target, states):
     return ["".join(qs), "".join(ps), "".join(ts)]
 
 
+class DeviceAllocator:
+    """The C++ API's DefaultDeviceAllocator (create_default_device_allocator,
+    allocator.hpp:297-305): a device-memory pool of max_caching_size bytes
+    (default 2 GiB, -1 = all available) shared by every aligner created with
+    it (pass it as CudaAlignerBatch(..., allocator=...))."""
+
+    def __init__(self, max_caching_size=None):
+        self._lib = load_library()
+        if max_caching_size is None:
+            max_caching_size = self._lib.gwamd_device_allocator_default_size()
+        self._handle = C.c_void_p()
+        _check(self._lib.gwamd_device_allocator_create(C.byref(self._handle), int(max_caching_size)))
+
+    def __del__(self):
+        h = getattr(self, "_handle", None)
+        if h is not None and h.value:
+            self._lib.gwamd_device_allocator_destroy(h)
+            self._handle = None
+
+    @property
+    def capacity(self):
+        return int(self._lib.gwamd_device_allocator_capacity(self._handle))
+
+    @property
+    def used(self):
+        """Device bytes reserved by the live aligners created with this pool."""
+        return int(self._lib.gwamd_device_allocator_used(self._handle))
+
+
 class CudaAlignerBatch:
     """Python API for MI355X sequence-to-sequence global alignment
     (cudaaligner.pyx:121-270).  ``algorithm`` (an extension) selects the
@@ -133,7 +173,7 @@ class CudaAlignerBatch:
 
     def __init__(self, max_query_length, max_target_length, max_alignments, alignment_type="global", stream=None,
                  device_id=0, max_device_memory_allocator_caching_size=-1, algorithm="hirschberg_myers",
-                 *args, **kwargs):
+                 *args, allocator=None, **kwargs):
         if alignment_type != "global":
             raise RuntimeError("Unknown alignment_type provided. Must be global.")
         if algorithm not in ALGORITHMS:
@@ -141,10 +181,17 @@ class CudaAlignerBatch:
         self._lib = load_library()
         self._handle = C.c_void_p()
         self.stream = stream
-        _check(self._lib.gwamd_aligner_create(C.byref(self._handle), int(max_query_length), int(max_target_length),
-                                              int(max_alignments), 0, ALGORITHMS[algorithm],
-                                              _stream_handle(stream), int(device_id),
-                                              int(max_device_memory_allocator_caching_size)))
+        if allocator is not None:
+            # create_aligner(..., DefaultDeviceAllocator, stream, device_id) (aligner.hpp:90)
+            _check(self._lib.gwamd_aligner_create_with_allocator(
+                C.byref(self._handle), int(max_query_length), int(max_target_length), int(max_alignments), 0,
+                ALGORITHMS[algorithm], _stream_handle(stream), int(device_id), allocator._handle))
+            self._allocator = allocator
+        else:
+            _check(self._lib.gwamd_aligner_create(C.byref(self._handle), int(max_query_length),
+                                                  int(max_target_length), int(max_alignments), 0,
+                                                  ALGORITHMS[algorithm], _stream_handle(stream), int(device_id),
+                                                  int(max_device_memory_allocator_caching_size)))
         self._synced = False
 
     def __del__(self):

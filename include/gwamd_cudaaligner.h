@@ -9,6 +9,12 @@
  *                                 (algorithm 1: AlignerGlobalMyers,        aligner_global_myers.hpp:24
  *                                  algorithm 2: AlignerGlobalMyersBanded,  aligner_global_myers_banded.hpp:24
  *                                  algorithm 3: AlignerGlobalUkkonen)      aligner_global_ukkonen.hpp:28
+ *   gwamd_aligner_create_with_allocator
+ *                                 create_aligner(..., DefaultDeviceAllocator, aligner.hpp:90
+ *                                 stream, device_id)
+ *   gwamd_device_allocator_create create_default_device_allocator(size)    allocator.hpp:297-305
+ *                                 (copies share one pool: a handle here)   allocator.hpp:274-279
+ *   gwamd_device_allocator_destroy / _capacity / _used / _default_size
  *   gwamd_aligner_destroy         ~Aligner                                 aligner.hpp:45
  *   gwamd_aligner_add_alignment   Aligner::add_alignment                   aligner.hpp:70-71
  *   gwamd_aligner_align_all       Aligner::align_all                       aligner.hpp:55
@@ -54,6 +60,7 @@ extern "C" {
 #define GWAMD_ALIGNER_UKKONEN 3          /* AlignerGlobalUkkonen (p = 100) */
 
 typedef struct gwamd_aligner gwamd_aligner;
+typedef struct gwamd_device_allocator gwamd_device_allocator;
 
 const char* gwamd_last_error(void);
 
@@ -63,6 +70,23 @@ int32_t gwamd_aligner_create(gwamd_aligner** out, int32_t max_query_length, int3
                              int32_t max_alignments, int32_t alignment_type, int32_t algorithm, void* stream,
                              int32_t device_id, int64_t max_device_memory_allocator_caching_size);
 void gwamd_aligner_destroy(gwamd_aligner* aligner);
+
+/* DefaultDeviceAllocator pool (create_default_device_allocator): a byte budget
+ * of max_caching_size (-1: all available device memory) shared by every
+ * aligner created with it; each aligner reserves its device bytes (fixed
+ * buffers + as many workspace slots as fit) until it is destroyed, and
+ * creation fails (GWAMD_E_RUNTIME) when the fixed buffers and one slot do not
+ * fit what is left.  The handle may be destroyed while aligners still use
+ * the pool (they keep it alive). */
+int32_t gwamd_device_allocator_create(gwamd_device_allocator** out, int64_t max_caching_size);
+void gwamd_device_allocator_destroy(gwamd_device_allocator* allocator);
+int64_t gwamd_device_allocator_capacity(const gwamd_device_allocator* allocator);
+int64_t gwamd_device_allocator_used(const gwamd_device_allocator* allocator);
+/* the default max_caching_size of create_default_device_allocator (2 GiB) */
+int64_t gwamd_device_allocator_default_size(void);
+int32_t gwamd_aligner_create_with_allocator(gwamd_aligner** out, int32_t max_query_length, int32_t max_target_length,
+                                            int32_t max_alignments, int32_t alignment_type, int32_t algorithm,
+                                            void* stream, int32_t device_id, gwamd_device_allocator* allocator);
 
 int32_t gwamd_aligner_add_alignment(gwamd_aligner* aligner, const char* query, int32_t query_length,
                                     const char* target, int32_t target_length, int32_t reverse_complement_query,

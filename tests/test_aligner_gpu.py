@@ -269,3 +269,75 @@ def test_pipelined_align_all_matches_oracle(algo, monkeypatch):
     assert res["3"] == res["1"] and res["8"] == res["1"]
     want, _ = oracle.align_batch(pairs, dict(ALGOS)[algo], max(len(q) for q in qs))
     assert res["1"] == want
+
+
+def test_split_launch_after_pipelined_align_all(monkeypatch):
+    # a batch whose last align_all() ran pipelined, then driven
+    # through the split C ABI entry points (upload / launch / download) with
+    # the same pair count and no manual synchronize: sync_alignments must wait
+    # for this launch's download (not the old stages' events) and
+    # last_kernel_ms must time this launch
+    monkeypatch.setenv("GWAMD_DIAG", "1")
+    monkeypatch.setenv("GWAMD_ALIGNER_GRID", "1")
+    monkeypatch.setenv("GWAMD_ALIGNER_PIPELINE", "4")
+    qs, ts = synth.pairs(91, 1500, 300, 330, 10, 10, 10)
+    pairs = list(zip(qs, ts))
+    b = CudaAlignerBatch(max(len(q) for q in qs), max(len(t) for t in ts), len(pairs), algorithm="myers")
+    for q, t in pairs:
+        assert b.add_alignment(q, t) == 0
+    b.align_all()
+    b.sync_alignments()
+    first = [states(a) for a in b.get_alignments()]
+    # clear the aligner's host result buffers so stale results cannot pass
+    import ctypes as C
+    pp, ln, stride = C.c_void_p(), C.c_void_p(), C.c_int32()
+    b._lib.gwamd_aligner_get_paths(b._handle, C.byref(pp), C.byref(ln), C.byref(stride))
+    C.memset(pp, 0, len(pairs) * stride.value)
+    C.memset(ln, 0, len(pairs) * 4)
+    b.upload()
+    b.launch()
+    b.download()
+    b.sync_alignments()
+    assert b.last_kernel_ms() > 0
+    assert [states(a) for a in b.get_alignments()] == first
+    want, _ = oracle.align_batch(pairs, oracle.ALIGN_MYERS, max(len(q) for q in qs))
+    assert first == want
+
+
+def test_shared_allocator_pool_caps_aligners():
+    # create_default_device_allocator() is a 2 GiB pool
+    # (allocator.hpp:297-305) and copies of one allocator share it
+    # (shared_ptr<MemoryResource>, allocator.hpp:274-279): two aligners made
+    # from one 1 GiB allocator cannot jointly exceed it; the bytes come back
+    # when an aligner is destroyed
+    import gc
+    from claragenomicsanalysis_amd.cudaaligner import DeviceAllocator
+    assert DeviceAllocator().capacity == 2 << 30
+    pool = DeviceAllocator(1 << 30)
+    # 4,000 pairs x 5 kb on all resident slots would take several GiB
+    a1 = CudaAlignerBatch(5000, 5000, 4000, allocator=pool)
+    grid1, dev1 = a1.config()
+    assert 0 < pool.used <= pool.capacity
+    assert pool.used == dev1
+    try:
+        a2 = CudaAlignerBatch(5000, 5000, 4000, allocator=pool)
+        grid2, dev2 = a2.config()
+        assert pool.used == dev1 + dev2 <= pool.capacity
+        del a2
+    except RuntimeError:
+        pass  # nothing left for the fixed buffers plus one slot
+    assert pool.used == dev1
+    # the first aligner still aligns correctly on its capped slots
+    qs, ts = synth.pairs(5, 40, 5000, 5000, 166, 166, 166)
+    for q, t in zip(qs, ts):
+        assert a1.add_alignment(q, t) == 0
+    a1.align_all()
+    a1.sync_alignments()
+    want, _ = oracle.align_batch(list(zip(qs, ts)), oracle.ALIGN_HM, 5000)
+    assert [states(a) for a in a1.get_alignments()] == want
+    del a1
+    gc.collect()
+    assert pool.used == 0
+    # a pool too small for the fixed buffers plus one slot throws
+    with pytest.raises(RuntimeError):
+        CudaAlignerBatch(5000, 5000, 4000, allocator=DeviceAllocator(1 << 20))
