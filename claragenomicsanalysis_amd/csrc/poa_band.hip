@@ -161,6 +161,53 @@ __device__ __forceinline__ int band_pred2(WinGraph<SizeT> g, BandAux X, int r, u
     return r - int((k & 1) ? (w >> 16) : (w & 0xffffu));
 }
 
+// The aux arrays with global-typed pointers (see WinGraphG).
+struct BandAuxG
+{
+    GWAMD_GLB uint8_t* codes;
+    GWAMD_GLB const uint32_t* reca;
+    GWAMD_GLB const uint32_t* recb;
+    GWAMD_GLB const uint32_t* recc;
+    GWAMD_GLB int32_t* col0;
+    GWAMD_GLB uint8_t* flags;
+    GWAMD_GLB const int32_t* xl;
+};
+
+__device__ __forceinline__ BandAuxG typed_aux(const BandAux& X)
+{
+    BandAuxG t;
+    t.codes = (GWAMD_GLB uint8_t*)(X.codes);
+    t.reca  = (GWAMD_GLB const uint32_t*)(X.reca);
+    t.recb  = (GWAMD_GLB const uint32_t*)(X.recb);
+    t.recc  = (GWAMD_GLB const uint32_t*)(X.recc);
+    t.col0  = (GWAMD_GLB int32_t*)(X.col0);
+    t.flags = (GWAMD_GLB uint8_t*)(X.flags);
+    t.xl    = (GWAMD_GLB const int32_t*)(X.xl);
+    return t;
+}
+
+template <typename SizeT>
+__device__ __forceinline__ int band_pred2(const WinGraphG<SizeT>& g, const BandAuxG& X, int r, uint32_t a, uint32_t b,
+                                          uint32_t c, int k)
+{
+    const int np = ra_np(a);
+    if (np == 0)
+        return 0;
+    if (np == int(kNpEsc))
+        return pred_row(g, int(g.sorted[r - 1]), k);
+    if (b >> 31)
+        return int(X.xl[(b & 0x7fffffffu) + uint32_t(k)]);
+    const uint32_t w = k < 2 ? b : c;
+    return r - int((k & 1) ? (w >> 16) : (w & 0xffffu));
+}
+
+template <typename SizeT>
+__device__ __forceinline__ int band_np2(const WinGraphG<SizeT>& g, int r, uint32_t a, uint32_t b)
+{
+    const int np = ra_np(a);
+    return np == int(kNpEsc) ? int(g.in_cnt[int(g.sorted[r - 1])]) : np;
+}
+
 template <typename SizeT>
 __device__ __forceinline__ int band_np2(WinGraph<SizeT> g, int r, uint32_t a, uint32_t b)
 {

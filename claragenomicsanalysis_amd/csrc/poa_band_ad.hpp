@@ -82,8 +82,8 @@ struct AdCtx
     GWAMD_LDS const uint8_t* read;
     GWAMD_LDS ScoreT* ring;
     GWAMD_LDS ScoreT* sink; // kWave words: target of ring writes outside a row
-    ScoreT* spill;
-    uint8_t* codes;
+    GWAMD_GLB ScoreT* spill;
+    GWAMD_GLB uint8_t* codes;
     int rowsz, codes_bytes, spill_bytes;
     GWAMD_LDS AdShared* sh;
 };
@@ -142,13 +142,13 @@ __device__ __forceinline__ void ad_publish(GWAMD_LDS AdShared* sh, int blk, uint
 // Returns the lane's emission at column L (its row's sink candidate).  Rows
 // with C.store set also go to the HBM spill rows (see band_forward_ad).
 template <typename ScoreT, typename SizeT, int CPL, int NS, bool GEN>
-__device__ __forceinline__ int ad_block(const AdCtx<ScoreT>& C, WinGraph<SizeT> g, BandAux X)
+__device__ __forceinline__ int ad_block(const AdCtx<ScoreT>& C, const WinGraphG<SizeT>& g, const BandAuxG& X)
 {
     const int lane = C.lane, r = C.r, bw = C.bw, gap = C.gap, minv = C.minv;
     int mode[NS], dsh[NS], tcap[NS];
     bool valid[NS];
     GWAMD_LDS const ScoreT* sp[NS];
-    const ScoreT* gp[NS];
+    GWAMD_GLB const ScoreT* gp[NS];
     const int nslot = max(C.np, 1);
 #pragma unroll
     for (int s = 0; s < NS; s++)
@@ -174,7 +174,7 @@ __device__ __forceinline__ int ad_block(const AdCtx<ScoreT>& C, WinGraph<SizeT> 
         mode[s] = m;
         dsh[s]  = C.bs - bsp;
         sp[s]   = m == kAdLds ? C.ring + (p % kAdRing) * C.rowsz + off : C.ring;
-        gp[s]   = glb(m == kAdSpill ? C.spill + size_t(p) * C.rowsz + off : C.spill);
+        gp[s]   = m == kAdSpill ? C.spill + size_t(p) * C.rowsz + off : C.spill;
         tcap[s] = m == kAdSpill ? C.rowsz - 1 - off : C.T;
     }
     // block-uniform slot properties
@@ -202,8 +202,8 @@ __device__ __forceinline__ int ad_block(const AdCtx<ScoreT>& C, WinGraph<SizeT> 
     GWAMD_LDS ScoreT* dw        = C.sink + lane;
     // HBM: codes (idx 1..bw) and the spill row (idx 0..bw); lanes out of
     // range store into row 0 of both, which no reader uses (rows start at 1)
-    uint8_t* const codes = glb(C.codes);
-    uint8_t* const spillb = reinterpret_cast<uint8_t*>(glb(C.spill));
+    GWAMD_GLB uint8_t* const codes  = C.codes;
+    GWAMD_GLB uint8_t* const spillb = (GWAMD_GLB uint8_t*)(C.spill);
     const int coff = C.act ? r * bw + (k0 - 1) : 0; // + t: code of idx t + k0
     // + t*size: byte offset of the spill value of idx t + k0
     const uint32_t soff = C.act ? uint32_t(sizeof(ScoreT)) * uint32_t(r * C.rowsz + k0 + CPL - 1) : 0u;
@@ -351,8 +351,8 @@ __device__ __forceinline__ int ad_block(const AdCtx<ScoreT>& C, WinGraph<SizeT> 
         *(row ? wp + t : dw) = ScoreT(e);
         codes[cell ? uint32_t(coff + t) : uint32_t(lane)] = uint8_t(code);
         if (any_store)
-            *reinterpret_cast<ScoreT*>(spillb + (row && store ? soff + uint32_t(sizeof(ScoreT) * t)
-                                                               : uint32_t(sizeof(ScoreT) * lane))) = ScoreT(e);
+            *(GWAMD_GLB ScoreT*)(spillb + (row && store ? soff + uint32_t(sizeof(ScoreT) * t)
+                                                         : uint32_t(sizeof(ScoreT) * lane))) = ScoreT(e);
         sv  = t == tL ? e : sv;
         cur = e;
         }
@@ -423,14 +423,16 @@ __device__ __forceinline__ void band_ad_init(GWAMD_LDS ScoreT* ring, int rowsz, 
 #define GWAMD_BAND_AD_ATTR __noinline__
 #endif
 template <typename ScoreT, typename SizeT, int CPL>
-__device__ GWAMD_BAND_AD_ATTR void band_forward_ad(WinGraph<SizeT> g, BandAux X, int V, GWAMD_LDS const uint8_t* read,
+__device__ GWAMD_BAND_AD_ATTR void band_forward_ad(WinGraph<SizeT> g0, BandAux X0, int V, GWAMD_LDS const uint8_t* read,
                                                 int L, const Band& B, const Scores sc, GWAMD_LDS ScoreT* ring,
-                                                ScoreT* spill, int rowsz, int score_rows, int lane, int wave, int nw,
+                                                ScoreT* spill0, int rowsz, int score_rows, int lane, int wave, int nw,
                                                 GWAMD_LDS AdShared* sh, BandProf& bp)
 {
-    X     = as_global(X);
-    g     = as_global(g);
-    spill = glb(spill);
+    // global-typed views of the graph, aux arrays and spill rows: out of line,
+    // the struct arguments arrive with flat pointers
+    const WinGraphG<SizeT> g      = typed_graph(g0);
+    const BandAuxG X              = typed_aux(X0);
+    GWAMD_GLB ScoreT* const spill = (GWAMD_GLB ScoreT*)(spill0);
     const uint64_t f_t0 = BandProf::now();
     const int bw        = B.bw;
     const int minv      = int(band_min_value<ScoreT>(sc));

@@ -111,6 +111,38 @@ __device__ __forceinline__ int pred_row(WinGraph<SizeT> g, int node, int p)
     return int(g.pos[int(g.in_e[node * kMaxEdges + p])]) + 1;
 }
 
+// The graph with global-typed pointers, for functions kept out of line (their
+// struct arguments arrive with flat pointers, and a flat access counts against
+// the LDS wait counter too): the anti-diagonal banded pass.
+#ifndef GWAMD_GLB
+#define GWAMD_GLB __attribute__((address_space(1)))
+#endif
+template <typename SizeT>
+struct WinGraphG
+{
+    GWAMD_GLB const uint16_t* in_cnt;
+    GWAMD_GLB const SizeT* in_e;
+    GWAMD_GLB const SizeT* sorted;
+    GWAMD_GLB const SizeT* pos;
+};
+
+template <typename SizeT>
+__device__ __forceinline__ WinGraphG<SizeT> typed_graph(WinGraph<SizeT> g)
+{
+    WinGraphG<SizeT> t;
+    t.in_cnt = (GWAMD_GLB const uint16_t*)(g.in_cnt);
+    t.in_e   = (GWAMD_GLB const SizeT*)(g.in_e);
+    t.sorted = (GWAMD_GLB const SizeT*)(g.sorted);
+    t.pos    = (GWAMD_GLB const SizeT*)(g.pos);
+    return t;
+}
+
+template <typename SizeT>
+__device__ __forceinline__ int pred_row(const WinGraphG<SizeT>& g, int node, int p)
+{
+    return int(g.pos[int(g.in_e[node * kMaxEdges + p])]) + 1;
+}
+
 // ---------------------------------------------------------------------------
 // Backbone from read 0 (cudapoa_kernels.cuh:171-209), lane-parallel.
 template <typename SizeT, bool MSA>

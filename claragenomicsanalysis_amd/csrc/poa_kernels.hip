@@ -1364,8 +1364,8 @@ __global__ void __launch_bounds__(kWave * NW, W ? (NW >= 8 ? 2 : 1) : (NW >= 4 ?
             // level-keyed Kahn sort on every wave of the workgroup
             // (GWAMD_TOPSORT=fifo, Dims::diag bit 2, keeps the FIFO below)
             if (rc == kSuccess && !d.spoa_accurate && !(d.diag & 4))
-                lv_done = topsort_levels<SizeT>(g, nc, V, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, tid, kThr, cpred,
-                                                lv_hint);
+                lv_done = topsort_levels<SizeT, NW>(g, nc, V, (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off, tid, kThr,
+                                                    cpred, lv_hint);
             lv_hint = lv_done ? nc : 0; // cpred holds c(v) of this sort for the next one
             if (wave == 0)
             {
@@ -1448,11 +1448,21 @@ __global__ void __launch_bounds__(kWave * NW, W ? (NW >= 8 ? 2 : 1) : (NW >= 4 ?
 // workgroup, for the known-answer and random-DAG tests against the FIFO sort.
 template <typename SizeT>
 __global__ void __launch_bounds__(1024) topsort_levels_test_kernel(WinGraph<SizeT> g, int n, int n_prev, int scratch,
-                                                                   SizeT* hint, int n_hint, int* ok)
+                                                                   SizeT* hint, int n_hint, int* ok, uint64_t* prof)
 {
     extern __shared__ __align__(16) uint8_t lds[];
+#ifdef GWAMD_TOPSORT_PROFILE
+    uint64_t p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bool r = topsort_levels<SizeT>(g, n, n_prev, (GWAMD_LDS uint8_t*)(lds), scratch, int(threadIdx.x),
+                                         int(blockDim.x), hint, n_hint, p);
+    if (threadIdx.x == 0 && prof)
+        for (int k = 0; k < 8; k++)
+            prof[k] += p[k];
+#else
     const bool r = topsort_levels<SizeT>(g, n, n_prev, (GWAMD_LDS uint8_t*)(lds), scratch, int(threadIdx.x),
                                          int(blockDim.x), hint, n_hint);
+    (void)prof;
+#endif
     if (threadIdx.x == 0)
         *ok = r ? 1 : 0;
 }
@@ -1460,7 +1470,8 @@ __global__ void __launch_bounds__(1024) topsort_levels_test_kernel(WinGraph<Size
 template <typename SizeT>
 int topsort_levels_test(int n, int n_prev, int n_hint, const uint16_t* in_cnt, const int32_t* in_e,
                         const uint16_t* out_cnt, const int32_t* out_e, int32_t* hint, const int32_t* order_prev,
-                        int threads, int scratch, int32_t* sorted)
+                        int threads, int scratch, int32_t* sorted, int reps = 0, double* ms = nullptr,
+                        uint64_t* prof_out = nullptr)
 {
     const size_t ne = size_t(n) * kMaxEdges;
     std::vector<SizeT> ie(ne), oe(ne), hi(n, SizeT(0));
@@ -1474,6 +1485,7 @@ int topsort_levels_test(int n, int n_prev, int n_hint, const uint16_t* in_cnt, c
     uint16_t *d_ic = nullptr, *d_oc = nullptr;
     SizeT *d_ie = nullptr, *d_oe = nullptr, *d_sorted = nullptr, *d_pos = nullptr, *d_hint = nullptr;
     int* d_ok   = nullptr;
+    uint64_t* d_prof = nullptr;
     int ok      = 0;
     auto fin    = [&](int r) {
         (void)hipFree(d_ic);
@@ -1484,6 +1496,7 @@ int topsort_levels_test(int n, int n_prev, int n_hint, const uint16_t* in_cnt, c
         (void)hipFree(d_pos);
         (void)hipFree(d_hint);
         (void)hipFree(d_ok);
+        (void)hipFree(d_prof);
         return r;
     };
     if (n <= 0 || threads < 64 || threads > 1024 || threads % 64 || scratch < 0 || scratch > 163840 ||
@@ -1505,7 +1518,8 @@ int topsort_levels_test(int n, int n_prev, int n_hint, const uint16_t* in_cnt, c
     if (hipMalloc(&d_ic, n * 2) || hipMalloc(&d_oc, n * 2) || hipMalloc(&d_ie, ne * sizeof(SizeT)) ||
         hipMalloc(&d_oe, ne * sizeof(SizeT)) || hipMalloc(&d_sorted, n * sizeof(SizeT)) ||
         hipMalloc(&d_pos, n * sizeof(SizeT)) || hipMalloc(&d_hint, n * sizeof(SizeT)) ||
-        hipMalloc(&d_ok, sizeof(int)))
+        hipMalloc(&d_ok, sizeof(int)) || hipMalloc(&d_prof, 8 * sizeof(uint64_t)) ||
+        hipMemset(d_prof, 0, 8 * sizeof(uint64_t)))
         return fin(-1);
     if (hipMemcpy(d_ic, in_cnt, n * 2, hipMemcpyHostToDevice) || hipMemcpy(d_oc, out_cnt, n * 2, hipMemcpyHostToDevice) ||
         hipMemcpy(d_ie, ie.data(), ne * sizeof(SizeT), hipMemcpyHostToDevice) ||
@@ -1525,9 +1539,35 @@ int topsort_levels_test(int n, int n_prev, int n_hint, const uint16_t* in_cnt, c
                             hipFuncAttributeMaxDynamicSharedMemorySize, scratch))
         return fin(-1);
     hipLaunchKernelGGL(topsort_levels_test_kernel<SizeT>, dim3(1), dim3(threads), size_t(scratch), 0, g, n, n_prev,
-                       scratch, d_hint, n_hint, d_ok);
+                       scratch, d_hint, n_hint, d_ok, nullptr);
     if (hipGetLastError() || hipDeviceSynchronize() || hipMemcpy(&ok, d_ok, sizeof(int), hipMemcpyDeviceToHost))
         return fin(-1);
+    if (reps > 0)
+    {
+        // timing mode: the same sort `reps` times (the graph, previous order and
+        // hints are inputs only; the outputs are rewritten identically)
+        hipEvent_t e0, e1;
+        if (hipEventCreate(&e0) || hipEventCreate(&e1))
+            return fin(-1);
+        (void)hipEventRecord(e0, 0);
+        for (int k = 0; k < reps; k++)
+        {
+            if (hipMemcpy(d_sorted, so.data(), n * sizeof(SizeT), hipMemcpyHostToDevice))
+                return fin(-1);
+            hipLaunchKernelGGL(topsort_levels_test_kernel<SizeT>, dim3(1), dim3(threads), size_t(scratch), 0, g, n,
+                               n_prev, scratch, d_hint, n_hint, d_ok, d_prof);
+        }
+        (void)hipEventRecord(e1, 0);
+        float t = 0.f;
+        if (hipEventSynchronize(e1) || hipEventElapsedTime(&t, e0, e1))
+            return fin(-1);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        if (ms)
+            *ms = double(t) / reps;
+        if (prof_out && hipMemcpy(prof_out, d_prof, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost))
+            return fin(-1);
+    }
     std::vector<SizeT> s(n);
     if (hipMemcpy(s.data(), d_sorted, n * sizeof(SizeT), hipMemcpyDeviceToHost) ||
         hipMemcpy(hi.data(), d_hint, n * sizeof(SizeT), hipMemcpyDeviceToHost))
@@ -1550,6 +1590,23 @@ int topsort_levels_test(int n, int n_prev, int n_hint, const uint16_t* in_cnt, c
 // receives the final c(v)).  Returns 1 when the level sort produced sorted[],
 // 0 when it declined (the kernels then run the FIFO sort), negative on a HIP
 // error or bad arguments.
+// Timing mode of the same hook (scripts/topsort_bench.py): after the checked
+// run, `reps` more sorts; *ms gets the mean time per sort (HIP events around
+// launches of one workgroup, copies of the previous order included) and
+// prof[8] the section cycles of GWAMD_TOPSORT_PROFILE builds.
+extern "C" int gwamd_internal_topsort_levels_timed(int size_bits, int n, int n_prev, int n_hint,
+                                                   const uint16_t* in_cnt, const int32_t* in_e,
+                                                   const uint16_t* out_cnt, const int32_t* out_e, int32_t* hint,
+                                                   const int32_t* order_prev, int threads, int scratch,
+                                                   int32_t* sorted, int reps, double* ms, uint64_t* prof)
+{
+    if (size_bits == 16)
+        return gwamd::poa::topsort_levels_test<int16_t>(n, n_prev, n_hint, in_cnt, in_e, out_cnt, out_e, hint,
+                                                        order_prev, threads, scratch, sorted, reps, ms, prof);
+    return gwamd::poa::topsort_levels_test<int32_t>(n, n_prev, n_hint, in_cnt, in_e, out_cnt, out_e, hint, order_prev,
+                                                    threads, scratch, sorted, reps, ms, prof);
+}
+
 extern "C" int gwamd_internal_topsort_levels(int size_bits, int n, int n_prev, int n_hint, const uint16_t* in_cnt,
                                              const int32_t* in_e, const uint16_t* out_cnt, const int32_t* out_e,
                                              int32_t* hint, const int32_t* order_prev, int threads, int scratch,

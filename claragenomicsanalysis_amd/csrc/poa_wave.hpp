@@ -1476,14 +1476,19 @@ __device__ __forceinline__ bool topsort_lds_big(WinGraph<SizeT> g, int n, GWAMD_
 constexpr int kLvIters  = 32;
 constexpr int kLvRounds = 40;
 constexpr int kLvU      = 4; // nodes per thread whose HBM loads are issued together
-constexpr int kLvE      = 8; // edge slots loaded with a node's counts
-constexpr int kLvC      = 16; // nodes per chunk of the in-order pass (their loads issued together)
+constexpr int kLvE      = 4; // edge slots loaded with a node's counts (more: a loop, rare)
+constexpr int kLvC      = 8; // nodes per chunk of the in-order pass (their loads issued together)
+constexpr int kLvT      = 2; // multi-parent nodes per batch of the candidate-table loop
 #ifdef GWAMD_TS_INLINE // diagnostic builds: the sort inlined into its kernels
 #define GWAMD_TS_ATTR __forceinline__
 #else
 #define GWAMD_TS_ATTR __noinline__
 #endif
-template <typename SizeT>
+// kInst: one instantiation per calling kernel family (an out-of-line function
+// is register-allocated for the most constrained of its callers; the LDS
+// kernel's 4-wave diagnostic shapes would hold config B's 2-wave kernel to
+// their 128 registers).
+template <typename SizeT, int kInst = 0>
 __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_prev, GWAMD_LDS uint8_t* scratch,
                                              int scratch_bytes, int tid, int nthr, SizeT* hint, int n_hint,
                                              uint64_t* prof = nullptr)
@@ -1500,7 +1505,9 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
     GWAMD_GLB SizeT* g_hint             = glb_of(hint);
     const int N8             = (n + 7) & ~7;
     const int nmw            = (n + 31) / 32; // anchor mask words
-    const int need           = 128 + 9 * N8 + 4 * ((nmw + 3) & ~3);
+    const int kt             = max(16, N8 / 64); // parent-candidate table entries (16 bytes each)
+    const int acap           = max(64, N8 / 4);  // anchor list entries (u16), in the same region
+    const int need           = 128 + 9 * N8 + 4 * ((nmw + 3) & ~3) + max(16 * kt, 2 * acap);
     n_prev                   = min(max(n_prev, 0), n);
     if (n <= 0 || n > 65535 || need > scratch_bytes)
         return false;
@@ -1521,6 +1528,8 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
     GWAMD_LDS uint16_t* bkt  = cc + N8;                                       // in-list cache, then level buckets
     GWAMD_LDS uint8_t* meta  = (GWAMD_LDS uint8_t*)(bkt + N8);                // 0x80 multi-pred | 0x40 multi-parent | ic/slot
     GWAMD_LDS uint32_t* mask = (GWAMD_LDS uint32_t*)(meta + N8);              // anchor bits
+    GWAMD_LDS uint32_t* ctab = mask + ((nmw + 3) & ~3); // per multi-parent node: 3 x (candidate | slot << 16)
+    GWAMD_LDS uint16_t* alist = (GWAMD_LDS uint16_t*)(ctab); // anchors during the iterations
     const int wave           = tid / kWave;
     const int lane           = tid & (kWave - 1);
     const int nwaves         = nthr / kWave;
@@ -1569,6 +1578,7 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
         ctl[1] = 0;
         ctl[2] = 0;
         ctl[3] = 0;
+        ctl[20] = 0; // candidate-table entries in use
     }
     int ctotal          = 0;
     const int cbase     = wg_excl_sum(mine, ctotal);
@@ -1596,7 +1606,7 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
             {
                 const int v = v0 + u * nthr;
                 if (v >= n)
-                    break;
+                    continue; // (not break: the loop must unroll, its arrays stay in registers)
                 int c = v;
                 if (ic[u] > 0)
                     c = hv[u] != v ? hv[u] : int(ev[u][0]);
@@ -1649,7 +1659,7 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
         // as an anchor
         {
             uint32_t pv = 0xffffffffu, pw = 0, last_mark = 0xffffffffu;
-            auto seq_chunk = [&](const int* vs, int cnt) {
+            auto seq_chunk = [&](const int(&vs)[kLvC], int cnt) {
                 int cs[kLvC];
                 uint32_t wc[kLvC];
 #pragma unroll
@@ -1662,7 +1672,7 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
                 for (int u = 0; u < kLvC; u++)
                 {
                     if (u >= cnt)
-                        break;
+                        continue; // (not break: the loop must unroll, its arrays stay in registers)
                     const uint32_t v = uint32_t(vs[u]), c = uint32_t(cs[u]);
                     if (c == v)
                         continue; // a source keeps (v, 0)
@@ -1711,29 +1721,77 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
         }
         __syncthreads();
         lap(2);
+        // the anchors as a list (batched rounds: every anchor's two reads in
+        // flight together instead of one dependent pair after another), or
+        // the mask walk when the list would not fit
+        int na_mine = 0;
+        for (int k = tid; k < nmw; k += nthr)
+            na_mine += __popc(mask[k]);
+        int na_total      = 0;
+        const int na_base = wg_excl_sum(na_mine, na_total);
+        const bool alist_ok = na_total <= acap; // uniform
+        if (alist_ok)
+        {
+            int pos = na_base;
+            for (int k = tid; k < nmw; k += nthr)
+            {
+                uint32_t bits = mask[k];
+                while (bits)
+                {
+                    alist[pos++] = uint16_t(k * 32 + __builtin_ctz(bits));
+                    bits &= bits - 1;
+                }
+            }
+            __syncthreads();
+        }
         // pointer jumping among the anchors only (an anchor's own word ends on
         // an anchor or a source)
         bool conv = false;
         for (int round = 0; round < kLvRounds; round++)
         {
             bool ch = false;
-            for (int k = tid; k < nmw; k += nthr)
+            if (alist_ok)
             {
-                uint32_t bits = mask[k];
-                while (bits)
+                for (int i0 = tid; i0 < na_total; i0 += kLvB * nthr)
                 {
-                    const int a = k * 32 + __builtin_ctz(bits);
-                    bits &= bits - 1;
-                    const uint32_t wa = word[a];
-                    const uint32_t x  = wa & 0xffffu;
-                    const uint32_t wx = word[x];
-                    if ((wx & 0xffffu) != x)
-                    {
-                        word[a] = (wx & 0xffffu) | ((wa & 0xffff0000u) + (wx & 0xffff0000u));
-                        ch      = true;
-                    }
+                    int a[kLvB];
+                    uint32_t wa[kLvB], wx[kLvB];
+#pragma unroll
+                    for (int u = 0; u < kLvB; u++)
+                        a[u] = alist[min(i0 + u * nthr, na_total - 1)];
+#pragma unroll
+                    for (int u = 0; u < kLvB; u++)
+                        wa[u] = word[a[u]];
+#pragma unroll
+                    for (int u = 0; u < kLvB; u++)
+                        wx[u] = word[wa[u] & 0xffffu];
+#pragma unroll
+                    for (int u = 0; u < kLvB; u++)
+                        if (i0 + u * nthr < na_total && (wx[u] & 0xffffu) != (wa[u] & 0xffffu))
+                        {
+                            word[a[u]] = (wx[u] & 0xffffu) | ((wa[u] & 0xffff0000u) + (wx[u] & 0xffff0000u));
+                            ch         = true;
+                        }
                 }
             }
+            else
+                for (int k = tid; k < nmw; k += nthr)
+                {
+                    uint32_t bits = mask[k];
+                    while (bits)
+                    {
+                        const int a = k * 32 + __builtin_ctz(bits);
+                        bits &= bits - 1;
+                        const uint32_t wa = word[a];
+                        const uint32_t x  = wa & 0xffffu;
+                        const uint32_t wx = word[x];
+                        if ((wx & 0xffffu) != x)
+                        {
+                            word[a] = (wx & 0xffffu) | ((wa & 0xffff0000u) + (wx & 0xffff0000u));
+                            ch      = true;
+                        }
+                    }
+                }
             r++;
             rounds_total++;
             if (ch)
@@ -1867,7 +1925,7 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
     lap(4);
 #ifdef GWAMD_TOPSORT_PROFILE
     if (prof && tid == 0)
-        (void)0; // (slot 7 times the outputs)
+        prof[7] += uint64_t(rounds_total) * 1000000000ull; // (outputs time below 1e9)
     (void)rounds_total;
 #endif
     if (!ok)
@@ -1974,7 +2032,7 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
         {
             const int v = v0 + u * nthr;
             if (v >= n)
-                break;
+                continue; // (not break: the loop must unroll, its arrays stay in registers)
             g_hint[v] = SizeT(par[u]);
             if (le[u] - lo[u] == 1)
                 cc[v] = uint16_t(lo[u]);
@@ -1991,82 +2049,253 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
             }
         }
     }
+    // members of multi-node levels with two or three predecessors one level
+    // below: the candidates and the node's slot in each one's out-list into the
+    // table (loads of kLvT nodes issued together; cc[v] becomes the entry,
+    // meta's low bits 63); others keep the sequential lookup in 3b
+    for (int v0 = tid; v0 < n; v0 += kLvT * nthr)
+    {
+        int lvl[kLvT], ic[kLvT], cand[kLvT][3], nc[kLvT], oc[kLvT][3];
+        bool want[kLvT];
+        SizeT iv[kLvT][kLvE], ov[kLvT][3][kLvE];
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < kLvT; u++)
+        {
+            const int v  = min(v0 + u * nthr, n - 1);
+            const int mt = meta[v];
+            lvl[u]       = int(word[v] >> 16);
+            ic[u]        = mt & 63;
+            want[u]      = v0 + u * nthr < n && (mt & 0x40) != 0 && lvl[u] > 0 && ic[u] <= kLvE &&
+                      lv_end(lvl[u]) - lv_off(lvl[u]) > 1;
+            any          = any || want[u];
+        }
+        // (about one node in a hundred: the wave skips the batch when none of
+        // its lanes has one, every instruction below is issued otherwise)
+        if (__builtin_amdgcn_ballot_w64(any) == 0)
+            continue;
+#pragma unroll
+        for (int u = 0; u < kLvT; u++)
+        {
+            const int v = min(v0 + u * nthr, n - 1);
+#pragma unroll
+            for (int e = 0; e < kLvE; e++)
+                iv[u][e] = want[u] && e < ic[u] ? g_in_e[v * kMaxEdges + e] : SizeT(0);
+        }
+#pragma unroll
+        for (int u = 0; u < kLvT; u++)
+        {
+            nc[u]      = 0;
+            cand[u][0] = cand[u][1] = cand[u][2] = 0;
+#pragma unroll
+            for (int e = 0; e < kLvE; e++)
+            {
+                const int p = int(iv[u][e]);
+                if (want[u] && e < ic[u] && int(word[p] >> 16) == lvl[u] - 1)
+                {
+                    // (selects, not cand[u][nc[u]]: a runtime index would put
+                    // the array in scratch memory)
+                    cand[u][0] = nc[u] == 0 ? p : cand[u][0];
+                    cand[u][1] = nc[u] == 1 ? p : cand[u][1];
+                    cand[u][2] = nc[u] == 2 ? p : cand[u][2];
+                    nc[u]++;
+                }
+            }
+            want[u] = want[u] && nc[u] <= 3;
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+            {
+                const bool live = want[u] && k < nc[u];
+                oc[u][k]        = live ? int(g_out_cnt[cand[u][k]]) : 0;
+#pragma unroll
+                for (int e = 0; e < kLvE; e++)
+                    ov[u][k][e] = live ? g_out_e[cand[u][k] * kMaxEdges + e] : SizeT(0);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kLvT; u++)
+        {
+            if (!want[u])
+                continue;
+            const int v = v0 + u * nthr;
+            uint32_t ent[3];
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+            {
+                int slot = 0;
+                if (k < nc[u])
+                {
+#pragma unroll
+                    for (int e = 0; e < kLvE; e++)
+                        slot = (e < oc[u][k] && int(ov[u][k][e]) == v) ? e : slot;
+                    for (int e = kLvE; e < oc[u][k]; e++)
+                        if (int(g_out_e[cand[u][k] * kMaxEdges + e]) == v)
+                            slot = e;
+                }
+                ent[k] = k < nc[u] ? (uint32_t(cand[u][k]) | (uint32_t(slot) << 16)) : 0xffffffffu;
+            }
+            const int idx =
+                __hip_atomic_fetch_add(&ctl[20], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (idx < kt)
+            {
+                ctab[4 * idx]     = ent[0];
+                ctab[4 * idx + 1] = ent[1];
+                ctab[4 * idx + 2] = ent[2];
+                cc[v]             = uint16_t(idx);
+                meta[v]           = uint8_t(0xc0 | 63);
+            }
+        }
+    }
     __syncthreads();
     lap(5);
-    // 3b. runs of multi-node levels, one lane per run
-    bool fail = false;
-    for (int l = tid; l < n; l += nthr)
-    {
-        int lo = lv_off(l), le = lv_end(l);
-        if (le - lo <= 1 || (l > 0 && lo - lv_off(l - 1) > 1))
-            continue;
-        int plo = l > 0 ? lv_off(l - 1) : 0;
-        for (int ll = l;;)
+    // 3b. runs of multi-node levels, one lane per run.  The key of a member
+    // v of level ll: (rank of its parent in level ll-1, slot of v in the
+    // parent's out-list), or v itself at level 0.
+    auto key_of = [&](int v, int ll, int plo, int m, int c) -> int {
+        if (ll == 0)
+            return v;
+        int par = c, slot = m & 63;
+        if ((m & 0x7f) == 0x40 + 63)
         {
-            // keys (rank of the parent in the level below, out-slot), or the
-            // node id at level 0, in place of c(v)
-            for (int i = lo; i < le; i++)
+            // several predecessors one level below, from the table: the one
+            // placed last
+            GWAMD_LDS const uint32_t* ent = ctab + 4 * c;
+            par                           = -1;
+            slot                          = 0;
+            int bp                        = -1;
+#pragma unroll
+            for (int k = 0; k < 3; k++)
             {
-                const int v = bkt[i];
-                int key     = v;
-                if (ll > 0)
+                const uint32_t x = ent[k];
+                if (x != 0xffffffffu && int(cc[x & 0xffffu]) > bp)
                 {
-                    int par, slot;
-                    if (meta[v] & 0x40)
-                    {
-                        // several predecessors one level below: the one placed last
-                        const int ic = meta[v] & 63;
-                        par          = -1;
-                        int bp       = -1;
-                        for (int e = 0; e < ic; e++)
-                        {
-                            const int p = int(g_in_e[v * kMaxEdges + e]);
-                            if (int(word[p] >> 16) == ll - 1 && int(cc[p]) > bp)
-                            {
-                                bp  = cc[p];
-                                par = p;
-                            }
-                        }
-                        const int oc = int(g_out_cnt[par]);
-                        slot         = 0;
-                        for (int s = 0; s < oc; s++)
-                            if (int(g_out_e[par * kMaxEdges + s]) == v)
-                                slot = s;
-                    }
-                    else
-                    {
-                        par  = cc[v];
-                        slot = meta[v] & 63;
-                    }
-                    const int pr = int(cc[par]) - plo;
-                    fail         = fail || pr >= 1024;
-                    key          = (pr << 6) | slot;
+                    bp   = cc[x & 0xffffu];
+                    par  = int(x & 0xffffu);
+                    slot = int(x >> 16);
                 }
-                cc[v] = uint16_t(key);
             }
-            fail = fail || le - lo > 255;
-            for (int i = lo; i < le; i++)
+        }
+        else if (m & 0x40)
+        {
+            // not in the table (more candidates or edges than it keeps): the
+            // in-list and the parent's out-list from HBM
+            const int ic = m & 63;
+            par          = -1;
+            int bp       = -1;
+            for (int e = 0; e < ic; e++)
             {
-                const int v = bkt[i];
-                const int k = cc[v];
-                int rank    = 0;
-                for (int j = lo; j < le; j++)
-                    rank += int(cc[bkt[j]]) < k ? 1 : 0;
-                meta[v] = uint8_t(rank);
+                const int p = int(g_in_e[v * kMaxEdges + e]);
+                if (int(word[p] >> 16) == ll - 1 && int(cc[p]) > bp)
+                {
+                    bp  = cc[p];
+                    par = p;
+                }
             }
-            for (int i = lo; i < le; i++)
+            const int oc = int(g_out_cnt[par]);
+            slot         = 0;
+            for (int s = 0; s < oc; s++)
+                if (int(g_out_e[par * kMaxEdges + s]) == v)
+                    slot = s;
+        }
+        return ((int(cc[par]) - plo) << 6) | slot;
+    };
+    bool fail = false;
+    constexpr int kLvS = 8; // levels whose bounds are loaded together by the scan
+    constexpr int kLvM = 4; // members of a level kept in registers
+    for (int l0 = tid; l0 < n; l0 += kLvS * nthr)
+    {
+        uint32_t wl[kLvS], wp[kLvS], wq[kLvS];
+#pragma unroll
+        for (int u = 0; u < kLvS; u++)
+        {
+            const int l = min(l0 + u * nthr, n - 1);
+            wl[u]       = word[l];
+            wp[u]       = l > 0 ? word[l - 1] : 0u;
+            wq[u]       = l > 1 ? word[l - 2] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kLvS; u++)
+        {
+            const int l = l0 + u * nthr;
+            int lo      = l > 0 ? int(wp[u] & 0xffffu) : 0;
+            int le      = int(wl[u] & 0xffffu);
+            const int pl = l > 1 ? int(wq[u] & 0xffffu) : 0;
+            if (l >= n || le - lo <= 1 || (l > 0 && lo - pl > 1))
+                continue;
+            int plo = l > 0 ? pl : 0;
+            for (int ll = l;;)
             {
-                const int v = bkt[i];
-                cc[v]       = uint16_t(lo + meta[v]);
+                const int m = le - lo;
+                if (m <= kLvM)
+                {
+                    // members, their records and parents' positions in
+                    // registers; ranks by comparing the keys
+                    int v[kLvM], mt[kLvM], c[kLvM], key[kLvM];
+#pragma unroll
+                    for (int k = 0; k < kLvM; k++)
+                        v[k] = bkt[lo + min(k, m - 1)];
+#pragma unroll
+                    for (int k = 0; k < kLvM; k++)
+                    {
+                        mt[k] = meta[v[k]];
+                        c[k]  = cc[v[k]];
+                    }
+#pragma unroll
+                    for (int k = 0; k < kLvM; k++)
+                        key[k] = (ll == 0 || (mt[k] & 0x40)) ? -1 : (((int(cc[c[k]]) - plo) << 6) | (mt[k] & 63));
+#pragma unroll
+                    for (int k = 0; k < kLvM; k++)
+                        if (key[k] < 0 && k < m)
+                            key[k] = key_of(v[k], ll, plo, mt[k], c[k]);
+#pragma unroll
+                    for (int k = 0; k < kLvM; k++)
+                        fail = fail || (k < m && key[k] >= (1024 << 6));
+#pragma unroll
+                    for (int k = 0; k < kLvM; k++)
+                    {
+                        int rank = 0;
+#pragma unroll
+                        for (int j = 0; j < kLvM; j++)
+                            rank += (j < m && key[j] < key[k]) ? 1 : 0;
+                        if (k < m)
+                            cc[v[k]] = uint16_t(lo + rank);
+                    }
+                }
+                else
+                {
+                    // wide level: keys in place of c(v), ranks through LDS
+                    for (int i = lo; i < le; i++)
+                    {
+                        const int v   = bkt[i];
+                        const int key = key_of(v, ll, plo, meta[v], cc[v]);
+                        fail          = fail || key >= (1024 << 6);
+                        cc[v]         = uint16_t(key);
+                    }
+                    fail = fail || m > 255;
+                    for (int i = lo; i < le; i++)
+                    {
+                        const int v = bkt[i];
+                        const int k = cc[v];
+                        int rank    = 0;
+                        for (int j = lo; j < le; j++)
+                            rank += int(cc[bkt[j]]) < k ? 1 : 0;
+                        meta[v] = uint8_t(rank);
+                    }
+                    for (int i = lo; i < le; i++)
+                    {
+                        const int v = bkt[i];
+                        cc[v]       = uint16_t(lo + meta[v]);
+                    }
+                }
+                ll++;
+                if (ll >= n)
+                    break;
+                plo = lo;
+                lo  = le;
+                le  = lv_end(ll);
+                if (le - lo <= 1)
+                    break;
             }
-            ll++;
-            if (ll >= n)
-                break;
-            plo = lo;
-            lo  = le;
-            le  = lv_end(ll);
-            if (le - lo <= 1)
-                break;
         }
     }
     if (fail)
