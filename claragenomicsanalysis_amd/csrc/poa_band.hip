@@ -1458,7 +1458,7 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
 
     PhaseTimer ph;
     BandProf bp;
-    uint64_t tsprof[8] = {0, 0, 0, 0, 0, 0, 0, 0}; // topsort sections (GWAMD_TOPSORT_PROFILE builds)
+    uint64_t tsprof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; // topsort sections (GWAMD_TOPSORT_PROFILE builds)
     uint64_t addprof[8] = {0, 0, 0, 0, 0, 0, 0, 0}; // add sections (GWAMD_ADD_PROFILE builds)
     const WindowDesc wd = b.windows[w];
     const int nseq      = wd.num_seqs;

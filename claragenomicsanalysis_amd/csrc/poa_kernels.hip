@@ -1452,11 +1452,11 @@ __global__ void __launch_bounds__(1024) topsort_levels_test_kernel(WinGraph<Size
 {
     extern __shared__ __align__(16) uint8_t lds[];
 #ifdef GWAMD_TOPSORT_PROFILE
-    uint64_t p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t p[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const bool r = topsort_levels<SizeT>(g, n, n_prev, (GWAMD_LDS uint8_t*)(lds), scratch, int(threadIdx.x),
                                          int(blockDim.x), hint, n_hint, p);
     if (threadIdx.x == 0 && prof)
-        for (int k = 0; k < 8; k++)
+        for (int k = 0; k < 10; k++)
             prof[k] += p[k];
 #else
     const bool r = topsort_levels<SizeT>(g, n, n_prev, (GWAMD_LDS uint8_t*)(lds), scratch, int(threadIdx.x),
@@ -1518,8 +1518,8 @@ int topsort_levels_test(int n, int n_prev, int n_hint, const uint16_t* in_cnt, c
     if (hipMalloc(&d_ic, n * 2) || hipMalloc(&d_oc, n * 2) || hipMalloc(&d_ie, ne * sizeof(SizeT)) ||
         hipMalloc(&d_oe, ne * sizeof(SizeT)) || hipMalloc(&d_sorted, n * sizeof(SizeT)) ||
         hipMalloc(&d_pos, n * sizeof(SizeT)) || hipMalloc(&d_hint, n * sizeof(SizeT)) ||
-        hipMalloc(&d_ok, sizeof(int)) || hipMalloc(&d_prof, 8 * sizeof(uint64_t)) ||
-        hipMemset(d_prof, 0, 8 * sizeof(uint64_t)))
+        hipMalloc(&d_ok, sizeof(int)) || hipMalloc(&d_prof, 10 * sizeof(uint64_t)) ||
+        hipMemset(d_prof, 0, 10 * sizeof(uint64_t)))
         return fin(-1);
     if (hipMemcpy(d_ic, in_cnt, n * 2, hipMemcpyHostToDevice) || hipMemcpy(d_oc, out_cnt, n * 2, hipMemcpyHostToDevice) ||
         hipMemcpy(d_ie, ie.data(), ne * sizeof(SizeT), hipMemcpyHostToDevice) ||
@@ -1565,7 +1565,7 @@ int topsort_levels_test(int n, int n_prev, int n_hint, const uint16_t* in_cnt, c
         (void)hipEventDestroy(e1);
         if (ms)
             *ms = double(t) / reps;
-        if (prof_out && hipMemcpy(prof_out, d_prof, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost))
+        if (prof_out && hipMemcpy(prof_out, d_prof, 10 * sizeof(uint64_t), hipMemcpyDeviceToHost))
             return fin(-1);
     }
     std::vector<SizeT> s(n);
@@ -1593,7 +1593,8 @@ int topsort_levels_test(int n, int n_prev, int n_hint, const uint16_t* in_cnt, c
 // Timing mode of the same hook (scripts/topsort_bench.py): after the checked
 // run, `reps` more sorts; *ms gets the mean time per sort (HIP events around
 // launches of one workgroup, copies of the previous order included) and
-// prof[8] the section cycles of GWAMD_TOPSORT_PROFILE builds.
+// prof[10] the section cycles, anchors and iterations of GWAMD_TOPSORT_PROFILE
+// builds.
 extern "C" int gwamd_internal_topsort_levels_timed(int size_bits, int n, int n_prev, int n_hint,
                                                    const uint16_t* in_cnt, const int32_t* in_e,
                                                    const uint16_t* out_cnt, const int32_t* out_e, int32_t* hint,

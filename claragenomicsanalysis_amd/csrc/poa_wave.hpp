@@ -1478,7 +1478,6 @@ constexpr int kLvRounds = 40;
 constexpr int kLvU      = 4; // nodes per thread whose HBM loads are issued together
 constexpr int kLvE      = 4; // edge slots loaded with a node's counts (more: a loop, rare)
 constexpr int kLvC      = 8; // nodes per chunk of the in-order pass (their loads issued together)
-constexpr int kLvT      = 2; // multi-parent nodes per batch of the candidate-table loop
 #ifdef GWAMD_TS_INLINE // diagnostic builds: the sort inlined into its kernels
 #define GWAMD_TS_ATTR __forceinline__
 #else
@@ -1505,9 +1504,8 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
     GWAMD_GLB SizeT* g_hint             = glb_of(hint);
     const int N8             = (n + 7) & ~7;
     const int nmw            = (n + 31) / 32; // anchor mask words
-    const int kt             = max(16, N8 / 64); // parent-candidate table entries (16 bytes each)
-    const int acap           = max(64, N8 / 4);  // anchor list entries (u16), in the same region
-    const int need           = 128 + 9 * N8 + 4 * ((nmw + 3) & ~3) + max(16 * kt, 2 * acap);
+    const int acap           = max(64, N8 / 4); // anchor list entries (u16)
+    const int need           = 128 + 9 * N8 + 4 * ((nmw + 3) & ~3) + 2 * acap;
     n_prev                   = min(max(n_prev, 0), n);
     if (n <= 0 || n > 65535 || need > scratch_bytes)
         return false;
@@ -1528,8 +1526,7 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
     GWAMD_LDS uint16_t* bkt  = cc + N8;                                       // in-list cache, then level buckets
     GWAMD_LDS uint8_t* meta  = (GWAMD_LDS uint8_t*)(bkt + N8);                // 0x80 multi-pred | 0x40 multi-parent | ic/slot
     GWAMD_LDS uint32_t* mask = (GWAMD_LDS uint32_t*)(meta + N8);              // anchor bits
-    GWAMD_LDS uint32_t* ctab = mask + ((nmw + 3) & ~3); // per multi-parent node: 3 x (candidate | slot << 16)
-    GWAMD_LDS uint16_t* alist = (GWAMD_LDS uint16_t*)(ctab); // anchors during the iterations
+    GWAMD_LDS uint16_t* alist = (GWAMD_LDS uint16_t*)(mask + ((nmw + 3) & ~3)); // anchors during the iterations
     const int wave           = tid / kWave;
     const int lane           = tid & (kWave - 1);
     const int nwaves         = nthr / kWave;
@@ -1578,7 +1575,6 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
         ctl[1] = 0;
         ctl[2] = 0;
         ctl[3] = 0;
-        ctl[20] = 0; // candidate-table entries in use
     }
     int ctotal          = 0;
     const int cbase     = wg_excl_sum(mine, ctotal);
@@ -1629,8 +1625,10 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
     int r   = 0; // flag generation: slot r & 1 holds r when some thread raised it
     bool ok = false;
     int rounds_total = 0;
+    int it_done      = 0;
     for (int it = 0; it < kLvIters; it++)
     {
+        it_done = it + 1;
         // reset: every word (c(v), 1), sources (v, 0); anchor bits cleared
         for (int v0 = tid; v0 < n; v0 += kLvB * nthr)
         {
@@ -1658,7 +1656,12 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
         // chains collapse in one pass; every ancestor a word ends on is marked
         // as an anchor
         {
-            uint32_t pv = 0xffffffffu, pw = 0, last_mark = 0xffffffffu;
+            // the last four nodes this thread placed and their fresh words: in
+            // level order a node's critical predecessor is usually one of them
+            // (parallel branches interleave), so its word comes from a
+            // register and the chain does not break into a new anchor
+            uint32_t pv = 0xffffffffu, pw = 0, pv1 = 0xffffffffu, pw1 = 0, pv2 = 0xffffffffu, pw2 = 0,
+                     pv3 = 0xffffffffu, pw3 = 0, last_mark = 0xffffffffu;
             auto seq_chunk = [&](const int(&vs)[kLvC], int cnt) {
                 int cs[kLvC];
                 uint32_t wc[kLvC];
@@ -1674,20 +1677,24 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
                     if (u >= cnt)
                         continue; // (not break: the loop must unroll, its arrays stay in registers)
                     const uint32_t v = uint32_t(vs[u]), c = uint32_t(cs[u]);
-                    if (c == v)
-                        continue; // a source keeps (v, 0)
-                    const uint32_t b = c == pv ? pw : wc[u];
-                    const uint32_t w = (b & 0xffffu) | ((b & 0xffff0000u) + (1u << 16));
-                    word[v]          = w;
-                    const uint32_t a = w & 0xffffu;
-                    if (a != last_mark)
+                    uint32_t w       = v; // a source keeps (v, 0)
+                    if (c != v)
                     {
-                        __hip_atomic_fetch_or(&mask[a >> 5], 1u << (a & 31), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-                        last_mark = a;
+                        const uint32_t b = c == pv ? pw : (c == pv1 ? pw1 : (c == pv2 ? pw2 : (c == pv3 ? pw3 : wc[u])));
+                        w                = (b & 0xffffu) | ((b & 0xffff0000u) + (1u << 16));
+                        word[v]          = w;
+                        const uint32_t a = w & 0xffffu;
+                        if (a != last_mark)
+                        {
+                            __hip_atomic_fetch_or(&mask[a >> 5], 1u << (a & 31), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+                            last_mark = a;
+                        }
                     }
-                    pv = v;
-                    pw = w;
+                    pv3 = pv2, pw3 = pw2;
+                    pv2 = pv1, pw2 = pw1;
+                    pv1 = pv, pw1 = pw;
+                    pv = v, pw = w;
                 }
             };
             const int ro = (n_prev + nthr - 1) / nthr;
@@ -1707,7 +1714,7 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
                     nx[u] = q + kLvC + u < q1 ? g_sorted[q + kLvC + u] : SizeT(0);
                 seq_chunk(vs, min(kLvC, q1 - q));
             }
-            pv = 0xffffffffu;
+            pv = pv1 = pv2 = pv3 = 0xffffffffu;
             const int rn = (n - n_prev + nthr - 1) / nthr;
             const int i0 = n_prev + min(tid * rn, n - n_prev), i1 = min(i0 + rn, n);
             for (int i = i0; i < i1; i += kLvC)
@@ -1925,7 +1932,11 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
     lap(4);
 #ifdef GWAMD_TOPSORT_PROFILE
     if (prof && tid == 0)
+    {
         prof[7] += uint64_t(rounds_total) * 1000000000ull; // (outputs time below 1e9)
+        prof[8] += uint64_t(ctl[3]);                        // anchors over the iterations
+        prof[9] += uint64_t(it_done);                       // iterations
+    }
     (void)rounds_total;
 #endif
     if (!ok)
@@ -2049,103 +2060,6 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
             }
         }
     }
-    // members of multi-node levels with two or three predecessors one level
-    // below: the candidates and the node's slot in each one's out-list into the
-    // table (loads of kLvT nodes issued together; cc[v] becomes the entry,
-    // meta's low bits 63); others keep the sequential lookup in 3b
-    for (int v0 = tid; v0 < n; v0 += kLvT * nthr)
-    {
-        int lvl[kLvT], ic[kLvT], cand[kLvT][3], nc[kLvT], oc[kLvT][3];
-        bool want[kLvT];
-        SizeT iv[kLvT][kLvE], ov[kLvT][3][kLvE];
-        bool any = false;
-#pragma unroll
-        for (int u = 0; u < kLvT; u++)
-        {
-            const int v  = min(v0 + u * nthr, n - 1);
-            const int mt = meta[v];
-            lvl[u]       = int(word[v] >> 16);
-            ic[u]        = mt & 63;
-            want[u]      = v0 + u * nthr < n && (mt & 0x40) != 0 && lvl[u] > 0 && ic[u] <= kLvE &&
-                      lv_end(lvl[u]) - lv_off(lvl[u]) > 1;
-            any          = any || want[u];
-        }
-        // (about one node in a hundred: the wave skips the batch when none of
-        // its lanes has one, every instruction below is issued otherwise)
-        if (__builtin_amdgcn_ballot_w64(any) == 0)
-            continue;
-#pragma unroll
-        for (int u = 0; u < kLvT; u++)
-        {
-            const int v = min(v0 + u * nthr, n - 1);
-#pragma unroll
-            for (int e = 0; e < kLvE; e++)
-                iv[u][e] = want[u] && e < ic[u] ? g_in_e[v * kMaxEdges + e] : SizeT(0);
-        }
-#pragma unroll
-        for (int u = 0; u < kLvT; u++)
-        {
-            nc[u]      = 0;
-            cand[u][0] = cand[u][1] = cand[u][2] = 0;
-#pragma unroll
-            for (int e = 0; e < kLvE; e++)
-            {
-                const int p = int(iv[u][e]);
-                if (want[u] && e < ic[u] && int(word[p] >> 16) == lvl[u] - 1)
-                {
-                    // (selects, not cand[u][nc[u]]: a runtime index would put
-                    // the array in scratch memory)
-                    cand[u][0] = nc[u] == 0 ? p : cand[u][0];
-                    cand[u][1] = nc[u] == 1 ? p : cand[u][1];
-                    cand[u][2] = nc[u] == 2 ? p : cand[u][2];
-                    nc[u]++;
-                }
-            }
-            want[u] = want[u] && nc[u] <= 3;
-#pragma unroll
-            for (int k = 0; k < 3; k++)
-            {
-                const bool live = want[u] && k < nc[u];
-                oc[u][k]        = live ? int(g_out_cnt[cand[u][k]]) : 0;
-#pragma unroll
-                for (int e = 0; e < kLvE; e++)
-                    ov[u][k][e] = live ? g_out_e[cand[u][k] * kMaxEdges + e] : SizeT(0);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kLvT; u++)
-        {
-            if (!want[u])
-                continue;
-            const int v = v0 + u * nthr;
-            uint32_t ent[3];
-#pragma unroll
-            for (int k = 0; k < 3; k++)
-            {
-                int slot = 0;
-                if (k < nc[u])
-                {
-#pragma unroll
-                    for (int e = 0; e < kLvE; e++)
-                        slot = (e < oc[u][k] && int(ov[u][k][e]) == v) ? e : slot;
-                    for (int e = kLvE; e < oc[u][k]; e++)
-                        if (int(g_out_e[cand[u][k] * kMaxEdges + e]) == v)
-                            slot = e;
-                }
-                ent[k] = k < nc[u] ? (uint32_t(cand[u][k]) | (uint32_t(slot) << 16)) : 0xffffffffu;
-            }
-            const int idx =
-                __hip_atomic_fetch_add(&ctl[20], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (idx < kt)
-            {
-                ctab[4 * idx]     = ent[0];
-                ctab[4 * idx + 1] = ent[1];
-                ctab[4 * idx + 2] = ent[2];
-                cc[v]             = uint16_t(idx);
-                meta[v]           = uint8_t(0xc0 | 63);
-            }
-        }
-    }
     __syncthreads();
     lap(5);
     // 3b. runs of multi-node levels, one lane per run.  The key of a member
@@ -2155,30 +2069,11 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
         if (ll == 0)
             return v;
         int par = c, slot = m & 63;
-        if ((m & 0x7f) == 0x40 + 63)
+        if (m & 0x40)
         {
-            // several predecessors one level below, from the table: the one
-            // placed last
-            GWAMD_LDS const uint32_t* ent = ctab + 4 * c;
-            par                           = -1;
-            slot                          = 0;
-            int bp                        = -1;
-#pragma unroll
-            for (int k = 0; k < 3; k++)
-            {
-                const uint32_t x = ent[k];
-                if (x != 0xffffffffu && int(cc[x & 0xffffu]) > bp)
-                {
-                    bp   = cc[x & 0xffffu];
-                    par  = int(x & 0xffffu);
-                    slot = int(x >> 16);
-                }
-            }
-        }
-        else if (m & 0x40)
-        {
-            // not in the table (more candidates or edges than it keeps): the
-            // in-list and the parent's out-list from HBM
+            // several predecessors one level below (about one member of a
+            // multi-node level in sixty): the one placed last, from the
+            // in-list and the parent's out-list in HBM
             const int ic = m & 63;
             par          = -1;
             int bp       = -1;
@@ -2200,37 +2095,51 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
         return ((int(cc[par]) - plo) << 6) | slot;
     };
     bool fail = false;
+    // (code size matters as much as latency here: the scan below unrolls
+    // only its loads, and the run loop exists once, so the section stays in
+    // the instruction cache)
     constexpr int kLvS = 8; // levels whose bounds are loaded together by the scan
     constexpr int kLvM = 4; // members of a level kept in registers
     for (int l0 = tid; l0 < n; l0 += kLvS * nthr)
     {
-        uint32_t wl[kLvS], wp[kLvS], wq[kLvS];
-#pragma unroll
-        for (int u = 0; u < kLvS; u++)
+        uint32_t starts = 0;
         {
-            const int l = min(l0 + u * nthr, n - 1);
-            wl[u]       = word[l];
-            wp[u]       = l > 0 ? word[l - 1] : 0u;
-            wq[u]       = l > 1 ? word[l - 2] : 0u;
+            uint32_t wl[kLvS], wp[kLvS], wq[kLvS];
+#pragma unroll
+            for (int u = 0; u < kLvS; u++)
+            {
+                const int l = min(l0 + u * nthr, n - 1);
+                wl[u]       = word[l];
+                wp[u]       = l > 0 ? word[l - 1] : 0u;
+                wq[u]       = l > 1 ? word[l - 2] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kLvS; u++)
+            {
+                const int l  = l0 + u * nthr;
+                const int lo = l > 0 ? int(wp[u] & 0xffffu) : 0;
+                const int le = int(wl[u] & 0xffffu);
+                const int pl = l > 1 ? int(wq[u] & 0xffffu) : 0;
+                if (l < n && le - lo > 1 && (l == 0 || lo - pl <= 1))
+                    starts |= 1u << u;
+            }
         }
-#pragma unroll
-        for (int u = 0; u < kLvS; u++)
+        while (starts)
         {
-            const int l = l0 + u * nthr;
-            int lo      = l > 0 ? int(wp[u] & 0xffffu) : 0;
-            int le      = int(wl[u] & 0xffffu);
-            const int pl = l > 1 ? int(wq[u] & 0xffffu) : 0;
-            if (l >= n || le - lo <= 1 || (l > 0 && lo - pl > 1))
-                continue;
-            int plo = l > 0 ? pl : 0;
+            const int l = l0 + __builtin_ctz(starts) * nthr;
+            starts &= starts - 1;
+            int lo  = lv_off(l), le = lv_end(l);
+            int plo = l > 0 ? lv_off(l - 1) : 0;
             for (int ll = l;;)
             {
                 const int m = le - lo;
-                if (m <= kLvM)
+                // members, their records and parents' positions in registers,
+                // ranks by comparing the keys, when the level is small and no
+                // member has several candidate parents
+                int v[kLvM], mt[kLvM], c[kLvM];
+                bool small = m <= kLvM && ll > 0;
+                if (small)
                 {
-                    // members, their records and parents' positions in
-                    // registers; ranks by comparing the keys
-                    int v[kLvM], mt[kLvM], c[kLvM], key[kLvM];
 #pragma unroll
                     for (int k = 0; k < kLvM; k++)
                         v[k] = bkt[lo + min(k, m - 1)];
@@ -2239,14 +2148,15 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
                     {
                         mt[k] = meta[v[k]];
                         c[k]  = cc[v[k]];
+                        small = small && (mt[k] & 0x40) == 0;
                     }
+                }
+                if (small)
+                {
+                    int key[kLvM];
 #pragma unroll
                     for (int k = 0; k < kLvM; k++)
-                        key[k] = (ll == 0 || (mt[k] & 0x40)) ? -1 : (((int(cc[c[k]]) - plo) << 6) | (mt[k] & 63));
-#pragma unroll
-                    for (int k = 0; k < kLvM; k++)
-                        if (key[k] < 0 && k < m)
-                            key[k] = key_of(v[k], ll, plo, mt[k], c[k]);
+                        key[k] = ((int(cc[c[k]]) - plo) << 6) | (mt[k] & 63);
 #pragma unroll
                     for (int k = 0; k < kLvM; k++)
                         fail = fail || (k < m && key[k] >= (1024 << 6));
@@ -2263,28 +2173,28 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
                 }
                 else
                 {
-                    // wide level: keys in place of c(v), ranks through LDS
+                    // keys in place of c(v), ranks through LDS
                     for (int i = lo; i < le; i++)
                     {
-                        const int v   = bkt[i];
-                        const int key = key_of(v, ll, plo, meta[v], cc[v]);
+                        const int vv  = bkt[i];
+                        const int key = key_of(vv, ll, plo, meta[vv], cc[vv]);
                         fail          = fail || key >= (1024 << 6);
-                        cc[v]         = uint16_t(key);
+                        cc[vv]        = uint16_t(key);
                     }
                     fail = fail || m > 255;
                     for (int i = lo; i < le; i++)
                     {
-                        const int v = bkt[i];
-                        const int k = cc[v];
-                        int rank    = 0;
+                        const int vv = bkt[i];
+                        const int k  = cc[vv];
+                        int rank     = 0;
                         for (int j = lo; j < le; j++)
                             rank += int(cc[bkt[j]]) < k ? 1 : 0;
-                        meta[v] = uint8_t(rank);
+                        meta[vv] = uint8_t(rank);
                     }
                     for (int i = lo; i < le; i++)
                     {
-                        const int v = bkt[i];
-                        cc[v]       = uint16_t(lo + meta[v]);
+                        const int vv = bkt[i];
+                        cc[vv]       = uint16_t(lo + meta[vv]);
                     }
                 }
                 ll++;

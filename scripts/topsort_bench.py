@@ -63,7 +63,7 @@ def main():
               hint.ctypes.data, order.ctypes.data, threads, scratch, res.ctypes.data, 0, C.byref(ms), None)
         res = np.zeros(n, np.int32)
         ms = C.c_double()
-        prof = np.zeros(8, np.uint64)
+        prof = np.zeros(10, np.uint64)
         hint_in = hint.copy()
         rc = f(bits, n, len(order), n_hint, in_cnt.ctypes.data, in_e.ctypes.data, out_cnt.ctypes.data,
                out_e.ctypes.data, hint_in.ctypes.data, order.ctypes.data, threads, scratch, res.ctypes.data, reps,
@@ -74,9 +74,10 @@ def main():
         if prof.any():
             rounds = int(prof[7]) // 1000000000
             prof[7] = int(prof[7]) % 1000000000
-            for name, v in zip(SECTIONS, prof):
+            for name, v in zip(SECTIONS, prof[:8]):
                 print("   %-28s %9.0f cycles" % (name, float(v) / (reps + 0)))
-            print("   jump rounds per sort %.1f" % (rounds / reps))
+            print("   jump rounds per sort %.1f, anchors %.0f, iterations %.1f" % (rounds / reps, prof[8] / reps,
+                                                                               prof[9] / reps))
 
 
 if __name__ == "__main__":
