@@ -1169,16 +1169,16 @@ __device__ int traceback_codes(WinGraph<SizeT> g, const RowProg& P, int V, int L
 #include "poa_fwd_w.hpp"
 
 // LDS-resident POA kernel: one workgroup of NW waves per window.  The forward
-// pass and the traceback tile loads use every wave; the serial phases (graph
-// update, topological sort, consensus, MSA) run on wave 0 while the other
-// waves wait at the next barrier.  W: 32-bit scores (nw_forward_lds_w, the
+// pass, the traceback tile loads and the level-keyed topological sort use
+// every wave; the serial phases (graph update, consensus, MSA) run on wave 0
+// while the other waves wait at the next barrier.  W: 32-bit scores (nw_forward_lds_w, the
 // reference's use32bitScore batches), else 16-bit.  Two waves per window
-// (config B: four windows per CU, two waves per SIMD) are held to 256
-// registers (HIP's second launch bound is the waves per SIMD), so the
-// allocation of the rest of the kernel cannot push it to one wave per SIMD
-// (half the windows resident).
+// (config B: four windows per CU, two waves per SIMD) need the kernel within
+// 256 registers; it is (252 with the per-kernel level sort instance), and a
+// second launch bound of 2 to force it costs config B 4% (the traceback
+// phase 5.8 -> 8.1 ms per window, same traceback code), so it is not set.
 template <bool MSA, int CPL, int NW, bool W>
-__global__ void __launch_bounds__(kWave * NW, W ? (NW >= 8 ? 2 : 1) : (NW >= 4 ? 4 : (NW == 2 ? 2 : 1)))
+__global__ void __launch_bounds__(kWave * NW, W ? (NW >= 8 ? 2 : 1) : (NW >= 4 ? 2 : 1))
     poa_window_kernel_lds(Buffers b, Dims d, Scores sc)
 {
     using SizeT  = int16_t;

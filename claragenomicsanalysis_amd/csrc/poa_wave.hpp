@@ -1624,8 +1624,8 @@ __device__ GWAMD_TS_ATTR bool topsort_levels(WinGraph<SizeT> g, int n, int n_pre
     lap(0);
     int r   = 0; // flag generation: slot r & 1 holds r when some thread raised it
     bool ok = false;
-    int rounds_total = 0;
-    int it_done      = 0;
+    [[maybe_unused]] int rounds_total = 0; // profile counters (GWAMD_TOPSORT_PROFILE)
+    [[maybe_unused]] int it_done      = 0;
     for (int it = 0; it < kLvIters; it++)
     {
         it_done = it + 1;
