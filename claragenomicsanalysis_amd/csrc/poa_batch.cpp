@@ -741,14 +741,16 @@ public:
     // (GWAMD_TOPSORT_RING=1, ring-mode parity tests); bit 1 keeps the LDS
     // kernel on the round-3 forward pass (GWAMD_POA_FWD=v1, A/B runs); bit 2
     // keeps the LDS and banded kernels on the FIFO Kahn sort instead of the
-    // level-keyed one (GWAMD_TOPSORT=fifo, cross-check tests and A/B runs)
+    // level-keyed one (GWAMD_TOPSORT=fifo, cross-check tests and A/B runs);
+    // bit 3 keeps the MSA's racon sort on the round-5 DFS step (GWAMD_RACON=v1)
     static int diag_bits()
     {
         const char* r = gwamd::host::diag_env("GWAMD_TOPSORT_RING");
         const char* f = gwamd::host::diag_env("GWAMD_POA_FWD");
         const char* t = gwamd::host::diag_env("GWAMD_TOPSORT");
+        const char* d = gwamd::host::diag_env("GWAMD_RACON");
         return ((r && std::atoi(r) != 0) ? 1 : 0) | ((f && std::string(f) == "v1") ? 2 : 0) |
-               ((t && std::string(t) == "fifo") ? 4 : 0);
+               ((t && std::string(t) == "fifo") ? 4 : 0) | ((d && std::string(d) == "v1") ? 8 : 0);
     }
     static int tb_walk_bits()
     {

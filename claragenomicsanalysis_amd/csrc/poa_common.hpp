@@ -100,7 +100,8 @@ struct Dims
     int32_t band_ad;        // banded kernel: waves of the anti-diagonal forward pass (0: row-parallel pass)
     int32_t tb_rank;        // traceback move windows (TbWin): bit 0 pointer-doubling walk, bit 1 strips, bit 2 32 x 4 strips
     int32_t diag;           // diagnostic switches (GWAMD_DIAG=1 only): bit 0 Kahn sort queued words in a ring,
-                            // bit 1 LDS kernel on the round-3 forward pass
+                            // bit 1 LDS kernel on the round-3 forward pass, bit 2 FIFO Kahn sort,
+                            // bit 3 round-5 racon DFS step for the MSA
 };
 
 // LDS bytes of the pointer-doubling traceback walk (walk_window_ranked)

@@ -1579,8 +1579,140 @@ int topsort_levels_test(int n, int n_prev, int n_hint, const uint16_t* in_cnt, c
     return fin(ok);
 }
 
+// Test hook: the racon DFS sort (topsort_racon_lds) of one graph by one wave,
+// with the group heads in HBM (heads != nullptr: racon_dfs_csr) or the
+// round-5 step (heads == nullptr).
+template <typename SizeT>
+__global__ void __launch_bounds__(64) topsort_racon_test_kernel(WinGraph<SizeT> g, int n, int scratch, int32_t* heads,
+                                                               SizeT* mpos, int* out)
+{
+    extern __shared__ __align__(16) uint8_t lds[];
+    // a static word first, as in the kernels: the dynamic scratch then does
+    // not start at LDS address 0 (a null scratch pointer means "no scratch")
+    __shared__ int keep[4];
+    if (threadIdx.x < 4)
+        keep[threadIdx.x] = n;
+    __syncthreads();
+    int cols     = 0;
+    const bool r = topsort_racon_lds<SizeT>(g, n, (GWAMD_LDS uint8_t*)(lds), scratch, int(threadIdx.x), mpos, &cols,
+                                            heads);
+    if (threadIdx.x == 0)
+    {
+        out[0] = r && keep[3] == n ? 1 : 0;
+        out[1] = cols;
+    }
+}
+
+template <typename SizeT>
+int topsort_racon_test(int n, const uint16_t* in_cnt, const int32_t* in_e, const uint16_t* aln_cnt,
+                       const int32_t* aln, int scratch, int v1, int32_t* sorted, int32_t* mpos, int* ncols, int reps,
+                       double* ms)
+{
+    if (n <= 0 || n > 65535 || scratch < 0 || scratch > 163840 - 64)
+        return -2;
+    const size_t ne = size_t(n) * kMaxEdges, na = size_t(n) * kMaxAlignments;
+    std::vector<SizeT> ie(ne), al(na);
+    for (size_t i = 0; i < ne; i++)
+        ie[i] = SizeT(in_e[i]);
+    for (size_t i = 0; i < na; i++)
+        al[i] = SizeT(aln[i]);
+    uint16_t *d_ic = nullptr, *d_ac = nullptr;
+    SizeT *d_ie = nullptr, *d_al = nullptr, *d_sorted = nullptr, *d_pos = nullptr, *d_mpos = nullptr;
+    int32_t* d_heads = nullptr;
+    int* d_out       = nullptr;
+    auto fin         = [&](int r) {
+        (void)hipFree(d_ic);
+        (void)hipFree(d_ac);
+        (void)hipFree(d_ie);
+        (void)hipFree(d_al);
+        (void)hipFree(d_sorted);
+        (void)hipFree(d_pos);
+        (void)hipFree(d_mpos);
+        (void)hipFree(d_heads);
+        (void)hipFree(d_out);
+        return r;
+    };
+    if (hipMalloc(&d_ic, n * 2) || hipMalloc(&d_ac, n * 2) || hipMalloc(&d_ie, ne * sizeof(SizeT)) ||
+        hipMalloc(&d_al, na * sizeof(SizeT)) || hipMalloc(&d_sorted, n * sizeof(SizeT)) ||
+        hipMalloc(&d_pos, n * sizeof(SizeT)) || hipMalloc(&d_mpos, n * sizeof(SizeT)) ||
+        hipMalloc(&d_heads, n * sizeof(int32_t)) || hipMalloc(&d_out, 2 * sizeof(int)))
+        return fin(-1);
+    if (hipMemcpy(d_ic, in_cnt, n * 2, hipMemcpyHostToDevice) || hipMemcpy(d_ac, aln_cnt, n * 2, hipMemcpyHostToDevice) ||
+        hipMemcpy(d_ie, ie.data(), ne * sizeof(SizeT), hipMemcpyHostToDevice) ||
+        hipMemcpy(d_al, al.data(), na * sizeof(SizeT), hipMemcpyHostToDevice) ||
+        hipMemset(d_sorted, 0xff, n * sizeof(SizeT)) || hipMemset(d_mpos, 0xff, n * sizeof(SizeT)))
+        return fin(-1);
+    WinGraph<SizeT> g{};
+    g.in_cnt    = d_ic;
+    g.aln_cnt   = d_ac;
+    g.in_e      = d_ie;
+    g.aln       = d_al;
+    g.sorted    = d_sorted;
+    g.pos       = d_pos;
+    g.max_nodes = n;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&topsort_racon_test_kernel<SizeT>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, scratch))
+        return fin(-1);
+    int32_t* hp = v1 ? nullptr : d_heads;
+    hipLaunchKernelGGL(topsort_racon_test_kernel<SizeT>, dim3(1), dim3(64), size_t(scratch), 0, g, n, scratch, hp,
+                       d_mpos, d_out);
+    int out[2] = {0, 0};
+    if (hipGetLastError() || hipDeviceSynchronize() || hipMemcpy(out, d_out, sizeof(out), hipMemcpyDeviceToHost))
+        return fin(-1);
+    if (reps > 0)
+    {
+        hipEvent_t e0, e1;
+        if (hipEventCreate(&e0) || hipEventCreate(&e1))
+            return fin(-1);
+        (void)hipEventRecord(e0, 0);
+        for (int k = 0; k < reps; k++)
+            hipLaunchKernelGGL(topsort_racon_test_kernel<SizeT>, dim3(1), dim3(64), size_t(scratch), 0, g, n,
+                               scratch, hp, d_mpos, d_out);
+        (void)hipEventRecord(e1, 0);
+        float t = 0.f;
+        if (hipEventSynchronize(e1) || hipEventElapsedTime(&t, e0, e1))
+            return fin(-1);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        if (ms)
+            *ms = double(t) / reps;
+    }
+    std::vector<SizeT> s(n), mp(n);
+    if (hipMemcpy(s.data(), d_sorted, n * sizeof(SizeT), hipMemcpyDeviceToHost) ||
+        hipMemcpy(mp.data(), d_mpos, n * sizeof(SizeT), hipMemcpyDeviceToHost))
+        return fin(-1);
+    for (int q = 0; q < n; q++)
+    {
+        sorted[q] = int32_t(s[q]);
+        if (mpos)
+            mpos[q] = int32_t(mp[q]);
+    }
+    if (ncols)
+        *ncols = out[1];
+    return fin(out[0]);
+}
+
 } // namespace poa
 } // namespace gwamd
+
+// Test hook (tests/test_poa_topsort.py, scripts/racon_bench.py): the racon
+// DFS sort (cudapoa_topsort.cuh:94-189) of one graph given as fixed-slot
+// in-edge and aligned-node arrays (kMaxEdges / kMaxAlignments slots), by one
+// wave with `scratch` bytes of LDS; v1 selects the round-5 DFS step.  Writes
+// the order, the MSA column of every node and the column count.  Returns 1
+// when the LDS sort ran, 0 when it declined (the kernels then run the HBM
+// sort), negative on a HIP error or bad arguments.  reps > 0: that many more
+// sorts, *ms = the mean time per sort.
+extern "C" int gwamd_internal_topsort_racon(int size_bits, int n, const uint16_t* in_cnt, const int32_t* in_e,
+                                            const uint16_t* aln_cnt, const int32_t* aln, int scratch, int v1,
+                                            int32_t* sorted, int32_t* mpos, int* ncols, int reps, double* ms)
+{
+    if (size_bits == 16)
+        return gwamd::poa::topsort_racon_test<int16_t>(n, in_cnt, in_e, aln_cnt, aln, scratch, v1, sorted, mpos,
+                                                       ncols, reps, ms);
+    return gwamd::poa::topsort_racon_test<int32_t>(n, in_cnt, in_e, aln_cnt, aln, scratch, v1, sorted, mpos, ncols,
+                                                   reps, ms);
+}
 
 // Test hook (tests/test_poa_topsort.py): topsort_levels of one graph given as
 // the reference's fixed-slot edge arrays (kMaxEdges slots per node), with the

@@ -71,7 +71,7 @@ struct PhaseTimer
 template <typename SizeT>
 __device__ __forceinline__ bool topsort_racon_lds(WinGraph<SizeT> g, int n, GWAMD_LDS uint8_t* scratch,
                                                   int scratch_bytes, int lane, SizeT* mpos = nullptr,
-                                                  int* ncols = nullptr);
+                                                  int* ncols = nullptr, int32_t* heads = nullptr);
 
 // Consensus and/or MSA of one finished window (cudapoa_generate_consensus.cuh:
 // 279-347, cudapoa_generate_msa.cuh:121-224).  scratch: free LDS of the
@@ -139,7 +139,8 @@ __device__ __forceinline__ void finish_window(const Buffers& b, const Dims& d, i
         int lds_cols        = 0;
         olap(0);
         const bool lds_done = graph_status == kSuccess && nseq > 0 &&
-                              topsort_racon_lds<SizeT>(g, node_count, scratch, scratch_bytes, lane, cpred, &lds_cols);
+                              topsort_racon_lds<SizeT>(g, node_count, scratch, scratch_bytes, lane, cpred, &lds_cols,
+                                                       (d.diag & 8) ? nullptr : cscore);
         olap(1);
         if (lane == 0)
         {
@@ -944,10 +945,210 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
 // entries u16, predecessors then aligned nodes), so a DFS step reads no HBM.
 constexpr int kRaconCsrStack = 4096;
 
+// The DFS of topsort_racon_lds over the LDS CSR copy, arranged so that a step
+// waits on as few dependent LDS round trips as the order allows:
+//  * a first visit reads the node's list (predecessors, then aligned nodes
+//    while its check flag is set) one entry per lane, then the marks and list
+//    words of all entries at once; the pushed entries are the entries whose
+//    mark is not 2, in list order (cudapoa_topsort.cuh:134-158), and the new
+//    top's mark and word come from the lane that read them;
+//  * a node found again on top with mark 1 is emitted without re-reading its
+//    lists: everything pushed above it has been popped, and entries are popped
+//    only when done, so all its predecessors (and the aligned nodes it pushed)
+//    are done, which is what the reference's second scan establishes;
+//  * a pop reads the popped node's mark and word together with the stack
+//    entry below it;
+//  * the outer loop over node ids (cudapoa_topsort.cuh:117-126) scans the
+//    marks 64 at a time;
+//  * an emitted group (cudapoa_topsort.cuh:160-175) is recorded as its head
+//    node in heads[] (HBM); the order and columns are expanded from the heads
+//    after the DFS, in parallel.
+// Returns false (partial output, nothing to trust) when the stack would
+// outgrow cap entries.
+template <typename SizeT>
+__device__ __forceinline__ bool racon_dfs_csr(WinGraph<SizeT> g, int n, GWAMD_LDS uint8_t* marks,
+                                              GWAMD_LDS uint32_t* info, GWAMD_LDS uint16_t* lists,
+                                              GWAMD_LDS uint16_t* stack, int cap, int lane, int32_t* heads_,
+                                              SizeT* mpos, int* ncols)
+{
+    GWAMD_GLB int32_t* heads  = (GWAMD_GLB int32_t*)(heads_);
+    const uint64_t lt         = (uint64_t(1) << lane) - 1;
+    int kq                    = 0; // emitted groups
+    int v0                    = 0;
+    while (true)
+    {
+        // next node id whose mark is 0 (the outer loop of the reference)
+        int id = -1, m = 0;
+        uint32_t w = 0;
+        for (; v0 < n; v0 += kWave)
+        {
+            // (reads at clamped addresses, then selects: no divergent branch
+            // between the loads and their wait)
+            const int v       = v0 + lane;
+            const int vc      = v < n ? v : 0;
+            const int mr      = int(marks[vc]);
+            const uint32_t iw = info[vc];
+            const int mk      = v < n ? mr : 2;
+            const uint64_t bf = __builtin_amdgcn_ballot_w64((mk & 3) == 0);
+            if (bf)
+            {
+                const int l = __builtin_ctzll(bf);
+                id          = v0 + l;
+                m           = __builtin_amdgcn_readlane(mk, l);
+                w           = uint32_t(__builtin_amdgcn_readlane(int(iw), l));
+                break;
+            }
+        }
+        if (id < 0)
+            break;
+        v0        = id + 1;
+        int top   = 0;
+        int below = 0; // stack[top - 1] when top > 0
+        if (lane == 0)
+            stack[0] = uint16_t(id);
+        while (true)
+        {
+            const int mm = m & 3; // 0: first visit; 1: emit; 2: pop only
+            if (mm == 0)
+            {
+                const int ic  = int((w >> 20) & 63u);
+                const int cnt = ic + ((m & 4) ? int(w >> 26) : 0);
+                const int o   = int(w & 0xfffffu);
+                const int e0 = lane, e1 = lane + kWave;
+                const int l0r = int(lists[e0 < cnt ? o + e0 : 0]);
+                const int n0  = e0 < cnt ? l0r : 0;
+                const int k0r = int(marks[n0]);
+                const uint32_t w0 = info[n0];
+                const int k0      = e0 < cnt ? k0r : 2;
+                int n1 = 0, k1 = 2;
+                uint32_t w1 = 0;
+                if (cnt > kWave) // (more than 64 list entries: rare)
+                {
+                    n1 = e1 < cnt ? int(lists[o + e1]) : 0;
+                    k1 = e1 < cnt ? int(marks[n1]) : 2;
+                    w1 = info[n1];
+                }
+                const bool p0     = (k0 & 3) != 2;
+                const bool p1     = (k1 & 3) != 2;
+                const uint64_t b0 = __builtin_amdgcn_ballot_w64(p0);
+                const uint64_t b1 = __builtin_amdgcn_ballot_w64(p1);
+                const int c0 = __popcll(b0), c1 = __popcll(b1);
+                if (c0 + c1 != 0) // (else valid: emitted below)
+                {
+                    if (top + c0 + c1 >= cap)
+                        return false;
+                    if (p0)
+                    {
+                        stack[top + 1 + __popcll(b0 & lt)] = uint16_t(n0);
+                        if (e0 >= ic) // aligned node: check_aligned_nodes = false
+                            marks[n0] = uint8_t(k0 & 3);
+                    }
+                    if (p1)
+                    {
+                        stack[top + 1 + c0 + __popcll(b1 & lt)] = uint16_t(n1);
+                        if (e1 >= ic)
+                            marks[n1] = uint8_t(k1 & 3);
+                    }
+                    if (lane == 0)
+                        marks[id] = uint8_t((m & 4) | 1);
+                    // the last entry pushed is the new top, the one before it
+                    // (or this node) lies below it
+                    int nid, nm, ne;
+                    uint32_t nw;
+                    if (c1)
+                    {
+                        const int l = 63 - __builtin_clzll(b1);
+                        nid = __builtin_amdgcn_readlane(n1, l), nm = __builtin_amdgcn_readlane(k1, l);
+                        nw  = uint32_t(__builtin_amdgcn_readlane(int(w1), l));
+                        ne  = kWave + l;
+                        const uint64_t r1 = b1 & ~(uint64_t(1) << l);
+                        below = r1 ? __builtin_amdgcn_readlane(n1, 63 - __builtin_clzll(r1))
+                                   : (c0 ? __builtin_amdgcn_readlane(n0, 63 - __builtin_clzll(b0)) : id);
+                    }
+                    else
+                    {
+                        const int l = 63 - __builtin_clzll(b0);
+                        nid = __builtin_amdgcn_readlane(n0, l), nm = __builtin_amdgcn_readlane(k0, l);
+                        nw  = uint32_t(__builtin_amdgcn_readlane(int(w0), l));
+                        ne  = l;
+                        const uint64_t r0 = b0 & ~(uint64_t(1) << l);
+                        below = r0 ? __builtin_amdgcn_readlane(n0, 63 - __builtin_clzll(r0)) : id;
+                    }
+                    top += c0 + c1;
+                    id = nid, w = nw;
+                    m  = ne >= ic ? (nm & 3) : nm;
+                    continue;
+                }
+            }
+            if (mm != 2)
+            {
+                // valid (cudapoa_topsort.cuh:160-176): mark 2; the group is
+                // emitted when check_aligned_nodes is set
+                if (lane == 0)
+                {
+                    marks[id] = uint8_t((m & 4) | 2);
+                    if (m & 4)
+                        heads[kq] = id;
+                }
+                kq += (m & 4) ? 1 : 0;
+            }
+            top--;
+            if (top < 0)
+                break;
+            id = below;
+            // the popped node's mark and word, and the entry below it
+            const int mr      = int(marks[id]);
+            const uint32_t wr = info[id];
+            const int br      = top > 0 ? int(stack[top - 1]) : 0;
+            m                 = __builtin_amdgcn_readfirstlane(mr);
+            w                 = uint32_t(__builtin_amdgcn_readfirstlane(int(wr)));
+            below             = __builtin_amdgcn_readfirstlane(br);
+        }
+    }
+    // expansion: head i is column i; its group is the head then all its
+    // aligned nodes (cudapoa_topsort.cuh:165-174, getNodeIDToMSAPosDevice)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    wave_sync();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    GWAMD_GLB SizeT* sorted = (GWAMD_GLB SizeT*)(g.sorted);
+    GWAMD_GLB SizeT* pos    = (GWAMD_GLB SizeT*)(g.pos);
+    GWAMD_GLB SizeT* mp     = (GWAMD_GLB SizeT*)(mpos);
+    int kbase               = 0;
+    for (int c = 0; c < kq; c += kWave)
+    {
+        const int i       = c + lane;
+        const bool act    = i < kq;
+        const int h       = act ? int(heads[i]) : 0;
+        const uint32_t hw = act ? info[h] : 0u;
+        const int ic = int((hw >> 20) & 63u), ac = act ? int(hw >> 26) : 0, o = int(hw & 0xfffffu);
+        int tot           = 0;
+        const int k       = kbase + wave_excl_sum(act ? 1 + ac : 0, lane, tot);
+        if (act)
+        {
+            sorted[k] = SizeT(h);
+            pos[h]    = SizeT(k);
+            if (mp)
+                mp[h] = SizeT(i);
+            for (int a = 0; a < ac; a++)
+            {
+                const int al     = int(lists[o + ic + a]);
+                sorted[k + 1 + a] = SizeT(al);
+                pos[al]           = SizeT(k + 1 + a);
+                if (mp)
+                    mp[al] = SizeT(i);
+            }
+        }
+        kbase += tot;
+    }
+    if (ncols)
+        *ncols = kq;
+    return true;
+}
+
 template <typename SizeT, bool CSR>
 __device__ __forceinline__ bool topsort_racon_lds_impl(WinGraph<SizeT> g, int n, GWAMD_LDS uint8_t* scratch,
                                                        int scratch_bytes, int lane, SizeT* mpos, int* ncols,
-                                                       int list_total)
+                                                       int list_total, int32_t* heads)
 {
     g = as_global(g);
     n                 = uniform(n);
@@ -966,26 +1167,60 @@ __device__ __forceinline__ bool topsort_racon_lds_impl(WinGraph<SizeT> g, int n,
         marks[v] = 4; // mark 0, check_aligned_nodes = true
     if constexpr (CSR)
     {
+        // two 64-node chunks per step, the counts and the first kPreE / kPreA
+        // slots of every node loaded together (one HBM round trip per step;
+        // longer lists read the rest one entry at a time)
+        constexpr int kPreE = 8, kPreA = 4, kU = 2;
         int base = 0;
-        for (int v0 = 0; v0 < n; v0 += kWave)
+        for (int v0 = 0; v0 < n; v0 += kU * kWave)
         {
-            const int v  = v0 + lane;
-            const int ic = v < n ? int(g.in_cnt[v]) : 0;
-            const int ac = v < n ? int(g.aln_cnt[v]) : 0;
-            int total    = 0;
-            const int o  = base + wave_excl_sum(ic + ac, lane, total);
-            if (v < n)
+            int ic[kU], ac[kU], pe[kU][kPreE], pa[kU][kPreA];
+#pragma unroll
+            for (int u = 0; u < kU; u++)
             {
-                info[v] = uint32_t(o) | (uint32_t(ic) << 20) | (uint32_t(ac) << 26);
-                for (int e = 0; e < ic; e++)
-                    lists[o + e] = uint16_t(int(g.in_e[v * kMaxEdges + e]));
-                for (int e = 0; e < ac; e++)
-                    lists[o + ic + e] = uint16_t(int(g.aln[v * kMaxAlignments + e]));
+                const int v  = v0 + u * kWave + lane;
+                const int vr = v < n ? v : 0;
+                ic[u]        = v < n ? int(g.in_cnt[vr]) : 0;
+                ac[u]        = v < n ? int(g.aln_cnt[vr]) : 0;
+#pragma unroll
+                for (int e = 0; e < kPreE; e++)
+                    pe[u][e] = int(g.in_e[vr * kMaxEdges + e]);
+#pragma unroll
+                for (int e = 0; e < kPreA; e++)
+                    pa[u][e] = int(g.aln[vr * kMaxAlignments + e]);
             }
-            base += total;
+#pragma unroll
+            for (int u = 0; u < kU; u++)
+            {
+                const int v   = v0 + u * kWave + lane;
+                int total     = 0;
+                const int o   = base + wave_excl_sum(ic[u] + ac[u], lane, total);
+                base         += total;
+                if (v < n)
+                {
+                    info[v] = uint32_t(o) | (uint32_t(ic[u]) << 20) | (uint32_t(ac[u]) << 26);
+#pragma unroll
+                    for (int e = 0; e < kPreE; e++)
+                        if (e < ic[u])
+                            lists[o + e] = uint16_t(pe[u][e]);
+                    for (int e = kPreE; e < ic[u]; e++)
+                        lists[o + e] = uint16_t(int(g.in_e[v * kMaxEdges + e]));
+#pragma unroll
+                    for (int e = 0; e < kPreA; e++)
+                        if (e < ac[u])
+                            lists[o + ic[u] + e] = uint16_t(pa[u][e]);
+                    for (int e = kPreA; e < ac[u]; e++)
+                        lists[o + ic[u] + e] = uint16_t(int(g.aln[v * kMaxAlignments + e]));
+                }
+            }
         }
     }
     wave_sync();
+    if constexpr (CSR)
+    {
+        if (heads)
+            return racon_dfs_csr<SizeT>(g, n, marks, info, lists, stack, cap, lane, heads, mpos, ncols);
+    }
     int k = 0, col = 0;
     for (int v0 = 0; v0 < n; v0++)
     {
@@ -1097,7 +1332,8 @@ __device__ __forceinline__ bool topsort_racon_lds_impl(WinGraph<SizeT> g, int n,
 
 template <typename SizeT>
 __device__ __forceinline__ bool topsort_racon_lds(WinGraph<SizeT> g, int n, GWAMD_LDS uint8_t* scratch,
-                                                  int scratch_bytes, int lane, SizeT* mpos, int* ncols)
+                                                  int scratch_bytes, int lane, SizeT* mpos, int* ncols,
+                                                  int32_t* heads)
 {
     g = as_global(g);
     n = uniform(n);
@@ -1115,8 +1351,8 @@ __device__ __forceinline__ bool topsort_racon_lds(WinGraph<SizeT> g, int n, GWAM
     total = uniform(total);
     const int need = ((n + 15) & ~15) + n * 4 + ((total * 2 + 15) & ~15) + 2 * kRaconCsrStack;
     if (total < (1 << 20) && need <= scratch_bytes)
-        return topsort_racon_lds_impl<SizeT, true>(g, n, scratch, scratch_bytes, lane, mpos, ncols, total);
-    return topsort_racon_lds_impl<SizeT, false>(g, n, scratch, scratch_bytes, lane, mpos, ncols, 0);
+        return topsort_racon_lds_impl<SizeT, true>(g, n, scratch, scratch_bytes, lane, mpos, ncols, total, heads);
+    return topsort_racon_lds_impl<SizeT, false>(g, n, scratch, scratch_bytes, lane, mpos, ncols, 0, nullptr);
 }
 
 // SPOA_ACCURATE per-read sort (cudapoa_kernels.cuh:324-337): the LDS racon
@@ -1127,7 +1363,7 @@ __device__ __forceinline__ int topsort_racon_wave(WinGraph<SizeT> g, int n, int3
                                                   int lane, GWAMD_LDS uint8_t* scratch = nullptr,
                                                   int scratch_bytes = 0)
 {
-    if (topsort_racon_lds<SizeT>(g, n, scratch, scratch_bytes, lane))
+    if (topsort_racon_lds<SizeT>(g, n, scratch, scratch_bytes, lane, nullptr, nullptr, marks))
         return int(kSuccess);
     int ok = 1;
     if (lane == 0)

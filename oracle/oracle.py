@@ -12,6 +12,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
 MAX_EDGES = 50
+MAX_ALIGNMENTS = 50
 
 _lib = None
 
@@ -46,6 +47,10 @@ def _declare(L):
     L.oracle_set_spoa_accurate.argtypes = [C.c_int32]
     L.oracle_topsort.restype = None
     L.oracle_topsort.argtypes = [i32, vp, vp, vp, vp]
+    L.oracle_poa_window_graph.restype = C.c_int
+    L.oracle_poa_window_graph.argtypes = [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp]
+    L.oracle_topsort_racon.restype = C.c_int
+    L.oracle_topsort_racon.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp]
     L.oracle_nw.restype = C.c_int
     L.oracle_nw.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]
     L.oracle_add_alignment.restype = C.c_int
@@ -218,6 +223,47 @@ def topsort(outgoing):
     res = np.zeros(n, np.int32)
     lib().oracle_topsort(n, _p(in_cnt), _p(out_e), _p(out_cnt), _p(res))
     return res.tolist()
+
+
+def poa_window_graph(reads, gap=-8, mismatch=-6, match=8, banded=False, band_width=256, score_bits=16,
+                     max_nodes=None, max_consensus=None):
+    """The final graph of one window with its aligned-node lists: (status, n,
+    in_cnt, in_e, aln_cnt, aln), edges and aligned nodes in slot order
+    (MAX_EDGES / MAX_ALIGNMENTS slots per node)."""
+    reads = [r.encode() if isinstance(r, str) else bytes(r) for r in reads]
+    max_len = max([len(r) for r in reads] + [1])
+    if max_nodes is None:
+        max_nodes = ((3 * max_len + 3) // 4) * 4 if not banded else ((4 * max_len + 3) // 4) * 4
+    if max_consensus is None:
+        max_consensus = 2 * max_len
+    seqs = np.frombuffer(b"".join(reads) + b"\0" * (2 * band_width + 64), dtype=np.uint8).copy()
+    lens = np.array([len(r) for r in reads], dtype=np.int32)
+    wts = np.ones(max(len(seqs), 1), dtype=np.int8)
+    nn = np.zeros(1, np.int32)
+    in_cnt = np.zeros(max_nodes, np.uint16)
+    aln_cnt = np.zeros(max_nodes, np.uint16)
+    in_e = np.zeros(max_nodes * MAX_EDGES, np.int32)
+    aln = np.zeros(max_nodes * MAX_ALIGNMENTS, np.int32)
+    st = lib().oracle_poa_window_graph(_p(seqs), _p(lens), _p(wts), len(reads), gap, mismatch, match, int(banded),
+                                       band_width, score_bits, max_nodes, max_consensus, _p(nn), _p(in_cnt),
+                                       _p(in_e), _p(aln_cnt), _p(aln))
+    n = int(nn[0])
+    return (st, n, in_cnt[:n].copy(), in_e[:n * MAX_EDGES].copy(), aln_cnt[:n].copy(),
+            aln[:n * MAX_ALIGNMENTS].copy())
+
+
+def topsort_racon(n, in_cnt, in_e, aln_cnt, aln):
+    """racon DFS sort (cudapoa_topsort.cuh:94-189) of a graph in slot arrays:
+    (ok, order, node -> MSA column, column count)."""
+    in_cnt = np.ascontiguousarray(in_cnt, np.uint16)
+    aln_cnt = np.ascontiguousarray(aln_cnt, np.uint16)
+    in_e = np.ascontiguousarray(in_e, np.int32)
+    aln = np.ascontiguousarray(aln, np.int32)
+    order = np.zeros(max(n, 1), np.int32)
+    mpos = np.zeros(max(n, 1), np.int32)
+    cols = np.zeros(1, np.int32)
+    ok = lib().oracle_topsort_racon(n, _p(in_cnt), _p(in_e), _p(aln_cnt), _p(aln), _p(order), _p(mpos), _p(cols))
+    return ok == 1, order[:n].tolist(), mpos[:n].tolist(), int(cols[0])
 
 
 def edges_from_lists(outgoing, n):

@@ -1148,6 +1148,73 @@ int oracle_poa_batch(const uint8_t* seqs, const int64_t* seq_offsets, const int3
     return used;
 }
 
+// Final graph of one window with its aligned-node lists (tests of the racon
+// sort on real window graphs): node count, in-edges (kMaxEdges slots) and
+// aligned nodes (kMaxAlignments slots) in slot order.  Returns the status.
+int oracle_poa_window_graph(const uint8_t* seqs, const int32_t* lens, const int8_t* wts, int32_t nseq, int32_t gap,
+                            int32_t mismatch, int32_t match, int32_t banded, int32_t band_width, int32_t score_bits,
+                            int32_t max_nodes, int32_t max_consensus, int32_t* final_nodes, uint16_t* in_cnt,
+                            int32_t* in_e, uint16_t* aln_cnt, int32_t* aln)
+{
+    WindowParams P{gap, mismatch, match, banded, band_width, score_bits, 0, max_nodes, max_consensus, nseq,
+                   g_spoa_accurate};
+    Graph g;
+    WindowStats st{0, 0, 0};
+    int32_t clen = 0;
+    std::vector<uint8_t> cons(size_t(max_consensus) + 1);
+    std::vector<uint16_t> covg(size_t(max_consensus) + 1);
+    uint8_t rc   = run_window(P, seqs, lens, wts, nseq, cons.data(), covg.data(), &clen, nullptr, g, &st);
+    *final_nodes = g.node_count;
+    for (int v = 0; v < g.node_count && v < max_nodes; v++)
+    {
+        in_cnt[v]  = g.in_cnt[v];
+        aln_cnt[v] = g.aln_cnt[v];
+        for (int e = 0; e < kMaxEdges; e++)
+            in_e[v * kMaxEdges + e] = e < g.in_cnt[v] ? g.in_e[v * kMaxEdges + e] : 0;
+        for (int a = 0; a < kMaxAlignments; a++)
+            aln[v * kMaxAlignments + a] = a < g.aln_cnt[v] ? g.aln[v * kMaxAlignments + a] : 0;
+    }
+    return rc;
+}
+
+// topsort_racon (cudapoa_topsort.cuh:94-189) of a given graph; the MSA column
+// of every node (getNodeIDToMSAPosDevice, cudapoa_generate_msa.cuh:27-45) and
+// the column count.  Returns 1, or 0 when the DFS stack outgrows 4 x nodes.
+int oracle_topsort_racon(int32_t node_count, const uint16_t* in_cnt, const int32_t* in_e, const uint16_t* aln_cnt,
+                         const int32_t* aln, int32_t* sorted_out, int32_t* mpos_out, int32_t* ncols)
+{
+    Graph g;
+    g.init(std::max(node_count, 1), 1, false);
+    g.node_count = node_count;
+    for (int v = 0; v < node_count; v++)
+    {
+        g.in_cnt[v]  = in_cnt[v];
+        g.aln_cnt[v] = aln_cnt[v];
+        for (int e = 0; e < in_cnt[v]; e++)
+            g.in_e[v * kMaxEdges + e] = in_e[v * kMaxEdges + e];
+        for (int a = 0; a < aln_cnt[v]; a++)
+            g.aln[v * kMaxAlignments + a] = aln[v * kMaxAlignments + a];
+    }
+    if (!topsort_racon(g))
+        return 0;
+    int col = 0;
+    for (int r = 0; r < node_count; r++)
+    {
+        const int id  = g.sorted[r];
+        sorted_out[r] = id;
+        mpos_out[id]  = col;
+        for (int a = 0; a < g.aln_cnt[id]; a++)
+        {
+            ++r;
+            sorted_out[r]          = g.sorted[r];
+            mpos_out[g.sorted[r]] = col;
+        }
+        col++;
+    }
+    *ncols = col;
+    return 1;
+}
+
 // ---- single-kernel known-answer hooks (reference test kernels) ----------------
 // Graph inputs use the fixed-slot layout of the reference tests (50 slots).
 
