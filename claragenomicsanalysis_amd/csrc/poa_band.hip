@@ -1371,6 +1371,28 @@ __device__ __forceinline__ void band_window_ptrs(const Buffers& b, const Dims& d
     X.xl_cap = d.aux_xl_cap;
 }
 
+// LDS bytes and layout of the graph update's scratch in the work region
+__device__ __forceinline__ int band_add_bytes(int L, int V)
+{
+    const int ls = (L + 16 + 15) & ~15;
+    return 5 * ls + ((2 * (V + L + 16) + 15) & ~15) + 2 * ls;
+}
+
+__device__ __forceinline__ AddScratch band_add_scratch(GWAMD_LDS uint8_t* work, GWAMD_LDS uint8_t* shb, int L, int V)
+{
+    const int ls   = (L + 16 + 15) & ~15;
+    const int hoff = 5 * ls + ((2 * (V + L + 16) + 15) & ~15);
+    AddScratch AX;
+    AX.gid   = (GWAMD_LDS uint16_t*)(work);
+    AX.curr  = (GWAMD_LDS uint16_t*)(work + 2 * ls);
+    AX.kind  = work + 4 * ls;
+    AX.owner = (GWAMD_LDS uint16_t*)(work + 5 * ls);
+    AX.hit   = work + hoff;
+    AX.ohit  = work + hoff + ls;
+    AX.sh    = (GWAMD_LDS int*)(shb);
+    return AX;
+}
+
 // One window per workgroup.  Wave 0 runs the whole window; with the
 // anti-diagonal pass (d.band_ad) the workgroup has kAdMaxWaves waves and waves
 // 1.. only join the forward passes: wave 0 posts each pass in sh_job and both
@@ -1383,8 +1405,9 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
     __shared__ int sh_status;
     __shared__ int sh_len;
     __shared__ AdShared ad_sh;
-    __shared__ int sh_job[5]; // window, V, L, gradient bits, job kind (0 forward pass, 1 topological sort:
-                              // window, node count, hint count, previous node count)
+    __shared__ int sh_job[8]; // window, V, L, gradient bits, job kind (0 forward pass, 1 topological sort:
+                              // window, node count, hint count, previous node count; 2 graph update:
+                              // window, node count, alignment length, L, -, read index, V)
 
     __shared__ int sh_next;
     if (int(blockIdx.x) >= b.num_windows)
@@ -1423,6 +1446,26 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
                 topsort_levels<SizeT>(g, sh_job[1], sh_job[3], (GWAMD_LDS uint8_t*)(lds), d.lds_sh_off,
                                       int(threadIdx.x), int(blockDim.x),
                                       static_cast<SizeT*>(b.cpred) + slot * size_t(d.max_nodes) * 4, sh_job[2]);
+                __syncthreads(); // pass done
+                continue;
+            }
+            if (sh_job[4] == 2)
+            {
+                // the order-free passes of the graph update (every wave)
+                const WindowDesc wd = b.windows[w];
+                const int s         = sh_job[5];
+                const int L         = sh_job[3];
+                const int V         = sh_job[6];
+                int nc              = sh_job[1];
+                const size_t mn     = size_t(d.max_nodes);
+                uint16_t* ecov      = MSA ? b.edge_cov + w * mn * kMaxEdges * d.max_seqs : nullptr;
+                uint16_t* ecovc     = MSA ? b.edge_cov_cnt + w * mn * kMaxEdges : nullptr;
+                SizeT* seq_begin    = MSA ? static_cast<SizeT*>(b.seq_begin) + size_t(w) * d.max_seqs : nullptr;
+                AddScratch AX       = band_add_scratch(work, shb, L, V);
+                add_alignment_parallel_batched<SizeT, MSA, kBandAddAU>(
+                    g, nc, static_cast<SizeT*>(b.ag) + slot * d.aln_cap, static_cast<SizeT*>(b.ar) + slot * d.aln_cap,
+                    sh_job[2], L, lread, b.wts + b.seq_off[wd.first_seq + s], s, ecov, ecovc, seq_begin, d.max_seqs,
+                    AX, lane, nullptr, wave, nw);
                 __syncthreads(); // pass done
                 continue;
             }
@@ -1553,25 +1596,30 @@ __global__ void __launch_bounds__(kWave * kAdMaxWaves) poa_window_kernel_band(Bu
             }
             int nc = node_count;
             int rc = -1;
+            if (band_add_bytes(L, V) <= d.lds_work_bytes)
             {
-                // add-alignment scratch in the work region, sized for this read
-                auto a16             = [](int v) { return (v + 15) & ~15; };
-                const int ls         = a16(L + 16);
-                const int hoff       = 5 * ls + a16(2 * (V + L + 16));
-                const int need       = hoff + 2 * ls;
-                if (need <= d.lds_work_bytes)
+                // add-alignment scratch in the work region, sized for this read;
+                // with helper waves the order-free passes run on all of them
+                AddScratch AX = band_add_scratch(work, shb, L, V);
+                if (nw > 1)
                 {
-                    AddScratch AX;
-                    AX.gid   = (GWAMD_LDS uint16_t*)(work);
-                    AX.curr  = (GWAMD_LDS uint16_t*)(work + 2 * ls);
-                    AX.kind  = work + 4 * ls;
-                    AX.owner = (GWAMD_LDS uint16_t*)(work + 5 * ls);
-                    AX.hit   = work + hoff;
-                    AX.ohit  = work + hoff + ls;
-                    AX.sh    = (GWAMD_LDS int*)(shb);
-                    rc = add_alignment_parallel_batched<SizeT, MSA, kBandAddAU>(g, nc, ag, ar, alen, L, lread, wts_g, s, ecov, ecovc,
-                                                            seq_begin, d.max_seqs, AX, lane, addprof);
+                    if (lane == 0)
+                    {
+                        sh_job[0] = w;
+                        sh_job[1] = nc;
+                        sh_job[2] = alen;
+                        sh_job[3] = L;
+                        sh_job[4] = 2;
+                        sh_job[5] = s;
+                        sh_job[6] = V;
+                    }
+                    __syncthreads(); // pass posted
                 }
+                rc = add_alignment_parallel_batched<SizeT, MSA, kBandAddAU>(g, nc, ag, ar, alen, L, lread, wts_g, s,
+                                                                           ecov, ecovc, seq_begin, d.max_seqs, AX,
+                                                                           lane, addprof, 0, nw);
+                if (nw > 1)
+                    __syncthreads(); // pass done
             }
             if (rc < 0)
             {

@@ -564,14 +564,25 @@ __device__ __forceinline__ int add_alignment_parallel(WinGraph<SizeT> g, int& no
 // per position): used by the banded kernel, whose windows are long (config C:
 // 10 kb reads, 21 ms of adds per window before); the LDS full-alignment kernel
 // keeps the one-position form (the batched one raises its register count and
-// slows its forward pass).
+// slows its forward pass).  nwv > 1: the nwv waves of the workgroup run it
+// together (wave wv; every wave calls it with the same arguments): the
+// order-free passes split the read positions among the waves and meet at
+// workgroup barriers; the new-node numbering and the new nodes' writes stay
+// on wave 0.  The return value and node_count are wave 0's.
 template <typename SizeT, bool MSA, int kAU = 4>
 __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g, int& node_count, const SizeT* ag, const SizeT* ar,
                                       int alen, int L, const uint8_t* read, const int8_t* w, int s, uint16_t* ecov,
                                       uint16_t* ecov_cnt, SizeT* seq_begin, int max_seqs, const AddScratch& X,
-                                      int lane, uint64_t* prof = nullptr)
+                                      int lane, uint64_t* prof = nullptr, int wv = 0, int nwv = 1)
 {
     g = as_global(g);
+    auto bar = [&]() {
+        if (nwv > 1)
+            __syncthreads();
+        else
+            wave_sync();
+    };
+    const int step1 = nwv * kWave, stepA = nwv * kAU * kWave;
 #ifdef GWAMD_ADD_PROFILE
     uint64_t pt = now_ticks();
     auto lap = [&](int k) { const uint64_t t = now_ticks(); if (prof) prof[k] += t - pt; pt = t; };
@@ -580,9 +591,9 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
 #endif
     const int nc0 = node_count;
     int err       = INT_MAX; // first error in read order: (pos << 8) | status
-    if (lane == 0)
+    if (lane == 0 && wv == 0)
         X.sh[0] = 0;
-    for (int k0 = 0; k0 < alen; k0 += 4 * kWave)
+    for (int k0 = wv * 4 * kWave; k0 < alen; k0 += 4 * step1)
     {
         int rp[4], gv[4];
 #pragma unroll
@@ -597,12 +608,12 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
             if (rp[u] >= 0 && rp[u] < L)
                 X.gid[rp[u]] = uint16_t(gv[u] < 0 ? 0xffff : gv[u]);
     }
-    wave_sync();
+    bar();
     lap(0);
     // kinds and existing targets.  kAU positions per lane and pass, their
     // graph loads issued together (the graph is in HBM: one round trip per
     // dependent level instead of one per position)
-    for (int r0 = 0; r0 < L; r0 += kAU * kWave)
+    for (int r0 = wv * kAU * kWave; r0 < L; r0 += stepA)
     {
         int gid[kAU], kind[kAU], curr[kAU], na[kAU], gb[kAU];
         uint8_t rb[kAU];
@@ -665,11 +676,11 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
             }
         }
     }
-    wave_sync();
+    bar();
     lap(1);
-    // new node ids: prefix sum over new-node elements in read order
+    // new node ids: prefix sum over new-node elements in read order (wave 0)
     int nnew = 0;
-    for (int r0 = 0; r0 < L; r0 += kWave)
+    for (int r0 = 0; wv == 0 && r0 < L; r0 += kWave)
     {
         const int rp     = r0 + lane;
         const bool isnew = rp < L && X.kind[rp] >= 2;
@@ -684,24 +695,24 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
         }
         nnew += total;
     }
-    wave_sync();
+    bar();
     lap(2);
     // independence checks without atomics: every element claims its node (and,
     // for aligned hits / ring updates, its aligned group); after a barrier an
     // element that no longer owns a claimed node has a conflicting partner.
-    for (int rp = lane; rp < L; rp += kWave)
+    for (int rp = wv * kWave + lane; rp < L; rp += step1)
         X.owner[int(X.curr[rp])] = uint16_t(rp);
-    wave_sync();
+    bar();
     bool conflict = false;
-    for (int rp = lane; rp < L; rp += kWave)
+    for (int rp = wv * kWave + lane; rp < L; rp += step1)
         conflict |= int(X.owner[int(X.curr[rp])]) != rp;
-    wave_sync();
+    bar();
     lap(3);
     // aligned groups of the mismatching positions: claim every member, then
     // check the claims (kAU positions per lane, loads batched as above)
     for (int pass = 0; pass < 2; pass++)
     {
-        for (int r0 = 0; r0 < L; r0 += kAU * kWave)
+        for (int r0 = wv * kAU * kWave; r0 < L; r0 += stepA)
         {
             int gid[kAU], na[kAU];
 #pragma unroll
@@ -754,16 +765,16 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
                     }
             }
         }
-        wave_sync();
+        bar();
     }
     if (conflict)
         X.sh[0] = 1;
-    wave_sync();
+    bar();
     if (X.sh[0])
         return -1;
     lap(4);
     // edge existence and edge-limit errors (kAU positions per lane and pass)
-    for (int r0 = 1; r0 < L; r0 += kAU * kWave)
+    for (int r0 = 1 + wv * kAU * kWave; r0 < L; r0 += stepA)
     {
         int head[kAU], curr[kAU], kind[kAU], ic[kAU], oc[kAU], hitv[kAU], ohitv[kAU];
         bool exists[kAU];
@@ -847,17 +858,28 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
         }
     }
     err = -wave_max(-err); // wave-wide minimum
+    if (nwv > 1)
+    {
+        // workgroup minimum through one word per wave
+        if (lane == 0)
+            X.sh[2 + wv] = err;
+        __syncthreads();
+        for (int q = 0; q < nwv; q++)
+            err = min(err, int(X.sh[2 + q]));
+    }
     if (err != INT_MAX)
         return err & 0xff;
-    wave_sync();
+    bar();
     lap(5);
-    add_write_new_nodes<SizeT>(g, X, L, read, lane);
+    if (wv == 0)
+        add_write_new_nodes<SizeT>(g, X, L, read, lane);
+    bar();
     lap(6);
     // writes 2: the edge head -> curr and the coverage of curr.  Element rp
     // touches only curr's in-list and coverage and head's out-list (head =
     // element rp-1's curr), so the elements are independent; kAU per lane and
     // pass, with their loads issued together.
-    for (int r0 = 0; r0 < L; r0 += kAU * kWave)
+    for (int r0 = wv * kAU * kWave; r0 < L; r0 += stepA)
     {
         int curr[kAU], head[kAU], kind[kAU], wsum[kAU], ic[kAU], oc[kAU], cv[kAU], hit[kAU], ohit[kAU];
 #pragma unroll
@@ -924,7 +946,7 @@ __device__ __forceinline__ int add_alignment_parallel_batched(WinGraph<SizeT> g,
         }
     }
     node_count = nc0 + nnew;
-    wave_sync();
+    bar();
     lap(7);
     return kSuccess;
 }
