@@ -287,11 +287,8 @@ __global__ void __launch_bounds__(kWave * NWV) __attribute__((amdgpu_waves_per_e
         // global-typed: flat stores would hold every LDS wait of the sweep behind them
         GWAMD_GLB BandEntry* E =
             (GWAMD_GLB BandEntry*)(a.ws + size_t(a.spec_phase == 1 ? idx : int(blockIdx.x)) * size_t(a.ws_slot_bytes));
-        // launch 1 computes distances only: launch 2 recomputes the one band
-        // the doubling rule accepts, with its band matrix (storing the widest
-        // speculative band of every pair was 21x the algorithmic HBM writes
-        // of D_banded_64k)
-        const bool st_on = a.spec_phase != 1;
+        // launch 1 stores the band matrix of its last sweep only
+        const bool st_on = a.spec_phase != 1 || ks == K - 1;
         const char* q  = a.seqs + size_t(2 * idx) * a.stride;
         const char* tg = a.seqs + size_t(2 * idx + 1) * a.stride;
         const int Q    = uni(a.lens[2 * idx]);
@@ -385,6 +382,8 @@ __global__ void __launch_bounds__(kWave * NWV) __attribute__((amdgpu_waves_per_e
                         ++kk;
                         continue;
                     }
+                    if (kk == K - 1)
+                        break; // accepted, and its band matrix is in this pair's slot
                 }
             }
             // all NWV waves: several chunks with their state in LDS; half

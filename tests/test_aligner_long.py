@@ -134,9 +134,9 @@ def test_myers_banded_two_column_sweep(waves, monkeypatch):
 @pytest.mark.parametrize("waves", ["4", "8"])
 def test_myers_banded_run_ahead_sweeps(spec, waves, monkeypatch):
     # band doubling run ahead (few long pairs): launch 1 runs sweeps
-    # 0..spec-1 of every pair on their own workgroups (distances only),
-    # launch 2 skips the rejected ones, recomputes the accepted one with its
-    # band matrix and carries on doubling past them. Pairs needing 1 to 5
+    # 0..spec-1 of every pair on their own workgroups (distance only, the last
+    # one with its band matrix), launch 2 skips the rejected ones and the
+    # stored one and carries on doubling past them. Pairs needing 1 to 5
     # sweeps, and one whose band reaches the whole query early
     monkeypatch.setenv("GWAMD_BAND_SPEC", spec)
     monkeypatch.setenv("GWAMD_BAND_WAVES", waves)
