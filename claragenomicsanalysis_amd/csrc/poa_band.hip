@@ -525,8 +525,12 @@ __device__ __forceinline__ int band_read_byte(const ReadBytesT<CPL>& rb, int c)
         return int((rb.h[c / 2] >> (8 * (c & 1))) & 0xffu);
 }
 
+// Out of line (round 6): with the level sort and the multi-wave graph update
+// in the kernel, the inlined pass's register allocation cost B_banded's
+// forward 52 -> 64 ms per window; its own function keeps its own allocation,
+// as band_forward_ad's does
 template <typename ScoreT, typename SizeT, int CPL>
-__device__ __forceinline__ int band_forward(WinGraph<SizeT> g, BandAux X, int V, GWAMD_LDS const uint8_t* read, int L,
+__device__ __noinline__ int band_forward(WinGraph<SizeT> g, BandAux X, int V, GWAMD_LDS const uint8_t* read, int L,
                             const Band& B, const Scores sc, GWAMD_LDS ScoreT* ring, GWAMD_LDS uint32_t* stage,
                             ScoreT* spill, int rowsz, int lane, BandProf& bp)
 {
